@@ -1,0 +1,531 @@
+// PyTorch dispatcher registration for the replicann gfx950 kernels.
+//
+// Host-only translation unit: validates shapes/dtypes, allocates outputs with
+// the caching allocator, picks the current HIP stream and calls the extern "C"
+// launchers compiled from csrc/kernels/*.hip.  Ops are registered under
+// torch.ops.replicann.* for the CUDA (= HIP on ROCm) dispatch key only: there is
+// no CPU kernel here — CPU tensors never reach these ops (ATen path in Python).
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include <cstdint>
+#include <optional>
+#include <tuple>
+#include <vector>
+
+using at::Tensor;
+using c10::optional;
+
+extern "C" {
+void rn_act_fwd(const void*, void*, long, int, hipStream_t);
+void rn_act_bwd(const void*, const void*, void*, long, int, hipStream_t);
+void rn_dropout(const void*, void*, long, float, uint64_t, hipStream_t);
+void rn_add(const void*, const void*, void*, long, int, hipStream_t);
+void rn_bias_act_grad(const void*, const void*, void*, float*, float*, int, int, int, int, hipStream_t);
+int rn_bias_act_grad_splits(int, int);
+int rn_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
+              hipStream_t);
+int rn_ln_bwd_waves(int);
+int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
+              float*, float*, int, int, hipStream_t);
+void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
+void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
+void rn_xent_fwd(const void*, const int64_t*, float*, float*, int, int, int, long, hipStream_t);
+void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
+void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, hipStream_t);
+void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
+int rn_norm_ws_floats();
+void rn_sumsq(const void*, long, int, float*, float*, hipStream_t);
+int rn_adamw(void*, float*, const void*, int, float*, float*, const uint8_t*, float*, long, float, float, float, float,
+             float, float, float, float, float, hipStream_t);
+void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, long, float, float, float, int, int, float,
+            float, hipStream_t);
+long rn_gemm_ws_floats(int, int, int);
+int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, float*, int, int, int, long, long, long,
+            int, int, int, int, int, int, hipStream_t);
+int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
+                int, int, float, int, float, uint64_t, hipStream_t);
+int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
+                void*, void*, void*, float*, float*, float*, const long*, int, int, int, int, int, float, int, float,
+                uint64_t, hipStream_t);
+int rn_attn_is_fast(int);
+void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+void rn_maxpool_fwd(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+void rn_maxpool_bwd(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int,
+                    hipStream_t);
+void rn_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
+void rn_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
+long rn_bn_ws_floats(int, int);
+void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, float*, float*, float*, int, int, float,
+               float, int, hipStream_t);
+void rn_bn_eval(const void*, const void*, const void*, const float*, const float*, void*, int, int, float, int,
+                hipStream_t);
+void rn_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
+               float*, int, int, int, hipStream_t);
+}
+
+namespace {
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16, got ", (t).scalar_type())
+#define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define GUARD(t) c10::hip::HIPGuardMasqueradingAsCUDA _guard((t).device())
+
+const void* optr(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------ GEMM
+Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<Tensor>& bias,
+            const optional<Tensor>& residual, int64_t act, const optional<Tensor>& preact, const optional<Tensor>& out,
+            bool accumulate, int64_t split_k, bool out_fp32) {
+    CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(b);
+    GUARD(a);
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm expects 2-D operands");
+    TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm operands need unit inner stride");
+    const int64_t M = ta ? a.size(1) : a.size(0);
+    const int64_t K = ta ? a.size(0) : a.size(1);
+    const int64_t Kb = tb ? b.size(1) : b.size(0);
+    const int64_t N = tb ? b.size(0) : b.size(1);
+    TORCH_CHECK(K == Kb, "gemm inner dims differ: ", K, " vs ", Kb);
+    Tensor c;
+    if (out && out->defined()) {
+        c = *out;
+        TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "gemm out shape mismatch");
+        out_fp32 = c.scalar_type() == at::kFloat;
+    } else {
+        c = at::empty({M, N}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
+    }
+    if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
+    if (residual && residual->defined()) {
+        CHECK_BF16(*residual);
+        TORCH_CHECK(residual->size(0) == M && residual->size(1) == N && residual->stride(0) == c.stride(0) &&
+                    residual->stride(1) == 1, "residual must match the output layout");
+    }
+    if (preact && preact->defined()) {
+        CHECK_BF16(*preact);
+        TORCH_CHECK(preact->size(0) == M && preact->size(1) == N && preact->stride(0) == c.stride(0));
+    }
+    if (M == 0 || N == 0) return c;
+    int split = (int)std::max<int64_t>(1, split_k);
+    Tensor ws;
+    if (split > 1) ws = at::empty({rn_gemm_ws_floats(M, N, split)}, a.options().dtype(at::kFloat));
+    // K must be a multiple of 8 (16-B rows); pad both operands with zeros otherwise
+    Tensor A = a, B = b;
+    int64_t Kp = K;
+    if (K % 8 != 0) {
+        Kp = (K + 7) / 8 * 8;
+        A = ta ? at::constant_pad_nd(a, {0, 0, 0, Kp - K}) : at::constant_pad_nd(a, {0, Kp - K});
+        B = tb ? at::constant_pad_nd(b, {0, Kp - K}) : at::constant_pad_nd(b, {0, 0, 0, Kp - K});
+    }
+    if (ta && (M % 8 != 0 || A.stride(0) % 8 != 0)) {  // M-contiguous A needs 16-B aligned rows
+        A = A.t().contiguous();
+        ta = false;
+    }
+    if (!tb && (N % 8 != 0 || B.stride(0) % 8 != 0)) {
+        B = B.t().contiguous();
+        tb = true;
+    }
+    if (!ta && A.stride(0) % 8 != 0) A = A.contiguous();
+    if (tb && B.stride(0) % 8 != 0) B = B.contiguous();
+    if (c.stride(0) % 4 != 0 && (bias || residual)) { /* epilogue handles unaligned via scalar path */ }
+    int rc = rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
+                     preact && preact->defined() ? preact->data_ptr() : nullptr, split > 1 ? ws.data_ptr<float>() : nullptr,
+                     (int)M, (int)N, (int)Kp, A.stride(0), B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32,
+                     accumulate, cur_stream());
+    TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
+    return c;
+}
+
+std::tuple<Tensor, Tensor> bias_act_grad(const Tensor& dy, const optional<Tensor>& h, int64_t act, bool want_bias) {
+    CHECK_CUDA(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
+    GUARD(dy);
+    const int M = dy.size(0), N = dy.size(1);
+    Tensor dh = act != 0 ? at::empty_like(dy) : dy;
+    Tensor db = at::empty({want_bias ? N : 0}, dy.options().dtype(at::kFloat));
+    Tensor part = at::empty({want_bias ? (int64_t)rn_bias_act_grad_splits(M, N) * N : 1}, dy.options().dtype(at::kFloat));
+    if (act != 0) { TORCH_CHECK(h && h->defined(), "activation grad needs the pre-activation"); CHECK_CONTIG(*h); }
+    if (M > 0)
+        rn_bias_act_grad(dy.data_ptr(), optr(h), dh.data_ptr(), want_bias ? db.data_ptr<float>() : nullptr,
+                         part.data_ptr<float>(), M, N, (int)act, want_bias, cur_stream());
+    else if (want_bias) db.zero_();
+    return {dh, db};
+}
+
+// ------------------------------------------------------------------ elementwise
+Tensor act_fwd(const Tensor& x, int64_t kind) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    Tensor y = at::empty_like(x);
+    rn_act_fwd(x.data_ptr(), y.data_ptr(), x.numel(), (int)kind, cur_stream());
+    return y;
+}
+Tensor act_bwd(const Tensor& dy, const Tensor& x, int64_t kind) {
+    CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); GUARD(dy);
+    Tensor dx = at::empty_like(dy);
+    rn_act_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), dy.numel(), (int)kind, cur_stream());
+    return dx;
+}
+Tensor dropout_fwd(const Tensor& x, double p, int64_t seed) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    Tensor y = at::empty_like(x);
+    rn_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint64_t)seed, cur_stream());
+    return y;
+}
+Tensor add_act(const Tensor& a, const Tensor& b, bool relu) {
+    CHECK_BF16(a); CHECK_CONTIG(a); CHECK_CONTIG(b); GUARD(a);
+    TORCH_CHECK(a.sizes() == b.sizes());
+    Tensor y = at::empty_like(a);
+    rn_add(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), relu, cur_stream());
+    return y;
+}
+
+// ------------------------------------------------------------------ softmax / xent
+Tensor softmax_fwd(const Tensor& x, double scale) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    Tensor y = at::empty_like(x);
+    if (x.numel()) rn_softmax_fwd(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), (float)scale, cur_stream());
+    return y;
+}
+Tensor softmax_bwd(const Tensor& dy, const Tensor& y, double scale) {
+    CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(y); GUARD(dy);
+    Tensor dx = at::empty_like(dy);
+    if (dy.numel()) rn_softmax_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), y.size(0), y.size(1), (float)scale, cur_stream());
+    return dx;
+}
+std::tuple<Tensor, Tensor> xent_fwd(const Tensor& logits, const Tensor& target, int64_t nvalid, int64_t ignore) {
+    CHECK_BF16(logits); CHECK_CONTIG(logits); GUARD(logits);
+    TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous());
+    const int M = logits.size(0), V = logits.size(1);
+    Tensor loss = at::empty({M}, logits.options().dtype(at::kFloat));
+    Tensor lse = at::empty({M}, logits.options().dtype(at::kFloat));
+    if (M) rn_xent_fwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), M, V,
+                       (int)nvalid, (long)ignore, cur_stream());
+    return {loss, lse};
+}
+void xent_bwd(const Tensor& logits, const Tensor& target, const Tensor& lse, const Tensor& gscale, const Tensor& grad,
+              int64_t nvalid, int64_t ignore) {
+    CHECK_BF16(logits); GUARD(logits);
+    TORCH_CHECK(gscale.scalar_type() == at::kFloat && gscale.is_cuda());
+    const int M = logits.size(0), V = logits.size(1);
+    if (M) rn_xent_bwd(logits.data_ptr(), target.data_ptr<int64_t>(), lse.data_ptr<float>(), gscale.data_ptr<float>(),
+                       grad.data_ptr(), M, V, (int)nvalid, (long)ignore, cur_stream());
+}
+
+// ------------------------------------------------------------------ layernorm
+std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const optional<Tensor>& r, const Tensor& w,
+                                                         const optional<Tensor>& b, double eps) {
+    CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); GUARD(x);
+    const int M = x.size(0), E = x.size(1);
+    Tensor y = at::empty_like(x);
+    Tensor h = (r && r->defined()) ? at::empty_like(x) : x;
+    Tensor mean = at::empty({M}, x.options().dtype(at::kFloat));
+    Tensor rstd = at::empty({M}, x.options().dtype(at::kFloat));
+    if (M) {
+        int rc = rn_ln_fwd(x.data_ptr(), optr(r), w.data_ptr(), optr(b), y.data_ptr(), h.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), M, E, (float)eps, cur_stream());
+        TORCH_CHECK(rc == 0, "layernorm: E must be a multiple of 8 and <= 8192, got ", E);
+    }
+    return {y, h, mean, rstd};
+}
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optional<Tensor>& gh, const Tensor& h,
+                                                 const Tensor& w, const Tensor& mean, const Tensor& rstd) {
+    CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(h); GUARD(dy);
+    const int M = dy.size(0), E = dy.size(1);
+    Tensor dx = at::empty_like(dy);
+    Tensor dw = at::empty({E}, dy.options().dtype(at::kFloat));
+    Tensor db = at::empty({E}, dy.options().dtype(at::kFloat));
+    const int W = rn_ln_bwd_waves(M);
+    Tensor part = at::empty({2 * (int64_t)W * E}, dy.options().dtype(at::kFloat));
+    if (M) {
+        int rc = rn_ln_bwd(dy.data_ptr(), optr(gh), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                           part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)W * E, M, E, cur_stream());
+        TORCH_CHECK(rc == 0, "layernorm_bwd: unsupported E=", E);
+    } else { dw.zero_(); db.zero_(); }
+    return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------ embedding
+Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const optional<Tensor>& wpe) {
+    CHECK_BF16(wte); CHECK_CONTIG(wte); GUARD(wte);
+    TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous());
+    const int E = wte.size(1);
+    TORCH_CHECK(E % 8 == 0, "embedding width must be a multiple of 8");
+    const int T = ids.dim() >= 2 ? ids.size(-1) : ids.numel();
+    const int rows = ids.numel();
+    if (wpe && wpe->defined()) TORCH_CHECK(wpe->size(0) >= T, "sequence longer than the position table");
+    auto shape = ids.sizes().vec();
+    shape.push_back(E);
+    Tensor x = at::empty(shape, wte.options());
+    if (rows) rn_emb_fwd(ids.data_ptr<int64_t>(), wte.data_ptr(), optr(wpe), x.data_ptr(), rows, T, E, cur_stream());
+    return x;
+}
+std::tuple<Tensor, Tensor> embedding_bwd(const Tensor& dx, const Tensor& ids, int64_t V, int64_t Tp) {
+    CHECK_BF16(dx); CHECK_CONTIG(dx); GUARD(dx);
+    const int E = dx.size(-1);
+    const int T = ids.dim() >= 2 ? ids.size(-1) : ids.numel();
+    const int B = ids.numel() / std::max(T, 1);
+    Tensor d32 = at::empty({V * E}, dx.options().dtype(at::kFloat));
+    Tensor dwte = at::empty({V, E}, dx.options());
+    Tensor dwpe = at::empty({Tp, E}, dx.options());
+    rn_emb_bwd(ids.data_ptr<int64_t>(), dx.data_ptr(), d32.data_ptr<float>(), dwte.data_ptr(), Tp ? dwpe.data_ptr() : nullptr,
+               B, T, (int)Tp, (int)V, E, cur_stream());
+    return {dwte, dwpe};
+}
+
+// ------------------------------------------------------------------ optimizers
+void sumsq(const Tensor& g, const Tensor& normbuf) {
+    CHECK_CONTIG(g); GUARD(g);
+    TORCH_CHECK(normbuf.scalar_type() == at::kFloat && normbuf.numel() >= 2);
+    Tensor part = at::empty({rn_norm_ws_floats()}, g.options().dtype(at::kFloat));
+    rn_sumsq(g.data_ptr(), g.numel(), g.scalar_type() == at::kBFloat16, part.data_ptr<float>(), normbuf.data_ptr<float>(),
+             cur_stream());
+}
+void adamw_step(const Tensor& p, const Tensor& master, const Tensor& g, const Tensor& m, const Tensor& v,
+                const Tensor& wdm, const Tensor& normbuf, double lr, double b1, double b2, double eps, double wd,
+                double bc1, double bc2, double gscale, double clip) {
+    CHECK_BF16(p); GUARD(p);
+    TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat);
+    TORCH_CHECK(p.numel() == master.numel() && p.numel() == g.numel() && wdm.numel() * 64 >= p.numel());
+    int rc = rn_adamw(p.data_ptr(), master.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16,
+                      m.data_ptr<float>(), v.data_ptr<float>(), wdm.data_ptr<uint8_t>(), normbuf.data_ptr<float>(),
+                      p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2,
+                      (float)gscale, (float)clip, cur_stream());
+    TORCH_CHECK(rc == 0, "adamw: flat buffer length must be a multiple of 8");
+}
+void sgd_step(const Tensor& p, const Tensor& master, const Tensor& g, const Tensor& buf, const Tensor& wdm,
+              const Tensor& normbuf, double lr, double mom, double wd, bool nesterov, bool first, double gscale,
+              double clip) {
+    CHECK_BF16(p); GUARD(p);
+    rn_sgd(p.data_ptr(), master.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16, buf.data_ptr<float>(),
+           wdm.data_ptr<uint8_t>(), normbuf.data_ptr<float>(), p.numel(), (float)lr, (float)mom, (float)wd, nesterov,
+           first, (float)gscale, (float)clip, cur_stream());
+}
+
+// ------------------------------------------------------------------ attention
+void strides_bth(const Tensor& t, std::vector<long>& s) {
+    TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "attention tensors must be (B, T, H, D) with unit D stride");
+    s.push_back(t.stride(0)); s.push_back(t.stride(1)); s.push_back(t.stride(2));
+}
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& bias,
+                                    double scale, bool causal, double p, int64_t seed) {
+    CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); GUARD(q);
+    const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3), Tk = k.size(1);
+    Tensor o = at::empty({B, Tq, H, D}, q.options());
+    Tensor lse = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
+    std::vector<long> s;
+    strides_bth(q, s); strides_bth(k, s); strides_bth(v, s); strides_bth(o, s);
+    int bias_b = 1;
+    if (bias && bias->defined()) {
+        TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->dim() == 3 && bias->is_contiguous());
+        bias_b = bias->size(0);
+    }
+    if (B * H * Tq == 0) return {o, lse};
+    int rc = rn_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                         bias && bias->defined() ? bias->data_ptr<float>() : nullptr, bias_b, s.data(), B, H, Tq, Tk, D,
+                         (float)scale, causal, (float)p, (uint64_t)seed, cur_stream());
+    TORCH_CHECK(rc == 0, "attention: unsupported shape D=", D, " Tk=", Tk);
+    return {o, lse};
+}
+void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                   const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
+                   const Tensor& dq, const Tensor& dk, const Tensor& dv) {
+    GUARD(q);
+    const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3), Tk = k.size(1);
+    std::vector<long> s;
+    for (const Tensor* t : {&q, &k, &v, &o, &dout, &dq, &dk, &dv}) strides_bth(*t, s);
+    Tensor delta = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
+    Tensor dk32, dv32;
+    if (!rn_attn_is_fast(D)) {
+        dk32 = at::zeros({B, Tk, H, D}, q.options().dtype(at::kFloat));
+        dv32 = at::zeros({B, Tk, H, D}, q.options().dtype(at::kFloat));
+    }
+    int bias_b = bias && bias->defined() ? bias->size(0) : 1;
+    if (B * H * Tq == 0) return;
+    int rc = rn_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                         bias && bias->defined() ? bias->data_ptr<float>() : nullptr, bias_b, dq.data_ptr(), dk.data_ptr(),
+                         dv.data_ptr(), delta.data_ptr<float>(), dk32.defined() ? dk32.data_ptr<float>() : nullptr,
+                         dv32.defined() ? dv32.data_ptr<float>() : nullptr, s.data(), B, H, Tq, Tk, D, (float)scale,
+                         causal, (float)p, (uint64_t)seed, cur_stream());
+    TORCH_CHECK(rc == 0, "attention backward: unsupported shape D=", D);
+}
+std::tuple<Tensor, Tensor, Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
+                                            const Tensor& o, const Tensor& lse, const optional<Tensor>& bias,
+                                            double scale, bool causal, double p, int64_t seed) {
+    Tensor dq = at::empty(q.sizes(), q.options());
+    Tensor dk = at::empty(k.sizes(), k.options());
+    Tensor dv = at::empty(v.sizes(), v.options());
+    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv);
+    return {dq, dk, dv};
+}
+void attn_bwd_out(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                  const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
+                  const Tensor& dq, const Tensor& dk, const Tensor& dv) {
+    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv);
+}
+
+// ------------------------------------------------------------------ conv / pool / bn
+Tensor im2col(const Tensor& x, int64_t KH, int64_t KW, int64_t S, int64_t P, int64_t Kp) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+    const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
+    Tensor cols = at::empty({(int64_t)N * OH * OW, Kp}, x.options());
+    rn_im2col(x.data_ptr(), cols.data_ptr(), N, H, W, C, KH, KW, S, P, OH, OW, Kp, cur_stream());
+    return cols;
+}
+Tensor col2im(const Tensor& dcols, int64_t N, int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S,
+              int64_t P, int64_t Kp) {
+    CHECK_BF16(dcols); CHECK_CONTIG(dcols); GUARD(dcols);
+    const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
+    Tensor dx = at::empty({N, H, W, C}, dcols.options());
+    rn_col2im(dcols.data_ptr(), dx.data_ptr(), N, H, W, C, KH, KW, S, P, OH, OW, Kp, cur_stream());
+    return dx;
+}
+Tensor maxpool_fwd(const Tensor& x, int64_t K, int64_t S, int64_t P) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+    const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+    Tensor y = at::empty({N, OH, OW, C}, x.options());
+    rn_maxpool_fwd(x.data_ptr(), y.data_ptr(), N, H, W, C, K, S, P, OH, OW, cur_stream());
+    return y;
+}
+Tensor maxpool_bwd(const Tensor& gy, const Tensor& x, const Tensor& y, int64_t K, int64_t S, int64_t P) {
+    GUARD(x);
+    const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+    Tensor dx = at::empty_like(x);
+    rn_maxpool_bwd(gy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), N, H, W, C, K, S, P, y.size(1), y.size(2),
+                   cur_stream());
+    return dx;
+}
+Tensor avgpool_fwd(const Tensor& x) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+    Tensor y = at::empty({N, C}, x.options());
+    rn_avgpool_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, cur_stream());
+    return y;
+}
+Tensor avgpool_bwd(const Tensor& gy, int64_t H, int64_t W) {
+    CHECK_BF16(gy); GUARD(gy);
+    const int N = gy.size(0), C = gy.size(1);
+    Tensor dx = at::empty({N, H, W, C}, gy.options());
+    rn_avgpool_bwd(gy.contiguous().data_ptr(), dx.data_ptr(), N, H * W, C, cur_stream());
+    return dx;
+}
+std::tuple<Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
+                                                 const Tensor& rmean, const Tensor& rvar, double mom, double eps,
+                                                 bool relu) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    TORCH_CHECK(rmean.scalar_type() == at::kFloat && rvar.scalar_type() == at::kFloat, "BN running stats must be fp32");
+    const int M = x.size(0), C = x.size(1);
+    Tensor y = at::empty_like(x);
+    Tensor mean = at::empty({C}, x.options().dtype(at::kFloat));
+    Tensor rstd = at::empty({C}, x.options().dtype(at::kFloat));
+    Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
+    rn_bn_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), y.data_ptr(),
+              mean.data_ptr<float>(), rstd.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)mom, (float)eps, relu,
+              cur_stream());
+    return {y, mean, rstd};
+}
+Tensor batchnorm_eval(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& rmean, const Tensor& rvar,
+                      double eps, bool relu) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    Tensor y = at::empty_like(x);
+    rn_bn_eval(x.data_ptr(), w.data_ptr(), b.data_ptr(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), y.data_ptr(),
+               x.size(0), x.size(1), (float)eps, relu, cur_stream());
+    return y;
+}
+std::tuple<Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor& x, const Tensor& y, const Tensor& w,
+                                                 const Tensor& mean, const Tensor& rstd, bool relu) {
+    CHECK_BF16(gy); CHECK_CONTIG(gy); GUARD(gy);
+    const int M = x.size(0), C = x.size(1);
+    Tensor dx = at::empty_like(x);
+    Tensor dw = at::empty({C}, x.options().dtype(at::kFloat));
+    Tensor db = at::empty({C}, x.options().dtype(at::kFloat));
+    Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
+    rn_bn_bwd(gy.data_ptr(), x.data_ptr(), y.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+              dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu, cur_stream());
+    return {dx, dw, db};
+}
+
+int64_t native_version() { return 1; }
+
+}  // namespace
+
+TORCH_LIBRARY(replicann, m) {
+    m.def("gemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, Tensor? residual, int act, Tensor? preact, "
+          "Tensor? out, bool accumulate, int split_k, bool out_fp32) -> Tensor");
+    m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias) -> (Tensor, Tensor)");
+    m.def("act_fwd(Tensor x, int kind) -> Tensor");
+    m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
+    m.def("dropout_fwd(Tensor x, float p, int seed) -> Tensor");
+    m.def("add_act(Tensor a, Tensor b, bool relu) -> Tensor");
+    m.def("softmax_fwd(Tensor x, float scale) -> Tensor");
+    m.def("softmax_bwd(Tensor dy, Tensor y, float scale) -> Tensor");
+    m.def("xent_fwd(Tensor logits, Tensor target, int nvalid, int ignore) -> (Tensor, Tensor)");
+    m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale, Tensor(a!) grad, int nvalid, int ignore) -> ()");
+    m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
+    m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
+    m.def("embedding_bwd(Tensor dx, Tensor ids, int V, int Tp) -> (Tensor, Tensor)");
+    m.def("sumsq(Tensor g, Tensor(a!) normbuf) -> ()");
+    m.def("adamw_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) m, Tensor(d!) v, Tensor wdm, Tensor(e!) normbuf, "
+          "float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, float clip) -> ()");
+    m.def("sgd_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) buf, Tensor wdm, Tensor(e!) normbuf, float lr, "
+          "float mom, float wd, bool nesterov, bool first, float gscale, float clip) -> ()");
+    m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? bias, float scale, bool causal, float p, int seed) -> (Tensor, Tensor)");
+    m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
+          "bool causal, float p, int seed) -> (Tensor, Tensor, Tensor)");
+    m.def("attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
+          "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+    m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
+    m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp) -> Tensor");
+    m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> Tensor");
+    m.def("maxpool_bwd(Tensor gy, Tensor x, Tensor y, int K, int S, int P) -> Tensor");
+    m.def("avgpool_fwd(Tensor x) -> Tensor");
+    m.def("avgpool_bwd(Tensor gy, int H, int W) -> Tensor");
+    m.def("batchnorm_fwd(Tensor x, Tensor w, Tensor b, Tensor(a!) rmean, Tensor(b!) rvar, float mom, float eps, bool relu) "
+          "-> (Tensor, Tensor, Tensor)");
+    m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu) -> Tensor");
+    m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu) -> (Tensor, Tensor, Tensor)");
+    m.def("native_version() -> int");
+}
+
+TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
+    m.impl("gemm", &gemm);
+    m.impl("bias_act_grad", &bias_act_grad);
+    m.impl("act_fwd", &act_fwd);
+    m.impl("act_bwd", &act_bwd);
+    m.impl("dropout_fwd", &dropout_fwd);
+    m.impl("add_act", &add_act);
+    m.impl("softmax_fwd", &softmax_fwd);
+    m.impl("softmax_bwd", &softmax_bwd);
+    m.impl("xent_fwd", &xent_fwd);
+    m.impl("xent_bwd", &xent_bwd);
+    m.impl("layernorm_fwd", &layernorm_fwd);
+    m.impl("layernorm_bwd", &layernorm_bwd);
+    m.impl("embedding_fwd", &embedding_fwd);
+    m.impl("embedding_bwd", &embedding_bwd);
+    m.impl("sumsq", &sumsq);
+    m.impl("adamw_step", &adamw_step);
+    m.impl("sgd_step", &sgd_step);
+    m.impl("attn_fwd", &attn_fwd);
+    m.impl("attn_bwd", &attn_bwd);
+    m.impl("attn_bwd_out", &attn_bwd_out);
+    m.impl("im2col", &im2col);
+    m.impl("col2im", &col2im);
+    m.impl("maxpool_fwd", &maxpool_fwd);
+    m.impl("maxpool_bwd", &maxpool_bwd);
+    m.impl("avgpool_fwd", &avgpool_fwd);
+    m.impl("avgpool_bwd", &avgpool_bwd);
+    m.impl("batchnorm_fwd", &batchnorm_fwd);
+    m.impl("batchnorm_eval", &batchnorm_eval);
+    m.impl("batchnorm_bwd", &batchnorm_bwd);
+}
+
+TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {
+    m.impl("native_version", &native_version);
+}

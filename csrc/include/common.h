@@ -1,0 +1,112 @@
+// Shared device helpers for the replicann gfx950 kernels.
+//
+// Everything here is written for CDNA4 directly: 64-lane waves, bf16 moved as
+// 16-byte vectors (8 elements per lane), fp32 math, hardware bf16 converts.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef short  s16x8 __attribute__((ext_vector_type(8)));
+typedef short  s16x4 __attribute__((ext_vector_type(4)));
+typedef float  f32x4 __attribute__((ext_vector_type(4)));
+typedef float  f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+#define RN_WAVE 64
+#define RN_DEV __device__ __forceinline__
+
+RN_DEV float bf2f(bf16 x) { return (float)x; }
+RN_DEV bf16 f2bf(float x) { return (bf16)x; }
+
+// 8 bf16 <-> 8 float
+RN_DEV void load8(const bf16* p, float* f) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
+}
+RN_DEV void store8(bf16* p, const float* f) {
+    bf16x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (bf16)f[i];
+    *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+RN_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+RN_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (scratch: >= 16 floats of LDS).
+RN_DEV float block_sum(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += scratch[i];
+    return t;
+}
+RN_DEV float block_max(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_max(v);
+    __syncthreads();
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    float t = -INFINITY;
+    for (int i = 0; i < nw; ++i) t = fmaxf(t, scratch[i]);
+    return t;
+}
+
+// Counter-based RNG (splitmix64 finaliser): uniform in [0,1) from (seed, index).
+// Stateless, so dropout masks are regenerated in the backward instead of stored.
+RN_DEV float hash_uniform(uint64_t seed, uint64_t idx) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// tanh-approximate GELU and its derivative
+RN_DEV float gelu_f(float x) {
+    const float c = 0.7978845608028654f;
+    float u = c * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+}
+RN_DEV float gelu_grad_f(float x) {
+    const float c = 0.7978845608028654f;
+    float x2 = x * x;
+    float u = c * (x + 0.044715f * x2 * x);
+    float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * c * (1.f + 3.f * 0.044715f * x2);
+}
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+template <int ACT>
+RN_DEV float act_f(float x) {
+    if constexpr (ACT == ACT_RELU) return fmaxf(x, 0.f);
+    else if constexpr (ACT == ACT_GELU) return gelu_f(x);
+    else return x;
+}
+template <int ACT>
+RN_DEV float act_grad_f(float x) {
+    if constexpr (ACT == ACT_RELU) return x > 0.f ? 1.f : 0.f;
+    else if constexpr (ACT == ACT_GELU) return gelu_grad_f(x);
+    else return 1.f;
+}
+
+#define HIP_CHECK_LAUNCH() (void)hipGetLastError()
+
+static inline int rn_cdiv(long a, long b) { return (int)((a + b - 1) / b); }

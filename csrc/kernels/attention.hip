@@ -1,0 +1,708 @@
+// Fused scaled-dot-product attention, forward + backward (N4/N5).
+//
+// Layout: q/k/v/o are [B][T][H][D] with arbitrary batch/token/head strides
+// (q, k, v are usually views into one packed QKV GEMM output).  LSE is saved as
+// [B][H][Tq] fp32 (natural log).
+//
+// Fast path D = 64 (GPT-2 small/medium, ViT-B/16), all v_mfma_f32_16x16x32_bf16:
+//   * every product is arranged so that the softmax row index (the query for
+//     fwd / dQ, the key for dK/dV) sits on lane&15 and the reduced index sits in
+//     accumulator registers: the accumulator tile is then directly the next
+//     MFMA's B operand (no LDS round trip, no lane shuffles for P or dS);
+//     the k-order inside each 32-wide k-step is permuted identically on both
+//     operands ({4g..4g+3} ∪ {16+4g..16+4g+3} for lane group g);
+//   * the other operand of those products is a column slice of a row-major LDS
+//     tile, read with ds_read_b64_tr_b16 (hardware transpose);
+//   * LDS tiles are [64 rows][64 bf16] (128-B rows) staged by LDS-DMA
+//     (buffer_load … lds) with the 16-B chunk XOR swizzle c ^ (((r>>1)&3)<<1),
+//     which is conflict-free for BOTH the ds_read_b128 row reads and the
+//     transposed reads (one image serves both);
+//   * online softmax in exp2 domain; causal tiles above the diagonal are
+//     skipped, diagonal tiles masked; heaviest causal blocks launch first;
+//   * dropout on P by a stateless counter hash, regenerated in the backward;
+//   * backward = delta kernel (rowsum dO·O) + dK/dV kernel (one workgroup per
+//     64 keys, loops over queries) + dQ kernel (one workgroup per 64 queries,
+//     loops over keys): no atomics, bitwise deterministic.
+// Generic path (any D ≤ 256, used by the reference-parity blocks with small
+// head sizes): straightforward per-query-row kernels with fp32 scores in LDS.
+#include "common.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct AttnArgs {
+    const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* bias;
+    const bf16* dout; bf16* dq; bf16* dk; bf16* dv; const float* delta;
+    long q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh;
+    long do_sb, do_st, do_sh, dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
+    int B, H, Tq, Tk, D;
+    int causal, bias_b;
+    float scale, p_drop;
+    uint64_t seed;
+    float* dk32; float* dv32;  // generic bwd scratch
+};
+
+RN_DEV int swz(int r) { return ((r >> 1) & 3) << 1; }
+
+RN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+    const uint64_t bp = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+}
+
+// Stage rows [r0, r0+64) (valid < rlim) of a [T][stride] bf16 matrix (64 cols at `base`)
+// into a swizzled 8 KiB LDS tile.  8 DMA instructions; each of the 4 waves issues 2.
+RN_DEV void stage64(const bf16* base, long st, int r0, int rlim, char* lds, int wave, int lane) {
+    __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ins = wave * 2 + i;
+        const int r = ins * 8 + (lane >> 3);
+        const int cg = (lane & 7) ^ swz(r);
+        const bool ok = (r0 + r) < rlim;
+        const uint32_t voff = ok ? (uint32_t)((((long)(r0 + r)) * st + cg * 8) * 2) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
+    }
+}
+
+// row fragment: 8 bf16 of row `row`, columns 32*s + 8*(lane>>4) .. +7
+RN_DEV s16x8 rowfrag(const char* t, int row, int s, int lane) {
+    const int chunk = s * 4 + (lane >> 4);
+    return *reinterpret_cast<const s16x8*>(t + row * 128 + ((chunk ^ swz(row)) << 4));
+}
+
+// column fragment: column c0 + (lane&15), rows {rb + 4g + 0..3} ∪ {rb + 16 + 4g + 0..3}
+RN_DEV s16x8 colfrag(const char* t, int rb, int c0, int lane) {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+    const int ch = (c0 >> 3) + (p >> 1);
+    const int r0 = rb + 4 * g + qq, r1 = r0 + 16;
+    const char* a0 = t + r0 * 128 + ((ch ^ swz(r0)) << 4) + (p & 1) * 8;
+    const char* a1 = t + r1 * 128 + ((ch ^ swz(r1)) << 4) + (p & 1) * 8;
+    s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    s16x8 r;
+    r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+    r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+    return r;
+}
+
+RN_DEV s16x8 gload16(const bf16* p, bool ok) {
+    if (!ok) return (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    return *reinterpret_cast<const s16x8*>(p);
+}
+
+RN_DEV short bfbits(float f) { return __builtin_bit_cast(short, (bf16)f); }
+
+RN_DEV s16x8 pack_p(const f32x4& a, const f32x4& b) {
+    s16x8 r;
+    r[0] = bfbits(a[0]); r[1] = bfbits(a[1]); r[2] = bfbits(a[2]); r[3] = bfbits(a[3]);
+    r[4] = bfbits(b[0]); r[5] = bfbits(b[1]); r[6] = bfbits(b[2]); r[7] = bfbits(b[3]);
+    return r;
+}
+
+RN_DEV uint64_t drop_idx(const AttnArgs& p, int b, int h, int qi, int kj) {
+    return (((uint64_t)(b * p.H + h) * p.Tq + qi) * (uint64_t)p.Tk) + kj;
+}
+
+#define MFMA __builtin_amdgcn_mfma_f32_16x16x32_bf16
+
+// ============================== forward, D = 64 ==============================
+// grid: (ceil(Tq/128), B*H); 4 waves x 32 query rows.
+template <bool CAUSAL, bool BIAS, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_fwd64_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nqb = gridDim.x;
+    const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heaviest first
+    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const int q0 = qb * 128 + wave * 32;
+    const int off = p.Tk - p.Tq;  // causal: key j visible to query i iff j <= i + off
+    const float sl2 = p.scale * LOG2E;
+
+    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
+    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
+    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
+
+    s16x8 qf[2][2];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int row = q0 + qi * 16 + c;
+            qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
+        }
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    f32x4 oacc[2][4];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    int kv_end = p.Tk;
+    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
+#define Kt(i) (smem + (i) * 16384)
+#define Vt(i) (smem + 8192 + (i) * 16384)
+    if (nkv > 0) {
+        stage64(kbase, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64(vbase, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+    }
+    const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+    for (int t = 0; t < nkv; ++t) {
+        __syncthreads();
+        const int cur = t & 1;
+        if (t + 1 < nkv) {
+            stage64(kbase, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
+            stage64(vbase, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
+        }
+        const int kv0 = t * 64;
+        // wave-uniform skip: this wave's queries all precede the tile
+        if (CAUSAL && kv0 > q0 + 31 + off) continue;
+        const char* kt = Kt(cur);
+        const char* vt = Vt(cur);
+        f32x4 sacc[2][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s16x8 a0 = rowfrag(kt, j * 16 + c, 0, lane);
+            s16x8 a1 = rowfrag(kt, j * 16 + c, 1, lane);
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) {
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                z = MFMA(a0, qf[qi][0], z, 0, 0, 0);
+                sacc[qi][j] = MFMA(a1, qf[qi][1], z, 0, 0, 0);
+            }
+        }
+        const bool need_mask = (kv0 + 64 > p.Tk) || (CAUSAL && kv0 + 63 > q0 + off);
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) {
+            const int qg = q0 + qi * 16 + c;
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float bb[4] = {0.f, 0.f, 0.f, 0.f};
+                const int kvb = kv0 + j * 16 + 4 * g;
+                if constexpr (BIAS) {
+                    if (qg < p.Tq) {
+                        const float* bp = p.bias + ((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvb;
+                        if (kvb + 3 < p.Tk && (p.Tk & 3) == 0) {
+                            float4 t4 = *reinterpret_cast<const float4*>(bp);
+                            bb[0] = t4.x; bb[1] = t4.y; bb[2] = t4.z; bb[3] = t4.w;
+                        } else {
+                            for (int r = 0; r < 4; ++r) bb[r] = (kvb + r < p.Tk) ? bp[r] : 0.f;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float x = sacc[qi][j][r] * sl2 + (BIAS ? bb[r] * LOG2E : 0.f);
+                    if (need_mask) {
+                        const int kvj = kvb + r;
+                        if (kvj >= p.Tk || (CAUSAL && kvj > qg + off)) x = -INFINITY;
+                    }
+                    sacc[qi][j][r] = x;
+                    tmax = fmaxf(tmax, x);
+                }
+            }
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+            const float mn = fmaxf(m[qi], tmax);
+            const float ms = (mn == -INFINITY) ? 0.f : mn;  // fully-masked rows stay at p = 0
+            const float alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[qi] - ms);
+            m[qi] = mn;
+            float ls = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float pv = __builtin_amdgcn_exp2f(sacc[qi][j][r] - ms);
+                    ls += pv;
+                    if constexpr (DROP) {
+                        const int kvj = kv0 + j * 16 + 4 * g + r;
+                        pv = (hash_uniform(p.seed, drop_idx(p, b, h, qg, kvj)) >= p.p_drop) ? pv * rd : 0.f;
+                    }
+                    sacc[qi][j][r] = pv;
+                }
+            l[qi] = l[qi] * alpha + ls;
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alpha;
+        }
+        // O^T[d][q] += V^T[d][kv] * P^T[kv][q]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            s16x8 pb[2];
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                s16x8 a = colfrag(vt, 32 * s, 16 * jd, lane);
+#pragma unroll
+                for (int qi = 0; qi < 2; ++qi) oacc[qi][jd] = MFMA(a, pb[qi], oacc[qi][jd], 0, 0, 0);
+            }
+        }
+    }
+    // epilogue
+    bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+        float lt = l[qi];
+        lt += __shfl_xor(lt, 16, 64);
+        lt += __shfl_xor(lt, 32, 64);
+        const int qg = q0 + qi * 16 + c;
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        if (qg < p.Tq) {
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                bf16x4 o4 = {(bf16)(oacc[qi][jd][0] * inv), (bf16)(oacc[qi][jd][1] * inv),
+                             (bf16)(oacc[qi][jd][2] * inv), (bf16)(oacc[qi][jd][3] * inv)};
+                *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
+            }
+            if (g == 0)
+                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] + log2f(lt)) * LN2 : INFINITY;
+        }
+    }
+}
+
+// ============================== backward, D = 64 ==============================
+// delta[b,h,q] = sum_d dO * O  — one thread per (b, q, h) row of D = 64 (8 x 16-B loads each)
+__global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= (long)p.B * p.Tq * p.H) return;
+    const int h = i % p.H;
+    const long bq = i / p.H;
+    const int q = bq % p.Tq, b = bq / p.Tq;
+    const bf16* dp = p.dout + b * p.do_sb + (long)q * p.do_st + h * p.do_sh;
+    const bf16* op = p.o + b * p.o_sb + (long)q * p.o_st + h * p.o_sh;
+    float s = 0.f;
+    for (int ch = 0; ch < p.D / 8; ++ch) {
+        float a[8], o[8];
+        load8(dp + ch * 8, a);
+        load8(op + ch * 8, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += a[j] * o[j];
+    }
+    const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + q] = s;
+}
+
+// dK, dV: grid (ceil(Tk/64), B*H); wave w owns keys kv0 + 16w + (lane&15)
+template <bool CAUSAL, bool BIAS, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int kb = blockIdx.x;  // low key blocks see the most queries under causal: they launch first
+    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const int kvw = kb * 64 + wave * 16;  // this wave's first key
+    const int kv = kvw + c;
+    const int off = p.Tk - p.Tq;
+    const float sl2 = p.scale * LOG2E;
+
+    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
+    const bf16* dobase = p.dout + b * p.do_sb + h * p.do_sh;
+    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
+    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
+    const float* lsep = p.lse + ((long)b * p.H + h) * p.Tq;
+    const float* dlp = p.delta + ((long)b * p.H + h) * p.Tq;
+
+    s16x8 kf[2], vf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        kf[s] = gload16(kbase + (long)kv * p.k_st + s * 32 + g * 8, kv < p.Tk);
+        vf[s] = gload16(vbase + (long)kv * p.v_st + s * 32 + g * 8, kv < p.Tk);
+    }
+    f32x4 dvacc[4], dkacc[4];
+#pragma unroll
+    for (int jd = 0; jd < 4; ++jd) { dvacc[jd] = (f32x4){0, 0, 0, 0}; dkacc[jd] = (f32x4){0, 0, 0, 0}; }
+
+    int qt0 = 0;
+    if (CAUSAL) qt0 = max(0, (kb * 64 - off)) / 64;
+    const int nqt = (p.Tq + 63) / 64;
+#define Qt(i) (smem + (i) * 16384)
+#define Ot(i) (smem + 8192 + (i) * 16384)
+    if (qt0 < nqt) {
+        stage64(qbase, p.q_st, qt0 * 64, p.Tq, Qt(0), wave, lane);
+        stage64(dobase, p.do_st, qt0 * 64, p.Tq, Ot(0), wave, lane);
+    }
+    const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+    for (int qt = qt0; qt < nqt; ++qt) {
+        __syncthreads();
+        const int cur = (qt - qt0) & 1;
+        if (qt + 1 < nqt) {
+            stage64(qbase, p.q_st, (qt + 1) * 64, p.Tq, Qt(cur ^ 1), wave, lane);
+            stage64(dobase, p.do_st, (qt + 1) * 64, p.Tq, Ot(cur ^ 1), wave, lane);
+        }
+        const int q0 = qt * 64;
+        if (CAUSAL && q0 + 63 + off < kvw) continue;  // wave-uniform: all queries precede this wave's keys
+        const char* qt_ = Qt(cur);
+        const char* ot_ = Ot(cur);
+        f32x4 pq[4], dsq[4];
+#pragma unroll
+        for (int qi = 0; qi < 4; ++qi) {
+            f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
+            s16x8 a0 = rowfrag(qt_, qi * 16 + c, 0, lane), a1 = rowfrag(qt_, qi * 16 + c, 1, lane);
+            sa = MFMA(a0, kf[0], sa, 0, 0, 0);
+            sa = MFMA(a1, kf[1], sa, 0, 0, 0);
+            s16x8 o0 = rowfrag(ot_, qi * 16 + c, 0, lane), o1 = rowfrag(ot_, qi * 16 + c, 1, lane);
+            da = MFMA(o0, vf[0], da, 0, 0, 0);
+            da = MFMA(o1, vf[1], da, 0, 0, 0);
+            // lane holds S[q = q0 + 16qi + 4g + r][kv]
+            const int qb4 = q0 + qi * 16 + 4 * g;
+            float ls[4], dl[4];
+            if (qb4 + 3 < p.Tq) {
+                float4 a = *reinterpret_cast<const float4*>(lsep + qb4);
+                float4 d = *reinterpret_cast<const float4*>(dlp + qb4);
+                ls[0] = a.x; ls[1] = a.y; ls[2] = a.z; ls[3] = a.w;
+                dl[0] = d.x; dl[1] = d.y; dl[2] = d.z; dl[3] = d.w;
+            } else {
+                for (int r = 0; r < 4; ++r) {
+                    ls[r] = qb4 + r < p.Tq ? lsep[qb4 + r] : INFINITY;
+                    dl[r] = qb4 + r < p.Tq ? dlp[qb4 + r] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int qg = qb4 + r;
+                float x = sa[r] * sl2;
+                if constexpr (BIAS) {
+                    if (qg < p.Tq && kv < p.Tk)
+                        x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kv] * LOG2E;
+                }
+                float pv = __builtin_amdgcn_exp2f(x - ls[r] * LOG2E);
+                if (kv >= p.Tk || qg >= p.Tq || (CAUSAL && kv > qg + off) || ls[r] == INFINITY) pv = 0.f;
+                float dpv = da[r];
+                float pd = pv;
+                if constexpr (DROP) {
+                    const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qg, kv)) >= p.p_drop;
+                    pd = keep ? pv * rd : 0.f;
+                    dpv = keep ? dpv * rd : 0.f;
+                }
+                pq[qi][r] = pd;
+                dsq[qi][r] = pv * (dpv - dl[r]);
+            }
+        }
+        // dV^T[d][kv] += dO^T[d][q] Pd[q][kv];  dK^T[d][kv] += Q^T[d][q] dS[q][kv]
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            s16x8 pb = pack_p(pq[2 * ks], pq[2 * ks + 1]);
+            s16x8 sb = pack_p(dsq[2 * ks], dsq[2 * ks + 1]);
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                s16x8 ao = colfrag(ot_, 32 * ks, 16 * jd, lane);
+                dvacc[jd] = MFMA(ao, pb, dvacc[jd], 0, 0, 0);
+                s16x8 aq = colfrag(qt_, 32 * ks, 16 * jd, lane);
+                dkacc[jd] = MFMA(aq, sb, dkacc[jd], 0, 0, 0);
+            }
+        }
+    }
+    if (kv < p.Tk) {
+        bf16* dkp = p.dk + b * p.dk_sb + (long)kv * p.dk_st + h * p.dk_sh;
+        bf16* dvp = p.dv + b * p.dv_sb + (long)kv * p.dv_st + h * p.dv_sh;
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) {
+            bf16x4 k4 = {(bf16)(dkacc[jd][0] * p.scale), (bf16)(dkacc[jd][1] * p.scale),
+                         (bf16)(dkacc[jd][2] * p.scale), (bf16)(dkacc[jd][3] * p.scale)};
+            bf16x4 v4 = {(bf16)dvacc[jd][0], (bf16)dvacc[jd][1], (bf16)dvacc[jd][2], (bf16)dvacc[jd][3]};
+            *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
+            *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
+        }
+    }
+}
+
+// dQ: grid (ceil(Tq/64), B*H); wave w owns queries q0 + 16w + (lane&15)
+template <bool CAUSAL, bool BIAS, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nqb = gridDim.x;
+    const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
+    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const int qw = qb * 64 + wave * 16;
+    const int qg = qw + c;
+    const int off = p.Tk - p.Tq;
+    const float sl2 = p.scale * LOG2E;
+
+    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
+    const bf16* dobase = p.dout + b * p.do_sb + h * p.do_sh;
+    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
+    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
+    s16x8 qf[2], df[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        qf[s] = gload16(qbase + (long)qg * p.q_st + s * 32 + g * 8, qg < p.Tq);
+        df[s] = gload16(dobase + (long)qg * p.do_st + s * 32 + g * 8, qg < p.Tq);
+    }
+    const bool qok = qg < p.Tq;
+    const float lse2 = qok ? p.lse[((long)b * p.H + h) * p.Tq + qg] * LOG2E : INFINITY;
+    const float dl = qok ? p.delta[((long)b * p.H + h) * p.Tq + qg] : 0.f;
+    f32x4 dqacc[4];
+#pragma unroll
+    for (int jd = 0; jd < 4; ++jd) dqacc[jd] = (f32x4){0, 0, 0, 0};
+
+    int kv_end = p.Tk;
+    if (CAUSAL) kv_end = min(p.Tk, qb * 64 + 64 + off);
+    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
+#define Kt(i) (smem + (i) * 16384)
+#define Vt(i) (smem + 8192 + (i) * 16384)
+    if (nkv > 0) {
+        stage64(kbase, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64(vbase, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+    }
+    const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+    for (int t = 0; t < nkv; ++t) {
+        __syncthreads();
+        const int cur = t & 1;
+        if (t + 1 < nkv) {
+            stage64(kbase, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
+            stage64(vbase, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
+        }
+        const int kv0 = t * 64;
+        if (CAUSAL && kv0 > qw + 15 + off) continue;
+        const char* kt = Kt(cur);
+        const char* vt = Vt(cur);
+        f32x4 dsv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
+            sa = MFMA(rowfrag(kt, j * 16 + c, 0, lane), qf[0], sa, 0, 0, 0);
+            sa = MFMA(rowfrag(kt, j * 16 + c, 1, lane), qf[1], sa, 0, 0, 0);
+            da = MFMA(rowfrag(vt, j * 16 + c, 0, lane), df[0], da, 0, 0, 0);
+            da = MFMA(rowfrag(vt, j * 16 + c, 1, lane), df[1], da, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int kvj = kv0 + j * 16 + 4 * g + r;
+                float x = sa[r] * sl2;
+                if constexpr (BIAS) {
+                    if (qok && kvj < p.Tk)
+                        x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvj] * LOG2E;
+                }
+                float pv = __builtin_amdgcn_exp2f(x - lse2);
+                if (kvj >= p.Tk || !qok || (CAUSAL && kvj > qg + off)) pv = 0.f;
+                float dpv = da[r];
+                if constexpr (DROP) {
+                    const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qg, kvj)) >= p.p_drop;
+                    dpv = keep ? dpv * rd : 0.f;
+                }
+                dsv[j][r] = pv * (dpv - dl);
+            }
+        }
+        // dQ^T[d][q] += K^T[d][kv] dS^T[kv][q]
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            s16x8 sb = pack_p(dsv[2 * ks], dsv[2 * ks + 1]);
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfrag(kt, 32 * ks, 16 * jd, lane), sb, dqacc[jd], 0, 0, 0);
+        }
+    }
+    if (qok) {
+        bf16* dqp = p.dq + b * p.dq_sb + (long)qg * p.dq_st + h * p.dq_sh;
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) {
+            bf16x4 q4 = {(bf16)(dqacc[jd][0] * p.scale), (bf16)(dqacc[jd][1] * p.scale),
+                         (bf16)(dqacc[jd][2] * p.scale), (bf16)(dqacc[jd][3] * p.scale)};
+            *reinterpret_cast<bf16x4*>(dqp + jd * 16 + 4 * g) = q4;
+        }
+    }
+}
+
+// ============================== generic path (any D <= 256) ==============================
+RN_DEV float bias_at(const AttnArgs& p, int b, int qi, int kj) {
+    return p.bias ? p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qi) * p.Tk + kj] : 0.f;
+}
+RN_DEV bool visible(const AttnArgs& p, int qi, int kj) { return !(p.causal && kj > qi + (p.Tk - p.Tq)); }
+
+// one block per (b, h, q); scores in LDS (Tk floats)
+__global__ void __launch_bounds__(256) attn_fwd_generic_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* sc = reinterpret_cast<float*>(smem);
+    float* qv = sc + p.Tk;
+    __shared__ float red[16];
+    const int qi = blockIdx.x, bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const bf16* qp = p.q + b * p.q_sb + (long)qi * p.q_st + h * p.q_sh;
+    for (int d = threadIdx.x; d < p.D; d += 256) qv[d] = bf2f(qp[d]);
+    __syncthreads();
+    float mx = -INFINITY;
+    for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
+        const bf16* kp = p.k + b * p.k_sb + (long)kj * p.k_st + h * p.k_sh;
+        float s = 0.f;
+        for (int d = 0; d < p.D; ++d) s += qv[d] * bf2f(kp[d]);
+        s = s * p.scale + bias_at(p, b, qi, kj);
+        if (!visible(p, qi, kj)) s = -INFINITY;
+        sc[kj] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = block_max(mx, red);
+    __syncthreads();
+    float sum = 0.f;
+    const float ms = mx == -INFINITY ? 0.f : mx;
+    for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
+        float e = __expf(sc[kj] - ms);
+        sc[kj] = e;
+        sum += e;
+    }
+    sum = block_sum(sum, red);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    const float rd = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+    for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
+        float pv = sc[kj] * inv;
+        if (p.p_drop > 0.f) pv = hash_uniform(p.seed, drop_idx(p, b, h, qi, kj)) >= p.p_drop ? pv * rd : 0.f;
+        sc[kj] = pv;
+    }
+    __syncthreads();
+    bf16* op = p.o + b * p.o_sb + (long)qi * p.o_st + h * p.o_sh;
+    for (int d = threadIdx.x; d < p.D; d += 256) {
+        float acc = 0.f;
+        for (int kj = 0; kj < p.Tk; ++kj) acc += sc[kj] * bf2f(p.v[b * p.v_sb + (long)kj * p.v_st + h * p.v_sh + d]);
+        op[d] = f2bf(acc);
+    }
+    if (threadIdx.x == 0) p.lse[((long)b * p.H + h) * p.Tq + qi] = sum > 0.f ? ms + __logf(sum) : INFINITY;
+}
+
+__global__ void __launch_bounds__(256) attn_bwd_generic_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* pp = reinterpret_cast<float*>(smem);   // P (undropped)
+    float* ds = pp + p.Tk;                          // dS
+    float* qv = ds + p.Tk;                          // q row
+    float* dov = qv + p.D;                          // dO row
+    __shared__ float red[16];
+    const int qi = blockIdx.x, bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const bf16* qp = p.q + b * p.q_sb + (long)qi * p.q_st + h * p.q_sh;
+    const bf16* dop = p.dout + b * p.do_sb + (long)qi * p.do_st + h * p.do_sh;
+    const bf16* op = p.o + b * p.o_sb + (long)qi * p.o_st + h * p.o_sh;
+    float dl = 0.f;
+    for (int d = threadIdx.x; d < p.D; d += 256) {
+        qv[d] = bf2f(qp[d]);
+        dov[d] = bf2f(dop[d]);
+        dl += dov[d] * bf2f(op[d]);
+    }
+    dl = block_sum(dl, red);
+    const float L = p.lse[((long)b * p.H + h) * p.Tq + qi];
+    const float rd = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+    for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
+        const bf16* kp = p.k + b * p.k_sb + (long)kj * p.k_st + h * p.k_sh;
+        const bf16* vp = p.v + b * p.v_sb + (long)kj * p.v_st + h * p.v_sh;
+        float s = 0.f, dp = 0.f;
+        for (int d = 0; d < p.D; ++d) { s += qv[d] * bf2f(kp[d]); dp += dov[d] * bf2f(vp[d]); }
+        s = s * p.scale + bias_at(p, b, qi, kj);
+        float pv = (visible(p, qi, kj) && L != INFINITY) ? __expf(s - L) : 0.f;
+        float pd = pv;
+        if (p.p_drop > 0.f) {
+            bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qi, kj)) >= p.p_drop;
+            pd = keep ? pv * rd : 0.f;
+            dp = keep ? dp * rd : 0.f;
+        }
+        pp[kj] = pd;
+        ds[kj] = pv * (dp - dl);
+    }
+    __syncthreads();
+    bf16* dqp = p.dq + b * p.dq_sb + (long)qi * p.dq_st + h * p.dq_sh;
+    for (int d = threadIdx.x; d < p.D; d += 256) {
+        float acc = 0.f;
+        for (int kj = 0; kj < p.Tk; ++kj) acc += ds[kj] * bf2f(p.k[b * p.k_sb + (long)kj * p.k_st + h * p.k_sh + d]);
+        dqp[d] = f2bf(acc * p.scale);
+    }
+    // dK, dV (fp32 scratch [B][Tk][H][D], atomics)
+    for (long e = threadIdx.x; e < (long)p.Tk * p.D; e += 256) {
+        const int kj = e / p.D, d = e % p.D;
+        const long idx = (((long)b * p.Tk + kj) * p.H + h) * p.D + d;
+        if (ds[kj] != 0.f) atomicAdd(p.dk32 + idx, ds[kj] * qv[d] * p.scale);
+        if (pp[kj] != 0.f) atomicAdd(p.dv32 + idx, pp[kj] * dov[d]);
+    }
+}
+
+__global__ void scatter_kv_k(AttnArgs p) {
+    const long n = (long)p.B * p.Tk * p.H * p.D;
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+        const int d = e % p.D;
+        const long t1 = e / p.D;
+        const int h = t1 % p.H;
+        const long t2 = t1 / p.H;
+        const int kj = t2 % p.Tk, b = t2 / p.Tk;
+        p.dk[b * p.dk_sb + (long)kj * p.dk_st + h * p.dk_sh + d] = f2bf(p.dk32[e]);
+        p.dv[b * p.dv_sb + (long)kj * p.dv_st + h * p.dv_sh + d] = f2bf(p.dv32[e]);
+    }
+}
+
+#define RN_DISPATCH3(KERN, grid, lds, st, args)                                                       \
+    do {                                                                                               \
+        const bool c_ = args.causal, b_ = args.bias != nullptr, d_ = args.p_drop > 0.f;              \
+        if (c_) {                                                                                      \
+            if (b_) { if (d_) KERN<true, true, true><<<grid, 256, lds, st>>>(args); else KERN<true, true, false><<<grid, 256, lds, st>>>(args); } \
+            else { if (d_) KERN<true, false, true><<<grid, 256, lds, st>>>(args); else KERN<true, false, false><<<grid, 256, lds, st>>>(args); } \
+        } else {                                                                                       \
+            if (b_) { if (d_) KERN<false, true, true><<<grid, 256, lds, st>>>(args); else KERN<false, true, false><<<grid, 256, lds, st>>>(args); } \
+            else { if (d_) KERN<false, false, true><<<grid, 256, lds, st>>>(args); else KERN<false, false, false><<<grid, 256, lds, st>>>(args); } \
+        }                                                                                              \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+// strides in elements: [b, t, h] for q, k, v, o ; d is contiguous
+int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* bias, int bias_b,
+                const long* strides, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
+                uint64_t seed, hipStream_t st) {
+    AttnArgs a = {};
+    a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = lse; a.bias = bias;
+    a.q_sb = strides[0]; a.q_st = strides[1]; a.q_sh = strides[2];
+    a.k_sb = strides[3]; a.k_st = strides[4]; a.k_sh = strides[5];
+    a.v_sb = strides[6]; a.v_st = strides[7]; a.v_sh = strides[8];
+    a.o_sb = strides[9]; a.o_st = strides[10]; a.o_sh = strides[11];
+    a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
+    a.scale = scale; a.p_drop = p_drop; a.seed = seed;
+    const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
+    if (fast) {
+        dim3 grid((Tq + 127) / 128, B * H);
+        RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
+    } else {
+        if (D > 256 || Tk > 12000) return -1;
+        dim3 grid(Tq, B * H);
+        attn_fwd_generic_k<<<grid, 256, (Tk + D) * 4, st>>>(a);
+    }
+    return 0;
+}
+
+// strides: q,k,v,o,do,dq,dk,dv (each b,t,h).  delta: B*H*Tq floats workspace.
+// dk32/dv32: generic path scratch (B*Tk*H*D floats each, zeroed by caller) or null.
+int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
+                const float* bias, int bias_b, void* dq, void* dk, void* dv, float* delta, float* dk32, float* dv32,
+                const long* s, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
+                uint64_t seed, hipStream_t st) {
+    AttnArgs a = {};
+    a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = (float*)lse;
+    a.bias = bias; a.dout = (const bf16*)dout; a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.delta = delta;
+    a.q_sb = s[0]; a.q_st = s[1]; a.q_sh = s[2]; a.k_sb = s[3]; a.k_st = s[4]; a.k_sh = s[5];
+    a.v_sb = s[6]; a.v_st = s[7]; a.v_sh = s[8]; a.o_sb = s[9]; a.o_st = s[10]; a.o_sh = s[11];
+    a.do_sb = s[12]; a.do_st = s[13]; a.do_sh = s[14]; a.dq_sb = s[15]; a.dq_st = s[16]; a.dq_sh = s[17];
+    a.dk_sb = s[18]; a.dk_st = s[19]; a.dk_sh = s[20]; a.dv_sb = s[21]; a.dv_st = s[22]; a.dv_sh = s[23];
+    a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
+    a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.dk32 = dk32; a.dv32 = dv32;
+    const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) &&
+                      (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
+                      (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
+    if (fast) {
+        attn_delta_k<<<(int)(((long)B * Tq * H + 255) / 256), 256, 0, st>>>(a);
+        dim3 g1((Tk + 63) / 64, B * H);
+        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 32768, st, a);
+        dim3 g2((Tq + 63) / 64, B * H);
+        RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
+    } else {
+        if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
+        dim3 grid(Tq, B * H);
+        attn_bwd_generic_k<<<grid, 256, (2 * Tk + 2 * D) * 4, st>>>(a);
+        long n = (long)B * Tk * H * D;
+        scatter_kv_k<<<(int)std::min<long>((n + 255) / 256, 4096), 256, 0, st>>>(a);
+    }
+    return 0;
+}
+
+int rn_attn_is_fast(int D) { return D == 64; }
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+// Elementwise kernels: activations, dropout, fused activation-backward + bias-grad,
+// add(+relu).  Memory-bound: every kernel moves bf16 as 16-byte vectors
+// (8 elements / lane), grid-strides over at most 256 CUs x 8 blocks.
+#include "common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+inline int ew_grid(long n8) {
+    long g = (n8 + TPB - 1) / TPB;
+    return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(TPB) act_fwd_k(const bf16* __restrict__ x, bf16* __restrict__ y, long n) {
+    long n8 = n / 8;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n8; i += (long)gridDim.x * TPB) {
+        float f[8];
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = act_f<ACT>(f[j]);
+        store8(y + i * 8, f);
+    }
+    for (long i = n8 * 8 + blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB)
+        y[i] = f2bf(act_f<ACT>(bf2f(x[i])));
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(TPB) act_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                 bf16* __restrict__ dx, long n) {
+    long n8 = n / 8;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n8; i += (long)gridDim.x * TPB) {
+        float g[8], f[8];
+        load8(dy + i * 8, g);
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] *= act_grad_f<ACT>(f[j]);
+        store8(dx + i * 8, g);
+    }
+    for (long i = n8 * 8 + blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB)
+        dx[i] = f2bf(bf2f(dy[i]) * act_grad_f<ACT>(bf2f(x[i])));
+}
+
+__global__ void __launch_bounds__(TPB) dropout_k(const bf16* __restrict__ x, bf16* __restrict__ y, long n,
+                                                 float p, uint64_t seed) {
+    const float keep = 1.f / (1.f - p);
+    long n8 = n / 8;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n8; i += (long)gridDim.x * TPB) {
+        float f[8];
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = hash_uniform(seed, i * 8 + j) >= p ? f[j] * keep : 0.f;
+        store8(y + i * 8, f);
+    }
+    for (long i = n8 * 8 + blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB)
+        y[i] = f2bf(hash_uniform(seed, i) >= p ? bf2f(x[i]) * keep : 0.f);
+}
+
+// out = relu?(a + b)
+template <bool RELU>
+__global__ void __launch_bounds__(TPB) add_k(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                             bf16* __restrict__ y, long n) {
+    long n8 = n / 8;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n8; i += (long)gridDim.x * TPB) {
+        float f[8], g[8];
+        load8(a + i * 8, f);
+        load8(b + i * 8, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = RELU ? fmaxf(f[j] + g[j], 0.f) : f[j] + g[j];
+        store8(y + i * 8, f);
+    }
+    for (long i = n8 * 8 + blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB) {
+        float v = bf2f(a[i]) + bf2f(b[i]);
+        y[i] = f2bf(RELU ? fmaxf(v, 0.f) : v);
+    }
+}
+
+// dH = dY * act'(H) (written only when ACT != NONE) and partial column sums of dH.
+// Grid: (col_blocks of 512 columns, row_splits).  Each lane owns 8 columns; the
+// block's 4 waves split the rows, partials combine through LDS and land in
+// part[row_split][N] (fp32), summed in fixed order by colsum_finish_k.
+template <int ACT, bool WANT_BIAS>
+__global__ void __launch_bounds__(TPB) bias_act_grad_k(const bf16* __restrict__ dy, const bf16* __restrict__ h,
+                                                       bf16* __restrict__ dh, float* __restrict__ part,
+                                                       int M, int N, int rows_per_split) {
+    __shared__ float red[4][512];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int col = blockIdx.x * 512 + lane * 8;
+    const int r0 = blockIdx.y * rows_per_split;
+    const int r1 = min(M, r0 + rows_per_split);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool vec = (N % 8 == 0);
+    if (vec && col < N) {
+        for (int r = r0 + wid; r < r1; r += 4) {
+            float g[8];
+            long off = (long)r * N + col;
+            load8(dy + off, g);
+            if constexpr (ACT != ACT_NONE) {
+                float f[8];
+                load8(h + off, f);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) g[j] *= act_grad_f<ACT>(f[j]);
+                store8(dh + off, g);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += g[j];
+        }
+    } else if (!vec) {
+        for (int r = r0 + wid; r < r1; r += 4) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                int c = col + j;
+                if (c < N) {
+                    long off = (long)r * N + c;
+                    float g = bf2f(dy[off]);
+                    if constexpr (ACT != ACT_NONE) {
+                        g *= act_grad_f<ACT>(bf2f(h[off]));
+                        dh[off] = f2bf(g);
+                    }
+                    acc[j] += g;
+                }
+            }
+        }
+    }
+    if constexpr (WANT_BIAS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wid][lane * 8 + j] = acc[j];
+        __syncthreads();
+        for (int c = threadIdx.x; c < 512; c += TPB) {
+            int gc = blockIdx.x * 512 + c;
+            if (gc < N) part[(long)blockIdx.y * N + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+        }
+    }
+}
+
+__global__ void colsum_finish_k(const float* __restrict__ part, float* __restrict__ out, int S, int N) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= N) return;
+    float s = 0.f;
+    for (int i = 0; i < S; ++i) s += part[(long)i * N + c];
+    out[c] = s;
+}
+
+}  // namespace
+
+extern "C" {
+
+void rn_act_fwd(const void* x, void* y, long n, int kind, hipStream_t st) {
+    int g = ew_grid(n / 8 + 1);
+    if (kind == ACT_GELU) act_fwd_k<ACT_GELU><<<g, TPB, 0, st>>>((const bf16*)x, (bf16*)y, n);
+    else act_fwd_k<ACT_RELU><<<g, TPB, 0, st>>>((const bf16*)x, (bf16*)y, n);
+}
+
+void rn_act_bwd(const void* dy, const void* x, void* dx, long n, int kind, hipStream_t st) {
+    int g = ew_grid(n / 8 + 1);
+    if (kind == ACT_GELU) act_bwd_k<ACT_GELU><<<g, TPB, 0, st>>>((const bf16*)dy, (const bf16*)x, (bf16*)dx, n);
+    else act_bwd_k<ACT_RELU><<<g, TPB, 0, st>>>((const bf16*)dy, (const bf16*)x, (bf16*)dx, n);
+}
+
+void rn_dropout(const void* x, void* y, long n, float p, uint64_t seed, hipStream_t st) {
+    dropout_k<<<ew_grid(n / 8 + 1), TPB, 0, st>>>((const bf16*)x, (bf16*)y, n, p, seed);
+}
+
+void rn_add(const void* a, const void* b, void* y, long n, int relu, hipStream_t st) {
+    int g = ew_grid(n / 8 + 1);
+    if (relu) add_k<true><<<g, TPB, 0, st>>>((const bf16*)a, (const bf16*)b, (bf16*)y, n);
+    else add_k<false><<<g, TPB, 0, st>>>((const bf16*)a, (const bf16*)b, (bf16*)y, n);
+}
+
+// part: workspace of >= splits*N floats.  Returns nothing; db (fp32, N) written if want_bias.
+void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, float* part, int M, int N, int act,
+                      int want_bias, hipStream_t st) {
+    int cblocks = (N + 511) / 512;
+    int splits = 1;
+    while (cblocks * splits < 512 && M / (splits * 2) >= 32) splits *= 2;
+    int rps = (M + splits - 1) / splits;
+    dim3 grid(cblocks, splits);
+#define RN_BAG(A, W) bias_act_grad_k<A, W><<<grid, TPB, 0, st>>>((const bf16*)dy, (const bf16*)h, (bf16*)dh, part, M, N, rps)
+    if (act == ACT_GELU) { if (want_bias) RN_BAG(ACT_GELU, true); else RN_BAG(ACT_GELU, false); }
+    else if (act == ACT_RELU) { if (want_bias) RN_BAG(ACT_RELU, true); else RN_BAG(ACT_RELU, false); }
+    else { if (want_bias) RN_BAG(ACT_NONE, true); else return; }
+#undef RN_BAG
+    if (want_bias) colsum_finish_k<<<(N + 255) / 256, 256, 0, st>>>(part, db, splits, N);
+}
+
+int rn_bias_act_grad_splits(int M, int N) {
+    int cblocks = (N + 511) / 512;
+    int splits = 1;
+    while (cblocks * splits < 512 && M / (splits * 2) >= 32) splits *= 2;
+    return splits;
+}
+
+}  // extern "C"

@@ -1,0 +1,240 @@
+// Embedding gather / scatter-add (N14) and fused optimizer steps (N12/N13).
+#include "common.h"
+
+namespace {
+
+// x[row] = wte[ids[row]] + wpe[row % T]   — one row per wave, 16-B vectors
+template <bool POS>
+__global__ void __launch_bounds__(256) emb_fwd_k(const int64_t* __restrict__ ids, const bf16* __restrict__ wte,
+                                                 const bf16* __restrict__ wpe, bf16* __restrict__ x, int rows,
+                                                 int T, int E) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long id = ids[row];
+    const int t = row % T;
+    for (int c = lane; c < E / 8; c += 64) {
+        float a[8];
+        load8(wte + id * E + c * 8, a);
+        if constexpr (POS) {
+            float p[8];
+            load8(wpe + (long)t * E + c * 8, p);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] += p[j];
+        }
+        store8(x + (long)row * E + c * 8, a);
+    }
+}
+
+// dwte (fp32, pre-zeroed) += dx rows at ids.  Each wave-instruction adds 64
+// consecutive floats = 256 contiguous bytes (full-rate atomic shape).
+__global__ void __launch_bounds__(256) emb_bwd_scatter_k(const int64_t* __restrict__ ids, const bf16* __restrict__ dx,
+                                                         float* __restrict__ dwte, int rows, int E) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long id = ids[row];
+    for (int c = lane; c < E; c += 64) atomicAdd(dwte + id * E + c, bf2f(dx[(long)row * E + c]));
+}
+
+// dwpe[t] = sum_b dx[b, t]   (thread per column, loops over the batch)
+__global__ void emb_bwd_pos_k(const bf16* __restrict__ dx, bf16* __restrict__ dwpe, int B, int T, int Tp, int E) {
+    const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (i >= (long)Tp * E) return;
+    const int t = i / E, c = i % E;
+    float s = 0.f;
+    if (t < T)
+        for (int b = 0; b < B; ++b) s += bf2f(dx[((long)b * T + t) * E + c]);
+    dwpe[i] = f2bf(s);
+}
+
+__global__ void f32_to_bf16_k(const float* __restrict__ a, bf16* __restrict__ b, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n / 4; i += (long)gridDim.x * blockDim.x) {
+        float4 v = reinterpret_cast<const float4*>(a)[i];
+        bf16x4 o = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+        reinterpret_cast<bf16x4*>(b)[i] = o;
+    }
+    for (long i = (n / 4) * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        b[i] = (bf16)a[i];
+}
+
+// ---- global squared norm: fixed-order two-stage reduction (deterministic) ----
+constexpr int NORM_BLOCKS = 1024;
+
+template <typename T>
+__global__ void __launch_bounds__(256) sumsq_part_k(const T* __restrict__ g, long n, float* __restrict__ part) {
+    __shared__ float sm[16];
+    float s = 0.f;
+    if constexpr (sizeof(T) == 2) {
+        for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+            float f[8];
+            load8((const bf16*)g + i * 8, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+        }
+        for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+            float f = bf2f(((const bf16*)g)[i]);
+            s += f * f;
+        }
+    } else {
+        for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+            float f = ((const float*)g)[i];
+            s += f * f;
+        }
+    }
+    s = block_sum(s, sm);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) sumsq_final_k(const float* __restrict__ part, int np, float* __restrict__ out) {
+    __shared__ float sm[16];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < np; i += 256) s += part[i];
+    s = block_sum(s, sm);
+    if (threadIdx.x == 0) { out[0] = s; out[1] = 0.f; }
+}
+
+// clip coefficient from the device-resident squared norm; <0 means "skip step"
+RN_DEV float clip_coef(const float* normbuf, float grad_scale, float clip) {
+    float nrm = sqrtf(normbuf[0]) * grad_scale;
+    if (!isfinite(nrm)) return -1.f;
+    return (clip > 0.f && nrm > clip) ? clip / (nrm + 1e-6f) : 1.f;
+}
+
+// AdamW over the flat buffer, 8 elements per lane.
+template <typename GT>
+__global__ void __launch_bounds__(256) adamw_k(bf16* __restrict__ p, float* __restrict__ master,
+                                               const GT* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                                               const uint8_t* __restrict__ wdm, float* __restrict__ normbuf, long n,
+                                               float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
+                                               float grad_scale, float clip) {
+    const float coef = clip_coef(normbuf, grad_scale, clip);
+    if (coef < 0.f) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) normbuf[1] = 1.f;  // step skipped (non-finite grads)
+        return;
+    }
+    const float gs = grad_scale * coef;
+    const float rbc1 = 1.f / bc1, rbc2 = 1.f / bc2;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        const long e = i * 8;
+        float gf[8];
+        if constexpr (sizeof(GT) == 2) load8((const bf16*)g + e, gf);
+        else {
+            float4 a = reinterpret_cast<const float4*>(g + e)[0], b = reinterpret_cast<const float4*>(g + e)[1];
+            gf[0] = a.x; gf[1] = a.y; gf[2] = a.z; gf[3] = a.w; gf[4] = b.x; gf[5] = b.y; gf[6] = b.z; gf[7] = b.w;
+        }
+        float4* mm = reinterpret_cast<float4*>(m + e);
+        float4* vv = reinterpret_cast<float4*>(v + e);
+        float4* ww = reinterpret_cast<float4*>(master + e);
+        float4 m0 = mm[0], m1 = mm[1], v0 = vv[0], v1 = vv[1], w0 = ww[0], w1 = ww[1];
+        float mf[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+        float vf[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        float wf[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float wdl = wdm[e >> 6] ? wd : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float gg = gf[j] * gs;
+            mf[j] = b1 * mf[j] + (1.f - b1) * gg;
+            vf[j] = b2 * vf[j] + (1.f - b2) * gg * gg;
+            float upd = (mf[j] * rbc1) / (sqrtf(vf[j] * rbc2) + eps) + wdl * wf[j];
+            wf[j] -= lr * upd;
+        }
+        mm[0] = make_float4(mf[0], mf[1], mf[2], mf[3]);
+        mm[1] = make_float4(mf[4], mf[5], mf[6], mf[7]);
+        vv[0] = make_float4(vf[0], vf[1], vf[2], vf[3]);
+        vv[1] = make_float4(vf[4], vf[5], vf[6], vf[7]);
+        ww[0] = make_float4(wf[0], wf[1], wf[2], wf[3]);
+        ww[1] = make_float4(wf[4], wf[5], wf[6], wf[7]);
+        store8(p + e, wf);
+    }
+}
+
+template <typename GT>
+__global__ void __launch_bounds__(256) sgd_k(bf16* __restrict__ p, float* __restrict__ master, const GT* __restrict__ g,
+                                             float* __restrict__ buf, const uint8_t* __restrict__ wdm,
+                                             float* __restrict__ normbuf, long n, float lr, float mom, float wd,
+                                             int nesterov, int first, float grad_scale, float clip) {
+    const float coef = clip_coef(normbuf, grad_scale, clip);
+    if (coef < 0.f) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) normbuf[1] = 1.f;
+        return;
+    }
+    const float gs = grad_scale * coef;
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+        float gg = (sizeof(GT) == 2 ? bf2f(((const bf16*)g)[e]) : (float)((const float*)g)[e]) * gs;
+        float w = master[e];
+        gg += (wdm[e >> 6] ? wd : 0.f) * w;
+        float b = first ? gg : mom * buf[e] + gg;
+        buf[e] = b;
+        float d = nesterov ? gg + mom * b : b;
+        w -= lr * d;
+        master[e] = w;
+        p[e] = f2bf(w);
+    }
+}
+
+inline int grid_for(long work) {
+    long g = (work + 255) / 256;
+    return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+}  // namespace
+
+extern "C" {
+
+void rn_emb_fwd(const int64_t* ids, const void* wte, const void* wpe, void* x, int rows, int T, int E,
+                hipStream_t st) {
+    dim3 g((rows + 3) / 4);
+    if (wpe) emb_fwd_k<true><<<g, 256, 0, st>>>(ids, (const bf16*)wte, (const bf16*)wpe, (bf16*)x, rows, T, E);
+    else emb_fwd_k<false><<<g, 256, 0, st>>>(ids, (const bf16*)wte, nullptr, (bf16*)x, rows, T, E);
+}
+
+// dwte32: V*E fp32 scratch (zeroed here); dwte: bf16 out; dwpe: bf16 (Tp*E) or null
+void rn_emb_bwd(const int64_t* ids, const void* dx, float* dwte32, void* dwte, void* dwpe, int B, int T, int Tp,
+                int V, int E, hipStream_t st) {
+    int rows = B * T;
+    (void)hipMemsetAsync(dwte32, 0, (size_t)V * E * 4, st);
+    emb_bwd_scatter_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (const bf16*)dx, dwte32, rows, E);
+    long n = (long)V * E;
+    f32_to_bf16_k<<<grid_for(n / 4), 256, 0, st>>>(dwte32, (bf16*)dwte, n);
+    if (dwpe) emb_bwd_pos_k<<<rn_cdiv((long)Tp * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)dwpe, B, T, Tp, E);
+}
+
+int rn_norm_ws_floats() { return NORM_BLOCKS; }
+
+// normbuf[0] = sum(g^2), normbuf[1] = 0 (skip flag); part: NORM_BLOCKS floats
+void rn_sumsq(const void* g, long n, int is_bf16, float* part, float* normbuf, hipStream_t st) {
+    int gb = grid_for(n / 8);
+    if (gb > NORM_BLOCKS) gb = NORM_BLOCKS;
+    if (is_bf16) sumsq_part_k<bf16><<<gb, 256, 0, st>>>((const bf16*)g, n, part);
+    else sumsq_part_k<float><<<gb, 256, 0, st>>>((const float*)g, n, part);
+    sumsq_final_k<<<1, 256, 0, st>>>(part, gb, normbuf);
+}
+
+int rn_adamw(void* p, float* master, const void* g, int g_bf16, float* m, float* v, const uint8_t* wdm,
+             float* normbuf, long n, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
+             float grad_scale, float clip, hipStream_t st) {
+    if (n % 8) return -1;
+    int gb = grid_for(n / 8);
+    if (g_bf16)
+        adamw_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, m, v, wdm, normbuf, n, lr, b1, b2, eps,
+                                          wd, bc1, bc2, grad_scale, clip);
+    else
+        adamw_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, m, v, wdm, normbuf, n, lr, b1, b2, eps,
+                                           wd, bc1, bc2, grad_scale, clip);
+    return 0;
+}
+
+void rn_sgd(void* p, float* master, const void* g, int g_bf16, float* buf, const uint8_t* wdm, float* normbuf,
+            long n, float lr, float mom, float wd, int nesterov, int first, float grad_scale, float clip,
+            hipStream_t st) {
+    int gb = grid_for(n);
+    if (g_bf16)
+        sgd_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, buf, wdm, normbuf, n, lr, mom, wd, nesterov,
+                                        first, grad_scale, clip);
+    else
+        sgd_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, buf, wdm, normbuf, n, lr, mom, wd,
+                                         nesterov, first, grad_scale, clip);
+}
+
+}  // extern "C"

@@ -1,0 +1,153 @@
+// Row softmax (N8) and fused softmax cross-entropy (N9).
+//
+// Softmax: one 256-thread block per row, online (max, sum) in one pass over
+// 16-byte vectors, normalised write in a second pass.
+// Cross-entropy: forward reads each logits row ONCE (online log-sum-exp with
+// one rescale per 8 elements) and stores only the per-row lse + NLL; backward
+// writes (softmax - onehot) * g / n in place over the logits, zero in the
+// padded columns [n_valid, V).
+#include "common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+RN_DEV void online_update(float& m, float& s, const float* f, int cnt) {
+    float lm = f[0];
+    for (int j = 1; j < cnt; ++j) lm = fmaxf(lm, f[j]);
+    float nm = fmaxf(m, lm);
+    float acc = (m == -INFINITY) ? 0.f : s * __expf(m - nm);
+    for (int j = 0; j < cnt; ++j) acc += __expf(f[j] - nm);
+    m = nm;
+    s = acc;
+}
+
+// reduce (m, s) pairs across the block
+RN_DEV void block_reduce_ms(float& m, float& s, float* sm) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+        float nm = fmaxf(m, om);
+        float a = (m == -INFINITY) ? 0.f : s * __expf(m - nm);
+        float b = (om == -INFINITY) ? 0.f : os * __expf(om - nm);
+        m = nm;
+        s = a + b;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) { sm[wid] = m; sm[8 + wid] = s; }
+    __syncthreads();
+    float M = -INFINITY;
+    for (int i = 0; i < TPB / 64; ++i) M = fmaxf(M, sm[i]);
+    float S = 0.f;
+    for (int i = 0; i < TPB / 64; ++i) S += (sm[i] == -INFINITY) ? 0.f : sm[8 + i] * __expf(sm[i] - M);
+    m = M;
+    s = S;
+}
+
+// row statistics over columns [0, n) of a row (scaled by `scale`)
+RN_DEV void row_ms(const bf16* row, int n, float scale, float& m, float& s, float* sm) {
+    m = -INFINITY;
+    s = 0.f;
+    const bool vec = ((reinterpret_cast<uintptr_t>(row) & 15) == 0);
+    int n8 = vec ? n / 8 : 0;
+    for (int i = threadIdx.x; i < n8; i += TPB) {
+        float f[8];
+        load8(row + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= scale;
+        online_update(m, s, f, 8);
+    }
+    for (int i = n8 * 8 + threadIdx.x; i < n; i += TPB) {
+        float f = bf2f(row[i]) * scale;
+        online_update(m, s, &f, 1);
+    }
+    block_reduce_ms(m, s, sm);
+}
+
+__global__ void __launch_bounds__(TPB) softmax_fwd_k(const bf16* __restrict__ x, bf16* __restrict__ y, int N,
+                                                     float scale) {
+    __shared__ float sm[16];
+    const bf16* xr = x + (long)blockIdx.x * N;
+    bf16* yr = y + (long)blockIdx.x * N;
+    float m, s;
+    row_ms(xr, N, scale, m, s, sm);
+    const float inv = 1.f / s;
+    for (int i = threadIdx.x; i < N; i += TPB) yr[i] = f2bf(__expf(bf2f(xr[i]) * scale - m) * inv);
+}
+
+__global__ void __launch_bounds__(TPB) softmax_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                     bf16* __restrict__ dx, int N, float scale) {
+    __shared__ float sm[16];
+    const long base = (long)blockIdx.x * N;
+    float d = 0.f;
+    for (int i = threadIdx.x; i < N; i += TPB) d += bf2f(dy[base + i]) * bf2f(y[base + i]);
+    d = block_sum(d, sm);
+    for (int i = threadIdx.x; i < N; i += TPB)
+        dx[base + i] = f2bf(scale * bf2f(y[base + i]) * (bf2f(dy[base + i]) - d));
+}
+
+__global__ void __launch_bounds__(TPB) xent_fwd_k(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                  float* __restrict__ loss, float* __restrict__ lse_out, int V,
+                                                  int nvalid, long ignore) {
+    __shared__ float sm[16];
+    const bf16* row = logits + (long)blockIdx.x * V;
+    float m, s;
+    row_ms(row, nvalid, 1.f, m, s, sm);
+    if (threadIdx.x == 0) {
+        float lse = m + __logf(s);
+        lse_out[blockIdx.x] = lse;
+        long t = tgt[blockIdx.x];
+        loss[blockIdx.x] = (t == ignore || t < 0 || t >= nvalid) ? 0.f : lse - bf2f(row[t]);
+    }
+}
+
+__global__ void __launch_bounds__(TPB) xent_bwd_k(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                  const float* __restrict__ lse, const float* __restrict__ gscale,
+                                                  bf16* __restrict__ grad, int V, int nvalid, long ignore) {
+    const long base = (long)blockIdx.x * V;
+    const long t = tgt[blockIdx.x];
+    const bool ign = (t == ignore);
+    const float L = lse[blockIdx.x];
+    const float g = ign ? 0.f : gscale[0];
+    const bool vec = (V % 8 == 0);
+    if (vec) {
+        for (int i = threadIdx.x; i < V / 8; i += TPB) {
+            float f[8];
+            load8(logits + base + i * 8, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                int c = i * 8 + j;
+                float p = c < nvalid ? __expf(f[j] - L) : 0.f;
+                f[j] = (p - (c == t ? 1.f : 0.f)) * g;
+            }
+            store8(grad + base + i * 8, f);
+        }
+    } else {
+        for (int c = threadIdx.x; c < V; c += TPB) {
+            float p = c < nvalid ? __expf(bf2f(logits[base + c]) - L) : 0.f;
+            grad[base + c] = f2bf((p - (c == t ? 1.f : 0.f)) * g);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+void rn_softmax_fwd(const void* x, void* y, int M, int N, float scale, hipStream_t st) {
+    softmax_fwd_k<<<M, TPB, 0, st>>>((const bf16*)x, (bf16*)y, N, scale);
+}
+void rn_softmax_bwd(const void* dy, const void* y, void* dx, int M, int N, float scale, hipStream_t st) {
+    softmax_bwd_k<<<M, TPB, 0, st>>>((const bf16*)dy, (const bf16*)y, (bf16*)dx, N, scale);
+}
+void rn_xent_fwd(const void* logits, const int64_t* tgt, float* loss, float* lse, int M, int V, int nvalid,
+                 long ignore, hipStream_t st) {
+    xent_fwd_k<<<M, TPB, 0, st>>>((const bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
+}
+void rn_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* grad, int M,
+                 int V, int nvalid, long ignore, hipStream_t st) {
+    xent_bwd_k<<<M, TPB, 0, st>>>((const bf16*)logits, tgt, lse, gscale, (bf16*)grad, V, nvalid, ignore);
+}
+
+}  // extern "C"

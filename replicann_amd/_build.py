@@ -1,0 +1,115 @@
+"""In-tree native build for the gfx950 extension ``replicann_amd/_C.so``.
+
+There is no native code in the reference; this is the N1
+component: every ``csrc/kernels/*.hip`` is compiled by ``hipcc
+--offload-arch=gfx950`` as a plain HIP translation unit (no torch headers, so
+they build in seconds), ``csrc/bindings/*.cpp`` register the ops with the
+PyTorch dispatcher (``TORCH_LIBRARY(replicann, ...)``), and everything is
+linked into one shared object next to this file.  The ``.so`` travels with the
+repo snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+
+Rebuilds are incremental: each object is keyed by a hash of its source, the
+shared headers and the flags.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "objs"
+OUT = Path(__file__).resolve().parent / "_C.so"
+ARCH = os.environ.get("REPLICANN_ARCH", "gfx950")
+
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-fPIC",
+    "-std=c++17",
+    "-ffp-contract=fast",
+    "-munsafe-fp-atomics",
+    "-Wno-unused-result",
+]
+
+
+def _torch_paths():
+    import torch
+
+    tdir = Path(torch.__file__).resolve().parent
+    inc = [tdir / "include", tdir / "include" / "torch" / "csrc" / "api" / "include"]
+    lib = tdir / "lib"
+    return inc, lib
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the gfx950 extension cannot be built")
+
+
+def _headers_digest() -> str:
+    h = hashlib.sha1()
+    for p in sorted((CSRC / "include").glob("*.h")):
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _compile(src: Path, hdr: str, torch_inc) -> Path:
+    is_binding = src.suffix == ".cpp"
+    flags = list(HIP_FLAGS) + [f"-I{CSRC / 'include'}"]
+    if is_binding:
+        # host-only TU: torch headers, no device code
+        flags = [f for f in flags if not f.startswith("--offload-arch")]
+        flags += ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-O2"]
+        flags += [f"-I{p}" for p in torch_inc]
+    key = hashlib.sha1((src.read_text() + hdr + " ".join(flags)).encode()).hexdigest()[:16]
+    obj = BUILD / f"{src.stem}.{key}.o"
+    if obj.exists():
+        return obj
+    cmd = [_hipcc()] + flags + ["-c", str(src), "-o", str(obj) + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+    os.replace(str(obj) + ".tmp", obj)
+    return obj
+
+
+def build(verbose: bool = True, jobs: int | None = None) -> Path:
+    """Compile every kernel + binding and link ``_C.so``. Returns its path."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    torch_inc, torch_lib = _torch_paths()
+    hdr = _headers_digest()
+    srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "bindings").glob("*.cpp"))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr, torch_inc), srcs))
+    link_key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
+    stamp = OUT.with_suffix(".stamp")
+    if OUT.exists() and stamp.exists() and stamp.read_text() == link_key:
+        if verbose:
+            print(f"[replicann build] up to date: {OUT}")
+        return OUT
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(OUT) + ".tmp",
+           f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+           f"-Wl,-rpath,{torch_lib}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    os.replace(str(OUT) + ".tmp", OUT)
+    stamp.write_text(link_key)
+    if verbose:
+        print(f"[replicann build] linked {OUT} from {len(objs)} objects")
+    return OUT
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

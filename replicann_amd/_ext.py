@@ -1,0 +1,74 @@
+"""Loader for the gfx950 extension (``_C.so``) and the device-path policy.
+
+Two execution paths only: HIP kernels for tensors on the
+GPU, plain ATen for CPU tensors.  On a GPU the native library is REQUIRED:
+if ``_C.so`` is missing or fails to load, every op raises instead of silently
+falling back to PyTorch.  (``REPLICANN_ALLOW_ATEN_FALLBACK=1`` exists only for
+the stock-PyTorch comparison bench and is never set by tests.)
+"""
+
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import torch
+
+_SO = Path(__file__).resolve().parent / "_C.so"
+_state = {"loaded": False, "error": None}
+
+
+def load() -> bool:
+    if _state["loaded"]:
+        return True
+    if _state["error"] is not None:
+        return False
+    try:
+        if not _SO.exists():
+            raise FileNotFoundError(f"{_SO} not built (run `python -m replicann_amd._build`)")
+        torch.ops.load_library(str(_SO))
+        _state["loaded"] = True
+    except Exception as e:  # pragma: no cover - depends on build state
+        _state["error"] = e
+    return _state["loaded"]
+
+
+def available() -> bool:
+    return load()
+
+
+def load_error():
+    load()
+    return _state["error"]
+
+
+def ops():
+    if not load():
+        raise RuntimeError(f"replicann native extension unavailable: {_state['error']}")
+    return torch.ops.replicann
+
+
+def aten_fallback_allowed() -> bool:
+    return os.environ.get("REPLICANN_ALLOW_ATEN_FALLBACK", "0") == "1"
+
+
+def use_native(*tensors) -> bool:
+    """True if this call must run on the HIP kernels.
+
+    CPU tensors -> False (ATen path).  GPU tensors -> True, and the library
+    must load; otherwise raise (no silent fallback on a GPU box).
+    """
+    dev = None
+    for t in tensors:
+        if isinstance(t, torch.Tensor):
+            dev = t.device
+            break
+    if dev is None or dev.type != "cuda":
+        return False
+    if aten_fallback_allowed():
+        return False
+    if not load():
+        raise RuntimeError(
+            f"GPU tensor passed to a replicann op but the gfx950 extension did not load: {_state['error']}"
+        )
+    return True

@@ -1,0 +1,8 @@
+"""Replicated model families (N17–N20)."""
+
+from .gpt2 import GPT2, GPT2Config
+from .mlp import MLP
+from .resnet import ResNet18
+from .vit import ViT, ViTConfig
+
+__all__ = ["GPT2", "GPT2Config", "MLP", "ResNet18", "ViT", "ViTConfig"]

@@ -1,0 +1,97 @@
+"""Pre-LN transformer block shared by GPT-2 and ViT (N19/N20).
+
+Unlike the reference's post-LN blocks (``arch/transformer.py``) this is the
+GPT-2/ViT formulation: fused c_attn with bias, scale 1/sqrt(head_dim), GELU
+(tanh) MLP, residual adds fused into the output-projection GEMM epilogues:
+
+    h   = LN1(x)                               layernorm kernel
+    qkv = h·Wqkvᵀ + b                          GEMM (bias epilogue)
+    a   = attention(qkv)  (causal for GPT-2)   flash fwd/bwd kernels
+    x   = x + a·Wprojᵀ + b                     GEMM (bias + residual epilogue)
+    h   = LN2(x)
+    u   = gelu(h·Wfcᵀ + b)                     GEMM (bias + GELU epilogue)
+    x   = x + u·Wfc2ᵀ + b                      GEMM (bias + residual epilogue)
+
+Six kernel launches per block forward (plus dropout when enabled).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class Linear(nn.Module):
+    """nn.Linear-compatible parameters (weight (out, in), bias (out,)) on the MFMA GEMM."""
+
+    def __init__(self, in_features, out_features, bias=True, std=0.02):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
+        nn.init.normal_(self.weight, std=std)
+
+    def forward(self, x, act=None, residual=None):
+        return ops.linear(x, self.weight, self.bias, act=act, residual=residual)
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, n, eps=1e-5):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(n))
+        self.bias = nn.Parameter(torch.zeros(n))
+        self.eps = eps
+
+    def forward(self, x):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class Attention(nn.Module):
+    def __init__(self, n_embd, n_head, causal, attn_dropout=0.0, resid_dropout=0.0, n_layer=12):
+        super().__init__()
+        self.n_head, self.causal = n_head, causal
+        self.c_attn = Linear(n_embd, 3 * n_embd)
+        self.c_proj = Linear(n_embd, n_embd, std=0.02 / math.sqrt(2 * n_layer))
+        self.attn_dropout, self.resid_dropout = attn_dropout, resid_dropout
+
+    def forward(self, h, residual):
+        B, T, E = h.shape
+        qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
+        a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
+                                 training=self.training)
+        a = a.reshape(B, T, E)
+        if self.resid_dropout > 0 and self.training:
+            return residual + ops.dropout(self.c_proj(a), self.resid_dropout, True)
+        return self.c_proj(a, residual=residual)
+
+
+class MLP(nn.Module):
+    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12):
+        super().__init__()
+        self.c_fc = Linear(n_embd, hidden)
+        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer))
+        self.dropout = dropout
+
+    def forward(self, h, residual):
+        u = self.c_fc(h, act="gelu")
+        if self.dropout > 0 and self.training:
+            return residual + ops.dropout(self.c_proj(u), self.dropout, True)
+        return self.c_proj(u, residual=residual)
+
+
+class PreLNBlock(nn.Module):
+    def __init__(self, n_embd, n_head, causal, mlp_ratio=4, dropout=0.0, n_layer=12, eps=1e-5):
+        super().__init__()
+        self.ln_1 = LayerNorm(n_embd, eps)
+        self.attn = Attention(n_embd, n_head, causal, dropout, dropout, n_layer)
+        self.ln_2 = LayerNorm(n_embd, eps)
+        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer)
+
+    def forward(self, x):
+        x = self.attn(self.ln_1(x), residual=x)
+        x = self.mlp(self.ln_2(x), residual=x)
+        return x

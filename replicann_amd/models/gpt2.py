@@ -1,0 +1,106 @@
+"""GPT-2 (small 124M / medium 355M) — N19, the headline model of BASELINE.json.
+
+Absent from the reference: built here from its standard
+definition — learned token + position embeddings, pre-LN blocks with fused
+c_attn (bias), true causal attention with scale 1/sqrt(head_dim), tanh-GELU
+MLP, final LayerNorm and an LM head tied to the token embedding.
+
+MI355X-specific choices:
+  * the token-embedding / LM-head matrix is STORED with 50304 = 393·128 rows
+    (MFMA tile multiple); rows ≥ 50257 are zero, never indexed, and masked out
+    of the softmax by the fused cross-entropy (``n_valid_cols``), so the model
+    is mathematically the 50257-vocab GPT-2;
+  * the loss path never materialises fp32 logits: bf16 logits from the GEMM,
+    log-sum-exp in the fused CE kernel, gradient written in place.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .blocks import LayerNorm, PreLNBlock
+
+
+@dataclass(frozen=True)
+class GPT2Config:
+    n_layer: int = 12
+    n_head: int = 12
+    n_embd: int = 768
+    block_size: int = 1024
+    vocab_size: int = 50257
+    vocab_pad: int = 50304
+    dropout: float = 0.0
+    ln_eps: float = 1e-5
+
+    @staticmethod
+    def small(**kw):
+        return GPT2Config(**kw)
+
+    @staticmethod
+    def medium(**kw):
+        return GPT2Config(n_layer=24, n_head=16, n_embd=1024, **kw)
+
+    @staticmethod
+    def tiny(**kw):
+        """Test-size config (same code paths)."""
+        d = dict(n_layer=2, n_head=4, n_embd=128, block_size=128, vocab_size=1000, vocab_pad=1024)
+        d.update(kw)
+        return GPT2Config(**d)
+
+
+class GPT2(nn.Module):
+    def __init__(self, config: GPT2Config | None = None, **kw):
+        super().__init__()
+        cfg = config or GPT2Config(**kw)
+        self.config = cfg
+        self.wte = nn.Parameter(torch.empty(cfg.vocab_pad, cfg.n_embd))
+        self.wpe = nn.Parameter(torch.empty(cfg.block_size, cfg.n_embd))
+        nn.init.normal_(self.wte, std=0.02)
+        nn.init.normal_(self.wpe, std=0.01)
+        with torch.no_grad():
+            self.wte[cfg.vocab_size:].zero_()
+        self.h = nn.ModuleList(
+            PreLNBlock(cfg.n_embd, cfg.n_head, causal=True, dropout=cfg.dropout, n_layer=cfg.n_layer,
+                       eps=cfg.ln_eps)
+            for _ in range(cfg.n_layer)
+        )
+        self.ln_f = LayerNorm(cfg.n_embd, cfg.ln_eps)
+
+    def num_params(self, non_embedding=False):
+        n = sum(p.numel() for p in self.parameters())
+        n -= (self.wte.shape[0] - self.config.vocab_size) * self.config.n_embd  # zero pad rows
+        if non_embedding:
+            n -= self.wpe.numel()
+        return n
+
+    def hidden(self, idx):
+        x = ops.embedding(idx, self.wte, self.wpe)
+        if self.config.dropout > 0 and self.training:
+            x = ops.dropout(x, self.config.dropout, True)
+        for blk in self.h:
+            x = blk(x)
+        return self.ln_f(x)
+
+    def forward(self, idx, targets=None):
+        """idx (B, T) → logits (B, T, vocab_pad) [, mean CE loss when targets given].
+
+        With ``targets`` only the loss is returned (logits are consumed in place).
+        """
+        h = self.hidden(idx)
+        logits = ops.linear(h, self.wte)
+        if targets is None:
+            return logits[..., : self.config.vocab_size]
+        return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1),
+                                 n_valid_cols=self.config.vocab_size, inplace_grad=True)
+
+    def flops_per_token(self, T=None):
+        """Training FLOPs per token (fwd+bwd): 6·N_matmul + attention (causal)."""
+        c = self.config
+        T = T or c.block_size
+        n_mm = c.n_layer * 12 * c.n_embd**2 + c.vocab_size * c.n_embd
+        attn = c.n_layer * 2 * 2 * T * c.n_embd * 0.5  # fwd, causal ≈ half
+        return 6 * n_mm + 3 * attn

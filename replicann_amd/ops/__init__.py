@@ -1,0 +1,17 @@
+"""Autograd-level ops.  GPU tensors → gfx950 HIP kernels (``replicann_amd/_C.so``);
+CPU tensors → plain ATen with the same math.  No other backends."""
+
+from .activation import dropout, gelu, relu, softmax
+from .attention import attention, attention_packed, attention_reference, mask_to_bias
+from .conv import conv2d_nhwc
+from .embedding import embedding
+from .linear import ACT_GELU, ACT_NONE, ACT_RELU, gemm, linear
+from .loss import cross_entropy
+from .norm import batch_norm_nhwc, layer_norm
+from .pool import avgpool_nhwc, maxpool_nhwc
+
+__all__ = [
+    "attention", "attention_packed", "attention_reference", "mask_to_bias", "avgpool_nhwc",
+    "batch_norm_nhwc", "conv2d_nhwc", "cross_entropy", "dropout", "embedding", "gelu", "gemm",
+    "layer_norm", "linear", "maxpool_nhwc", "relu", "softmax", "ACT_GELU", "ACT_NONE", "ACT_RELU",
+]

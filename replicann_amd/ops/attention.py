@@ -1,0 +1,147 @@
+"""Fused scaled-dot-product attention (csrc/kernels/attention.hip).
+
+Replaces the reference's per-head Python loop
+(``src/replicann/nn/attention.py:28-50`` — ``q@kᵀ*scale`` → mask → softmax →
+dropout → ``@v`` — called once per head at ``:180``) with one flash-style
+kernel over all (batch, head) pairs: scores never reach HBM, the online softmax
+runs in registers, dropout is a counter-based in-kernel RNG regenerated in the
+backward, and the backward recomputes P from the saved log-sum-exp.
+
+Layout is "token-major, heads interleaved": q, k, v are (B, T, H, D) views
+straight out of the fused QKV GEMM (row stride 3·H·D), and the output is
+(B, T, H, D) contiguous — i.e. already the (B, T, H·D) input of the output
+projection, so the reference's ``torch.cat`` of heads disappears.
+
+Supported semantics (all needed for reference parity, SURVEY.md §2.1 Q1–Q4):
+  * arbitrary ``scale`` (the reference uses 1/sqrt(embedding_size), Q1);
+  * ``causal`` — true causal tile skipping (GPT-2);
+  * ``bias`` — an additive float mask (B|1, Tq, Tk) (the reference's 0/1
+    "tril" float mask is *added*, Q2; bool masks become -inf biases);
+  * ``dropout_p`` on the attention probabilities (Q4).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+
+def mask_to_bias(mask, dtype=torch.float32):
+    """Reference mask semantics → additive bias.
+
+    bool: True = masked out (-inf), ``nn/attention.py:39-40``;
+    float (any float dtype — the reference only accepts fp32, Q3): added as-is.
+    """
+    if mask is None:
+        return None
+    if mask.dtype == torch.bool:
+        return torch.zeros(mask.shape, dtype=dtype, device=mask.device).masked_fill(mask, float("-inf"))
+    if mask.is_floating_point():
+        return mask.to(dtype)
+    raise TypeError(f"Unexpected type `{mask.dtype}` of the `mask`.")
+
+
+def _bias_3d(bias, B, Tq, Tk):
+    if bias is None:
+        return None
+    b = bias
+    while b.dim() < 3:
+        b = b.unsqueeze(0)
+    if b.dim() > 3:
+        b = b.reshape(-1, b.shape[-2], b.shape[-1])
+    return b.expand(b.shape[0] if b.shape[0] in (1, B) else B, Tq, Tk).float().contiguous()
+
+
+def attention_reference(q, k, v, scale, causal=False, bias=None, dropout_p=0.0, training=False):
+    """fp32 math reference in the (B, T, H, D) layout."""
+    qt = q.transpose(1, 2).float()
+    kt = k.transpose(1, 2).float()
+    vt = v.transpose(1, 2).float()
+    w = qt @ kt.transpose(-2, -1) * scale
+    if bias is not None:
+        b = bias.float()
+        if b.dim() == 3:
+            b = b.unsqueeze(1)
+        w = w + b
+    if causal:
+        Tq, Tk = w.shape[-2], w.shape[-1]
+        m = torch.ones(Tq, Tk, dtype=torch.bool, device=w.device).triu(1 + Tk - Tq)
+        w = w.masked_fill(m, float("-inf"))
+    p = torch.softmax(w, dim=-1)
+    if dropout_p > 0 and training:
+        p = torch.nn.functional.dropout(p, dropout_p, True)
+    o = p @ vt
+    return o.transpose(1, 2).to(q.dtype)
+
+
+class _AttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, bias, scale, causal, dropout_p, seed):
+        o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, seed)
+        ctx.save_for_backward(q, k, v, o, lse, bias)
+        ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed = scale, causal, dropout_p, seed
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, bias = ctx.saved_tensors
+        dq, dk, dv = _ext.ops().attn_bwd(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
+                                         ctx.dropout_p, ctx.seed)
+        return dq, dk, dv, None, None, None, None, None
+
+
+def attention(q, k, v, *, scale=None, causal=False, bias=None, mask=None, dropout_p=0.0,
+              training=False):
+    """O = softmax(q·kᵀ·scale + bias [causal]) [dropout] · v, all in (B, T, H, D)."""
+    B, Tq, H, D = q.shape
+    Tk = k.shape[1]
+    if scale is None:
+        scale = D ** -0.5
+    if mask is not None:
+        bias = mask_to_bias(mask) if bias is None else bias + mask_to_bias(mask)
+    p = dropout_p if training else 0.0
+    if _ext.use_native(q):
+        b3 = _bias_3d(bias, B, Tq, Tk)
+        seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+        return _AttnFn.apply(q, k, v, b3, float(scale), bool(causal), float(p), seed)
+    return attention_reference(q, k, v, scale, causal, bias, p, training)
+
+
+class _AttnPackedFn(torch.autograd.Function):
+    """Attention on a packed (B, T, 3, H, D) QKV tensor; backward writes one packed dQKV."""
+
+    @staticmethod
+    def forward(ctx, qkv, bias, scale, causal, dropout_p, seed):
+        q, k, v = qkv.unbind(2)
+        o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, seed)
+        ctx.save_for_backward(qkv, o, lse, bias)
+        ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed = scale, causal, dropout_p, seed
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, bias = ctx.saved_tensors
+        q, k, v = qkv.unbind(2)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = dqkv.unbind(2)
+        _ext.ops().attn_bwd_out(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
+                                ctx.dropout_p, ctx.seed, dq, dk, dv)
+        return dqkv, None, None, None, None, None
+
+
+def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dropout_p=0.0,
+                     training=False):
+    """Attention over a packed (B, T, 3, H, D) tensor → (B, T, H, D)."""
+    B, T, three, H, D = qkv.shape
+    if scale is None:
+        scale = D ** -0.5
+    if mask is not None:
+        bias = mask_to_bias(mask) if bias is None else bias + mask_to_bias(mask)
+    p = dropout_p if training else 0.0
+    if _ext.use_native(qkv):
+        b3 = _bias_3d(bias, B, T, T)
+        seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+        return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed)
+    q, k, v = qkv.unbind(2)
+    return attention_reference(q, k, v, scale, causal, bias, p, training)

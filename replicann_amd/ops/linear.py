@@ -1,0 +1,152 @@
+"""Linear layers on the gfx950 MFMA GEMM (csrc/kernels/gemm_bf16.hip).
+
+Replaces the reference's per-head ``nn.Linear`` launches
+(reference ``src/replicann/nn/attention.py:135-137``, ``arch/transformer.py:29-31``)
+with one GEMM per projection whose epilogue fuses bias, activation
+(ReLU / tanh-GELU), residual add and bf16 down-cast.
+
+Backward = one dgrad GEMM (dX = dH·W, "NN") + one wgrad GEMM
+(dW = dHᵀ·X, "TN", split-K over the token dimension) + a fused
+activation-backward / bias-gradient reduction kernel.  All three GEMM layouts
+run on the same kernel: K-contiguous operands are read from LDS with
+``ds_read_b128``, M/N-contiguous ones with the ``ds_read_b64_tr_b16``
+hardware transpose, so no operand is ever transposed in HBM.
+
+CPU tensors take the plain ATen path (same math, fp32 accumulation).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+_ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU}
+
+
+def _act_ref(h: torch.Tensor, act: int) -> torch.Tensor:
+    if act == ACT_RELU:
+        return F.relu(h)
+    if act == ACT_GELU:
+        return F.gelu(h, approximate="tanh")
+    return h
+
+
+def _act_grad_ref(dy: torch.Tensor, h: torch.Tensor, act: int) -> torch.Tensor:
+    if act == ACT_RELU:
+        return dy * (h > 0).to(dy.dtype)
+    if act == ACT_GELU:
+        hf = h.float()
+        c = math.sqrt(2.0 / math.pi)
+        u = c * (hf + 0.044715 * hf**3)
+        t = torch.tanh(u)
+        d = 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * c * (1 + 3 * 0.044715 * hf * hf)
+        return (dy.float() * d).to(dy.dtype)
+    return dy
+
+
+# --------------------------------------------------------------------------
+# raw GEMM entry point (used by linear, conv2d, attention fallbacks)
+# --------------------------------------------------------------------------
+def gemm(a, b, *, ta=False, tb=False, bias=None, residual=None, act=ACT_NONE, preact=None,
+         out=None, accumulate=False, split_k=0, out_dtype=None):
+    """C = act(op(A) @ op(B) + bias) + residual  (op = transpose if flag set).
+
+    A, B are 2-D row-major bf16.  On CPU it is the ATen reference.
+    ``accumulate`` adds into ``out`` (fp32 or bf16) instead of overwriting.
+    """
+    if _ext.use_native(a):
+        return _ext.ops().gemm(a, b, ta, tb, bias, residual, act, preact, out, accumulate, split_k,
+                               out_dtype == torch.float32)
+    A = a.t() if ta else a
+    B = b.t() if tb else b
+    h = A.float() @ B.float()
+    if bias is not None:
+        h = h + bias.float()
+    if preact is not None:
+        preact.copy_(h)
+    y = _act_ref(h, act)
+    if residual is not None:
+        y = y + residual.float()
+    dt = out_dtype or (out.dtype if out is not None else a.dtype)
+    if out is not None:
+        if accumulate:
+            out.add_(y.to(out.dtype))
+        else:
+            out.copy_(y)
+        return out
+    return y.to(dt)
+
+
+def bias_act_grad(dy2d, h2d, act, want_bias):
+    """dH = dY ⊙ act'(H) and db = Σ_rows dH in one pass (fused kernel on GPU)."""
+    if _ext.use_native(dy2d):
+        dh, db = _ext.ops().bias_act_grad(dy2d, h2d if act != ACT_NONE else None, act, want_bias)
+        return dh, (db if want_bias else None)
+    dh = _act_grad_ref(dy2d, h2d, act) if act != ACT_NONE else dy2d
+    db = dh.float().sum(0) if want_bias else None
+    return dh, db
+
+
+def _pick_split_k(m_out: int, n_out: int, k: int) -> int:
+    tiles = math.ceil(m_out / 128) * math.ceil(n_out / 128)
+    if tiles >= 512 or k < 1024:
+        return 1
+    s = 1
+    while tiles * s < 512 and k // (s * 2) >= 512:
+        s *= 2
+    return s
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, act, residual):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        res2 = residual.reshape(-1, weight.shape[0]) if residual is not None else None
+        native = _ext.use_native(x2)
+        preact = None
+        if act != ACT_NONE:
+            preact = torch.empty(x2.shape[0], weight.shape[0], device=x.device, dtype=x.dtype)
+        if native:
+            y = _ext.ops().gemm(x2, weight, False, True, bias, res2, act, preact, None, False, 0, False)
+        else:
+            y = gemm(x2, weight, tb=True, bias=bias, residual=res2, act=act, preact=preact,
+                     out_dtype=x.dtype)
+        ctx.save_for_backward(x2, weight, preact)
+        ctx.act = act
+        ctx.has_bias = bias is not None
+        ctx.has_res = residual is not None
+        ctx.shp = shp
+        return y.reshape(*shp[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight, preact = ctx.saved_tensors
+        gy2 = gy.reshape(-1, weight.shape[0])
+        if not gy2.is_contiguous():
+            gy2 = gy2.contiguous()
+        dh, db = bias_act_grad(gy2, preact, ctx.act, ctx.has_bias)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            sk = _pick_split_k(weight.shape[0], weight.shape[1], x2.shape[0])
+            gw = gemm(dh, x2, ta=True, split_k=sk, out_dtype=weight.dtype)
+        gb = db.to(weight.dtype) if (db is not None and ctx.needs_input_grad[2]) else None
+        gres = gy if ctx.has_res else None
+        return gx, gw, gb, None, gres
+
+
+def linear(x, weight, bias=None, act=None, residual=None):
+    """y = act(x @ weightᵀ + bias) [+ residual].  ``act`` ∈ {None,'relu','gelu'}."""
+    a = _ACTS[act] if not isinstance(act, int) else act
+    if not x.is_cuda and not torch.is_grad_enabled() and residual is None and a == ACT_NONE:
+        return F.linear(x, weight, bias)
+    return _LinearFn.apply(x, weight, bias, a, residual)

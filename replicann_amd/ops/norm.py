@@ -1,0 +1,107 @@
+"""LayerNorm and BatchNorm on gfx950 (csrc/kernels/layernorm.hip, batchnorm.hip).
+
+LayerNorm replaces ``nn.LayerNorm`` used at reference
+``arch/transformer.py:65,72,188`` (post-LN ``LN(x + sublayer(x))``,
+``:111-112,149-150,198-200``).  The kernel handles one row per wave (E ≤ 8192,
+bf16 vectorised 16-B loads, fp32 statistics) and optionally fuses the residual
+add in forward (h = x + r; y = LN(h), h is returned for the backward) and the
+residual-gradient add in backward.
+
+BatchNorm2d (N11; needed by ResNet-18, absent from the reference) works on
+NHWC activations with a fused ReLU.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+
+
+class _LayerNormFn(torch.autograd.Function):
+    """y = LN(x [+ residual]); with a residual the pre-norm sum h is a 2nd output."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, residual):
+        shp = x.shape
+        E = shp[-1]
+        x2 = x.reshape(-1, E).contiguous()
+        r2 = residual.reshape(-1, E).contiguous() if residual is not None else None
+        y, h, mean, rstd = _ext.ops().layernorm_fwd(x2, r2, weight, bias, eps)
+        ctx.save_for_backward(x2 if residual is None else h, weight, mean, rstd)
+        ctx.has_res = residual is not None
+        ctx.has_bias = bias is not None
+        ctx.shp = shp
+        if residual is not None:
+            return y.reshape(shp), h.reshape(shp)
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, gy, gh=None):
+        h, weight, mean, rstd = ctx.saved_tensors
+        E = ctx.shp[-1]
+        gy2 = gy.reshape(-1, E).contiguous()
+        gh2 = gh.reshape(-1, E).contiguous() if gh is not None else None
+        dx, dw, db = _ext.ops().layernorm_bwd(gy2, gh2, h, weight, mean, rstd)
+        dx = dx.reshape(ctx.shp)
+        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None,
+                dx if ctx.has_res else None)
+
+
+def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False):
+    """LayerNorm over the last dim.  With ``residual``: h = x + residual, y = LN(h).
+
+    Returns y, or (y, h) when ``return_sum``.
+    """
+    if _ext.use_native(x):
+        if residual is None:
+            y = _LayerNormFn.apply(x, weight, bias, eps, None)
+            return (y, x) if return_sum else y
+        y, h = _LayerNormFn.apply(x, weight, bias, eps, residual)
+        return (y, h) if return_sum else y
+    h = x + residual if residual is not None else x
+    y = F.layer_norm(h, (h.shape[-1],), weight, bias, eps)
+    return (y, h) if return_sum else y
+
+
+# --------------------------------------------------------------------------
+# BatchNorm2d (NHWC, training uses batch statistics, fused ReLU)
+# --------------------------------------------------------------------------
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu):
+        # x: (N, H, W, C) contiguous channels-last storage
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        y, mean, rstd = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
+                                                 momentum, eps, relu)
+        ctx.save_for_backward(x2, y, weight, bias, mean, rstd)
+        ctx.relu = relu
+        ctx.shp = x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, y, weight, bias, mean, rstd = ctx.saved_tensors
+        C = ctx.shp[-1]
+        dx, dw, db = _ext.ops().batchnorm_bwd(gy.reshape(-1, C).contiguous(), x2, y, weight, mean,
+                                              rstd, ctx.relu)
+        return dx.reshape(ctx.shp), dw.to(weight.dtype), db.to(bias.dtype), None, None, None, None, None
+
+
+def batch_norm_nhwc(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5,
+                    relu=False):
+    """BatchNorm over (N,H,W) of an NHWC tensor, optional fused ReLU."""
+    if _ext.use_native(x):
+        if training:
+            return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu)
+        C = x.shape[-1]
+        y = _ext.ops().batchnorm_eval(x.reshape(-1, C).contiguous(), weight, bias, running_mean, running_var,
+                                      eps, relu)
+        return y.reshape(x.shape)
+    xc = x.permute(0, 3, 1, 2)
+    y = F.batch_norm(xc, running_mean, running_var, weight, bias, training, momentum, eps)
+    if relu:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)

@@ -1,0 +1,161 @@
+"""Fused optimizers over a :class:`FlatParams` buffer (csrc/kernels/optim.hip) — N12/N13.
+
+Mixed-precision policy (N23): model parameters live in bf16 (what the GEMMs
+read), the optimizer owns an fp32 master copy and fp32 moments.  One step is:
+
+1. ``grad_norm`` kernel: Σ g² over the flat bf16 gradient → a device scalar
+   (block partials + a fixed-order final reduce: deterministic);
+2. ONE update kernel over every parameter: reads g (bf16), applies the DDP
+   averaging factor and the clip coefficient min(1, max_norm/‖g‖) *from
+   device memory* (no host sync), updates m, v and the fp32 master, writes the
+   bf16 parameter.  A non-finite ‖g‖ turns the whole step into a no-op
+   in-kernel (the NaN/Inf step guard of SURVEY.md §5).
+
+Weight decay applies to ≥2-D parameters only (per-64-element granule mask).
+On CPU the same math runs as vectorised torch ops on the flat buffers.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _ext
+from ..utils.flat import ALIGN, FlatParams
+
+
+class _FlatOptimizer:
+    def __init__(self, flat: FlatParams, lr, weight_decay, max_grad_norm, grad_scale):
+        self.flat = flat
+        self.lr = lr
+        self.weight_decay = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.grad_scale = grad_scale  # e.g. 1/world_size for DDP SUM-reduced grads
+        self.step_count = 0
+        dev = flat.data.device
+        self.master = flat.data.float() if flat.data.dtype != torch.float32 else flat.data
+        self.norm_buf = torch.zeros(2, dtype=torch.float32, device=dev)  # [‖g‖², skipped flag]
+        self._wd_elem = None
+
+    @property
+    def native(self):
+        return _ext.use_native(self.flat.data)
+
+    def grad_norm(self):
+        """Global L2 norm of the (scaled) gradient as a device tensor."""
+        if self.native:
+            _ext.ops().sumsq(self.flat.grad, self.norm_buf)
+        else:
+            self.norm_buf[0] = self.flat.grad.float().pow(2).sum()
+        return self.norm_buf[0].sqrt() * self.grad_scale
+
+    def _wd_elementwise(self):
+        if self._wd_elem is None:
+            self._wd_elem = self.flat.wd_mask.repeat_interleave(ALIGN).to(torch.float32)
+        return self._wd_elem
+
+    def zero_grad(self):
+        self.flat.zero_grad()
+
+
+class FusedAdamW(_FlatOptimizer):
+    def __init__(self, flat: FlatParams, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
+                 max_grad_norm=1.0, grad_scale=1.0):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, grad_scale)
+        self.betas, self.eps = betas, eps
+        self.m = torch.zeros_like(self.master)
+        self.v = torch.zeros_like(self.master)
+
+    def step(self, lr=None):
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        clip = self.max_grad_norm if self.max_grad_norm else 0.0
+        if self.native:
+            ops = _ext.ops()
+            ops.sumsq(self.flat.grad, self.norm_buf)
+            ops.adamw_step(self.flat.data, self.master, self.flat.grad, self.m, self.v, self.flat.wd_mask,
+                           self.norm_buf, lr, b1, b2, self.eps, self.weight_decay, bc1, bc2,
+                           self.grad_scale, clip)
+            return
+        g = self.flat.grad.float() * self.grad_scale
+        norm = g.pow(2).sum().sqrt()
+        if not torch.isfinite(norm):
+            return
+        if clip > 0:
+            g = g * min(1.0, clip / (float(norm) + 1e-6))
+        self.m.mul_(b1).add_(g, alpha=1 - b1)
+        self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (self.v / bc2).sqrt_().add_(self.eps)
+        upd = (self.m / bc1) / denom + self.weight_decay * self._wd_elementwise() * self.master
+        self.master.add_(upd, alpha=-lr)
+        if self.master is not self.flat.data:
+            self.flat.data.copy_(self.master)
+
+    def state_dict(self):
+        return {"step": self.step_count, "master": self.master, "m": self.m, "v": self.v, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        self.master.copy_(sd["master"])
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.lr = sd.get("lr", self.lr)
+        self.flat.data.copy_(self.master)
+
+
+class FusedSGD(_FlatOptimizer):
+    """SGD with momentum (+ Nesterov) and decoupled-free L2 weight decay (torch semantics)."""
+
+    def __init__(self, flat: FlatParams, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=False,
+                 max_grad_norm=0.0, grad_scale=1.0):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, grad_scale)
+        self.momentum, self.nesterov = momentum, nesterov
+        self.buf = torch.zeros_like(self.master)
+
+    def step(self, lr=None):
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        clip = self.max_grad_norm if self.max_grad_norm else 0.0
+        first = self.step_count == 1
+        if self.native:
+            ops = _ext.ops()
+            ops.sumsq(self.flat.grad, self.norm_buf)
+            ops.sgd_step(self.flat.data, self.master, self.flat.grad, self.buf, self.flat.wd_mask,
+                         self.norm_buf, lr, self.momentum, self.weight_decay, self.nesterov, first,
+                         self.grad_scale, clip)
+            return
+        g = self.flat.grad.float() * self.grad_scale
+        norm = g.pow(2).sum().sqrt()
+        if not torch.isfinite(norm):
+            return
+        if clip > 0:
+            g = g * min(1.0, clip / (float(norm) + 1e-6))
+        g = g + self.weight_decay * self._wd_elementwise() * self.master
+        if first:
+            self.buf.copy_(g)
+        else:
+            self.buf.mul_(self.momentum).add_(g)
+        d = g + self.momentum * self.buf if self.nesterov else self.buf
+        self.master.add_(d, alpha=-lr)
+        if self.master is not self.flat.data:
+            self.flat.data.copy_(self.master)
+
+    def state_dict(self):
+        return {"step": self.step_count, "master": self.master, "buf": self.buf, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        self.master.copy_(sd["master"])
+        self.buf.copy_(sd["buf"])
+        self.flat.data.copy_(self.master)
+
+
+def cosine_lr(step, base_lr, warmup, total, min_ratio=0.1):
+    if step < warmup:
+        return base_lr * (step + 1) / warmup
+    t = min(1.0, (step - warmup) / max(1, total - warmup))
+    return base_lr * (min_ratio + (1 - min_ratio) * 0.5 * (1 + math.cos(math.pi * t)))

@@ -1,0 +1,44 @@
+"""Process-group setup and data parallelism (N15/N16)."""
+
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+from .ddp import DistributedDataParallel
+
+
+def dist_env():
+    """(rank, local_rank, world_size) from torchrun-style env vars (defaults: single process)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_distributed(backend=None, timeout_s=600):
+    """Initialise torch.distributed from env:// if WORLD_SIZE>1.
+
+    GPU → backend "nccl" (RCCL over xGMI), one process per GPU, device =
+    LOCAL_RANK.  CPU → "gloo".  Returns (rank, local_rank, world, device).
+    """
+    rank, local_rank, world = dist_env()
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        be = backend or ("nccl" if use_gpu else "gloo")
+        kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return rank, local_rank, world, device
+
+
+__all__ = ["DistributedDataParallel", "dist_env", "init_distributed"]

@@ -1,0 +1,223 @@
+"""Training / evaluation entrypoints (N21) — ``replicann_amd.train(...)``,
+``replicann_amd.evaluate(...)`` and ``python -m replicann_amd`` (``train`` sub-command).
+
+The reference has no training code at all; this API is
+defined here and frozen.  One step:
+
+    zero_grad (1 memset) → [fwd → loss → bwd (bucketed RCCL all-reduce
+    overlapping)] × grad_accum → ddp.finish() → fused AdamW/SGD (2 kernels)
+
+Everything inside a step is asynchronous: no host synchronisation unless a
+log line needs the loss value.
+"""
+
+from __future__ import annotations
+
+import argparse
+import contextlib
+import json
+import time
+from dataclasses import asdict, dataclass, field
+
+import torch
+
+from . import models
+from .optim import FusedAdamW, FusedSGD, cosine_lr
+from .parallel import DistributedDataParallel, init_distributed
+from .utils.checkpoint import load_checkpoint, save_checkpoint
+from .utils.data import SyntheticImages, SyntheticLM, SyntheticMNIST
+from .utils.flat import FlatParams
+from .utils.metrics import MetricsLogger, is_rank0, phase
+
+MODEL_KINDS = {
+    "gpt2-small": "lm", "gpt2-medium": "lm", "gpt2-tiny": "lm",
+    "vit-b16": "image", "vit-tiny": "image",
+    "resnet18": "image", "resnet18-tiny": "image",
+    "mlp": "mnist",
+}
+
+
+def build_model(name, **kw):
+    if name == "gpt2-small":
+        return models.GPT2(models.GPT2Config.small(**kw))
+    if name == "gpt2-medium":
+        return models.GPT2(models.GPT2Config.medium(**kw))
+    if name == "gpt2-tiny":
+        return models.GPT2(models.GPT2Config.tiny(**kw))
+    if name == "vit-b16":
+        return models.ViT(models.ViTConfig.base16(**kw))
+    if name == "vit-tiny":
+        return models.ViT(models.ViTConfig.tiny(**kw))
+    if name == "resnet18":
+        return models.ResNet18(**kw)
+    if name == "resnet18-tiny":
+        return models.ResNet18(num_classes=10, widths=(16, 32, 64, 128), **kw)
+    if name == "mlp":
+        return models.MLP(**kw)
+    raise ValueError(f"unknown model {name!r}; known: {sorted(MODEL_KINDS)}")
+
+
+@dataclass
+class TrainConfig:
+    model: str = "gpt2-small"
+    batch_size: int = 16          # per-rank micro-batch
+    seq_len: int = 1024
+    image_size: int = 224
+    steps: int = 20
+    warmup_steps: int = 2
+    lr: float = 6e-4
+    min_lr_ratio: float = 0.1
+    weight_decay: float = 0.1
+    optimizer: str = "adamw"      # adamw | sgd
+    momentum: float = 0.9
+    dtype: str = "bf16"           # bf16 | fp32
+    grad_accum: int = 1
+    max_grad_norm: float = 1.0
+    bucket_mb: float = 64.0
+    log_every: int = 10
+    metrics_path: str | None = None
+    checkpoint: str | None = None
+    resume: str | None = None
+    seed: int = 0
+    device: str | None = None
+    model_kwargs: dict = field(default_factory=dict)
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig, model=None):
+        self.cfg = cfg
+        self.rank, self.local_rank, self.world, dev = init_distributed(
+            backend="gloo" if cfg.device == "cpu" else None)
+        self.device = torch.device(cfg.device) if cfg.device else dev
+        torch.manual_seed(cfg.seed)
+        self.kind = MODEL_KINDS.get(cfg.model, "lm")
+        self.model = model if model is not None else build_model(cfg.model, **cfg.model_kwargs)
+        dtype = torch.bfloat16 if (cfg.dtype == "bf16" and self.device.type == "cuda") else torch.float32
+        self.dtype = dtype
+        self.model.to(self.device)
+        for p in self.model.parameters():
+            p.data = p.data.to(dtype)
+        self.flat = FlatParams(self.model)
+        self.ddp = DistributedDataParallel(self.model, self.flat, cfg.bucket_mb) if self.world > 1 else None
+        gs = 1.0 / self.world
+        if cfg.optimizer == "adamw":
+            self.opt = FusedAdamW(self.flat, lr=cfg.lr, weight_decay=cfg.weight_decay,
+                                  max_grad_norm=cfg.max_grad_norm, grad_scale=gs)
+        else:
+            self.opt = FusedSGD(self.flat, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
+                                max_grad_norm=cfg.max_grad_norm, grad_scale=gs)
+        self.step_idx = 0
+        if cfg.resume:
+            self.step_idx, _ = load_checkpoint(cfg.resume, self.model, self.opt)
+            if self.ddp is not None:
+                self.ddp._broadcast_state()
+        self.data = self._make_data()
+        self.logger = MetricsLogger(cfg.metrics_path)
+
+    # ------------------------------------------------------------------
+    def _make_data(self):
+        c = self.cfg
+        seed = c.seed * 1000 + self.rank
+        if self.kind == "lm":
+            vocab = self.model.config.vocab_size
+            return SyntheticLM(c.batch_size, c.seq_len, vocab, self.device, seed=seed)
+        if self.kind == "image":
+            m = self.model
+            size = m.config.image_size if hasattr(m, "config") else c.image_size
+            classes = m.config.num_classes if hasattr(m, "config") else m.fc.out_features
+            return SyntheticImages(c.batch_size, size, 3, classes, self.device, self.dtype, seed=seed)
+        return SyntheticMNIST(c.batch_size, self.device, seed=seed)
+
+    @property
+    def net(self):
+        return self.ddp if self.ddp is not None else self.model
+
+    def samples_per_step(self):
+        return self.cfg.batch_size * self.cfg.grad_accum * self.world
+
+    def step(self, lr=None):
+        """One optimizer step; returns the (device) loss of the last micro-batch."""
+        c = self.cfg
+        self.opt.zero_grad()
+        loss = None
+        for micro in range(c.grad_accum):
+            x, y = next(self.data)
+            sync_ctx = (self.ddp.no_sync() if (self.ddp is not None and micro < c.grad_accum - 1)
+                        else contextlib.nullcontext())
+            with sync_ctx:
+                with phase("forward"):
+                    loss = self.net(x, y)
+                with phase("backward"):
+                    (loss / c.grad_accum if c.grad_accum > 1 else loss).backward()
+        if self.ddp is not None:
+            with phase("allreduce_wait"):
+                self.ddp.finish()
+        with phase("optimizer"):
+            self.opt.step(lr)
+        self.step_idx += 1
+        return loss
+
+    def lr_at(self, i):
+        c = self.cfg
+        return cosine_lr(i, c.lr, c.warmup_steps, max(c.steps, 1), c.min_lr_ratio)
+
+    def run(self):
+        c = self.cfg
+        t0 = time.time()
+        last = None
+        for i in range(self.step_idx, c.steps):
+            loss = self.step(self.lr_at(i))
+            if (i + 1) % c.log_every == 0 or i + 1 == c.steps:
+                lv = float(loss)
+                dt = time.time() - t0
+                self.logger.log(step=i + 1, loss=round(lv, 5), samples_per_s=round(
+                    self.samples_per_step() * (i + 1 - self.step_idx) / max(dt, 1e-9), 2))
+                last = lv
+        if c.checkpoint:
+            save_checkpoint(c.checkpoint, self.model, self.opt, c.steps, asdict(c))
+        return {"final_loss": last, "steps": c.steps, "wall_s": time.time() - t0}
+
+
+def train(config: TrainConfig | None = None, model=None, **kw):
+    """Train a replicated model; returns a summary dict."""
+    cfg = config or TrainConfig(**kw)
+    return Trainer(cfg, model=model).run()
+
+
+@torch.no_grad()
+def evaluate(model, data, steps=10):
+    """Mean loss (and accuracy for classifiers) over ``steps`` batches."""
+    was = model.training
+    model.eval()
+    tot, acc, n = 0.0, 0.0, 0
+    for _ in range(steps):
+        x, y = next(data)
+        out = model(x)
+        if out.dim() == 3:  # LM logits
+            lf = out.float().reshape(-1, out.shape[-1])
+            tot += float(torch.nn.functional.cross_entropy(lf, y.reshape(-1)))
+        else:
+            tot += float(torch.nn.functional.cross_entropy(out.float(), y))
+            acc += float((out.argmax(-1) == y).float().mean())
+        n += 1
+    model.train(was)
+    return {"loss": tot / n, "accuracy": acc / n}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="replicann_amd training entrypoint")
+    for f, v in asdict(TrainConfig()).items():
+        if isinstance(v, dict):
+            continue
+        t = type(v) if v is not None else str
+        ap.add_argument(f"--{f.replace('_', '-')}", type=t, default=v)
+    ap.add_argument("--model-kwargs", type=json.loads, default={})
+    a = vars(ap.parse_args(argv))
+    cfg = TrainConfig(**a)
+    out = train(cfg)
+    if is_rank0():
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

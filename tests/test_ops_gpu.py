@@ -1,0 +1,317 @@
+"""T2: every HIP kernel vs a plain PyTorch fp32 reference of the same op (gfx950 only)."""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from replicann_amd import _ext, ops
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf(*shape, scale=1.0, dev="cuda"):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def test_native_loaded(cuda):
+    assert _ext.available()
+    assert torch.ops.replicann.native_version() == 1
+
+
+# ----------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 96), (1000, 384, 520), (64, 24, 8)])
+def test_gemm_layouts(cuda, ta, tb, M, N, K):
+    torch.manual_seed(0)
+    a = bf(K, M) if ta else bf(M, K)
+    b = bf(N, K) if tb else bf(K, N)
+    ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
+    out = ops.gemm(a, b, ta=ta, tb=tb)
+    assert out.shape == (M, N)
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_gemm_identity_asymmetric(cuda):
+    # A = I with an asymmetric B catches a transposed C-write
+    M = 128
+    a = torch.eye(M, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(M * 64, device="cuda").reshape(64, M) % 61).to(torch.bfloat16)  # [N=64][K=M]
+    out = ops.gemm(a, b, tb=True)
+    torch.testing.assert_close(out.float(), b.float().t(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_epilogue(cuda, act):
+    torch.manual_seed(1)
+    M, N, K = 300, 264, 192
+    a, w = bf(M, K), bf(N, K, scale=0.1)
+    bias, res = bf(N), bf(M, N)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    out = ops.gemm(a, w, tb=True, bias=bias, residual=res, act=act, preact=pre if act else None)
+    h = a.float() @ w.float().t() + bias.float()
+    y = {0: h, 1: F.relu(h), 2: F.gelu(h, approximate="tanh")}[act] + res.float()
+    assert rel_err(out, y) < 1e-2
+    if act:
+        assert rel_err(pre, h) < 1e-2
+
+
+@pytest.mark.parametrize("split", [2, 4, 8])
+def test_gemm_splitk_fp32_accumulate(cuda, split):
+    torch.manual_seed(2)
+    M, N, K = 192, 320, 4096
+    a, b = bf(K, M), bf(K, N)
+    ref = a.float().t() @ b.float()
+    out = ops.gemm(a, b, ta=True, split_k=split, out_dtype=torch.float32)
+    assert out.dtype == torch.float32 and rel_err(out, ref) < 5e-3
+    acc = torch.ones(M, N, device="cuda")
+    ops.gemm(a, b, ta=True, split_k=split, out=acc, accumulate=True)
+    assert rel_err(acc, ref + 1) < 5e-3
+
+
+def test_linear_autograd(cuda):
+    torch.manual_seed(3)
+    x = bf(4, 33, 96).requires_grad_()
+    w = bf(160, 96, scale=0.1).requires_grad_()
+    b = bf(160).requires_grad_()
+    r = bf(4, 33, 160).requires_grad_()
+    y = ops.linear(x, w, b, act="gelu", residual=r)
+    g = bf(4, 33, 160)
+    y.backward(g)
+    xf, wf, bf_, rf = [t.detach().float().requires_grad_() for t in (x, w, b, r)]
+    yf = F.gelu(xf @ wf.t() + bf_, approximate="tanh") + rf
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2
+    for t, tf in ((x, xf), (w, wf), (b, bf_), (r, rf)):
+        assert rel_err(t.grad, tf.grad) < 2e-2
+
+
+# ----------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("E", [768, 1024, 96])
+def test_layernorm(cuda, E):
+    torch.manual_seed(4)
+    x, r = bf(37, E), bf(37, E)
+    w, b = bf(E).requires_grad_(), bf(E).requires_grad_()
+    xg, rg = x.clone().requires_grad_(), r.clone().requires_grad_()
+    y, h = ops.layer_norm(xg, w, b, 1e-5, residual=rg, return_sum=True)
+    gy = bf(37, E)
+    (y.float() * gy.float()).sum().backward()
+    xf, rf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, r, w, b)]
+    yf = F.layer_norm(xf + rf, (E,), wf, bf_, 1e-5)
+    (yf * gy.float()).sum().backward()
+    assert rel_err(y, yf) < 1e-2
+    assert rel_err(h, xf + rf) < 1e-2
+    for t, tf in ((xg, xf), (rg, rf), (w, wf), (b, bf_)):
+        assert rel_err(t.grad, tf.grad) < 2e-2
+
+
+# ----------------------------------------------------------------- cross entropy
+def test_cross_entropy_padded(cuda):
+    torch.manual_seed(5)
+    N, V, nv = 64, 1024, 1000
+    logits = bf(N, V, scale=3.0)
+    tgt = torch.randint(0, nv, (N,), device="cuda")
+    tgt[3] = -100
+    lg = logits.clone().requires_grad_()
+    loss = ops.cross_entropy(lg, tgt, n_valid_cols=nv)
+    loss.backward()
+    lf = logits.float()[:, :nv].requires_grad_()
+    lref = F.cross_entropy(lf, tgt, ignore_index=-100)
+    lref.backward()
+    assert abs(loss.item() - lref.item()) < 1e-2
+    assert rel_err(lg.grad[:, :nv], lf.grad) < 2e-2
+    assert lg.grad[:, nv:].abs().max().item() == 0
+
+
+# ----------------------------------------------------------------- attention
+def _attn_check(B, T, H, D, causal, bias=None, Tk=None, tol=2e-2):
+    Tk = Tk or T
+    q, k, v = bf(B, T, H, D), bf(B, Tk, H, D), bf(B, Tk, H, D)
+    qg, kg, vg = [t.clone().requires_grad_() for t in (q, k, v)]
+    scale = 1 / math.sqrt(D) if D != 64 else 0.125
+    o = ops.attention(qg, kg, vg, scale=scale, causal=causal, bias=bias)
+    go = bf(B, T, H, D)
+    o.backward(go)
+    qf, kf, vf = [t.detach().float().requires_grad_() for t in (q, k, v)]
+    of = ops.attention_reference(qf, kf, vf, scale, causal, bias)
+    of.backward(go.float())
+    assert rel_err(o, of) < tol
+    for t, tf in ((qg, qf), (kg, kf), (vg, vf)):
+        assert rel_err(t.grad, tf.grad) < 2 * tol
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("T", [256, 197, 64])
+def test_attention_d64(cuda, causal, T):
+    torch.manual_seed(6)
+    _attn_check(2, T, 3, 64, causal)
+
+
+def test_attention_d64_long(cuda):
+    torch.manual_seed(7)
+    _attn_check(1, 1024, 2, 64, True)
+
+
+def test_attention_bias_additive(cuda):
+    torch.manual_seed(8)
+    T = 96
+    bias = torch.tril(torch.ones(T, T, device="cuda")).unsqueeze(0)  # the reference's 0/1 mask, added
+    _attn_check(2, T, 2, 64, False, bias=bias)
+
+
+@pytest.mark.parametrize("D", [4, 32, 48])
+def test_attention_generic_d(cuda, D):
+    torch.manual_seed(9)
+    _attn_check(2, 40, 3, D, True)
+
+
+def test_attention_packed_grad(cuda):
+    torch.manual_seed(10)
+    B, T, H, D = 2, 128, 4, 64
+    qkv = bf(B, T, 3, H, D).requires_grad_()
+    o = ops.attention_packed(qkv, causal=True)
+    go = bf(B, T, H, D)
+    o.backward(go)
+    qf = qkv.detach().float().requires_grad_()
+    q, k, v = qf.unbind(2)
+    of = ops.attention_reference(q, k, v, 0.125, True)
+    of.backward(go.float())
+    assert rel_err(o, of) < 2e-2 and rel_err(qkv.grad, qf.grad) < 4e-2
+
+
+def test_attention_dropout_unbiased(cuda):
+    torch.manual_seed(11)
+    B, T, H, D = 4, 128, 4, 64
+    q, k, v = bf(B, T, H, D), bf(B, T, H, D), bf(B, T, H, D)
+    o0 = ops.attention(q, k, v, causal=True)
+    outs = torch.stack([ops.attention(q, k, v, causal=True, dropout_p=0.1, training=True).float() for _ in range(16)])
+    assert rel_err(outs.mean(0), o0) < 0.1
+    assert not torch.equal(outs[0], outs[1])
+
+
+# ----------------------------------------------------------------- misc kernels
+def test_softmax_act_dropout(cuda):
+    torch.manual_seed(12)
+    x = bf(50, 300).requires_grad_()
+    y = ops.softmax(x, scale=0.5)
+    g = bf(50, 300)
+    y.backward(g)
+    xf = x.detach().float().requires_grad_()
+    yf = torch.softmax(xf * 0.5, -1)
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2 and rel_err(x.grad, xf.grad) < 2e-2
+    z = bf(1000, 8).requires_grad_()
+    for fn, rf in ((ops.gelu, lambda t: F.gelu(t, approximate="tanh")), (ops.relu, F.relu)):
+        zz = z.detach().clone().requires_grad_()
+        out = fn(zz)
+        out.sum().backward()
+        zf = z.detach().float().requires_grad_()
+        rf(zf).sum().backward()
+        assert rel_err(out, rf(z.float())) < 1e-2 and rel_err(zz.grad, zf.grad) < 2e-2
+    d = ops.dropout(torch.ones(100000, device="cuda", dtype=torch.bfloat16), 0.25, True)
+    keep = (d != 0).float().mean().item()
+    assert abs(keep - 0.75) < 0.01 and abs(d.float().mean().item() - 1.0) < 0.02
+
+
+def test_embedding(cuda):
+    torch.manual_seed(13)
+    V, E, B, T = 500, 128, 3, 40
+    wte = bf(V, E).requires_grad_()
+    wpe = bf(64, E).requires_grad_()
+    ids = torch.randint(0, V, (B, T), device="cuda")
+    ids[0, :5] = 7  # repeated ids exercise the scatter-add
+    x = ops.embedding(ids, wte, wpe)
+    g = bf(B, T, E)
+    x.backward(g)
+    wf, pf = wte.detach().float().requires_grad_(), wpe.detach().float().requires_grad_()
+    xf = F.embedding(ids, wf) + pf[:T]
+    xf.backward(g.float())
+    assert rel_err(x, xf) < 1e-2 and rel_err(wte.grad, wf.grad) < 1e-2 and rel_err(wpe.grad, pf.grad) < 1e-2
+
+
+def test_fused_adamw_matches_cpu(cuda):
+    from replicann_amd.optim import FusedAdamW
+    from replicann_amd.utils.flat import FlatParams
+
+    torch.manual_seed(14)
+    m_gpu = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.Linear(128, 8)).cuda().to(torch.bfloat16)
+    m_cpu = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.Linear(128, 8))
+    m_cpu.load_state_dict({k: v.float().cpu() for k, v in m_gpu.state_dict().items()})
+    fg, fc = FlatParams(m_gpu), FlatParams(m_cpu)
+    og = FusedAdamW(fg, lr=1e-2, max_grad_norm=0.5, grad_scale=0.5)
+    oc = FusedAdamW(fc, lr=1e-2, max_grad_norm=0.5, grad_scale=0.5)
+    for _ in range(3):
+        g = torch.randn(fc.numel)
+        fg.grad.copy_(g.to(torch.bfloat16))
+        fc.grad.copy_(g.to(torch.bfloat16).float())
+        og.step()
+        oc.step()
+    assert rel_err(og.master.cpu(), oc.master) < 1e-4
+    # non-finite gradient -> step skipped in-kernel
+    before = og.master.clone()
+    fg.grad[5] = float("nan")
+    og.step()
+    assert torch.equal(before, og.master) and og.norm_buf[1].item() == 1.0
+
+
+# ----------------------------------------------------------------- conv / bn / pool
+@pytest.mark.parametrize("cfg", [(3, 7, 2, 3), (16, 3, 1, 1), (16, 1, 2, 0), (8, 3, 2, 1), (3, 16, 16, 0)])
+def test_conv2d(cuda, cfg):
+    torch.manual_seed(15)
+    C, Kk, S, P = cfg
+    x = bf(2, 32, 32, C).requires_grad_()
+    w = bf(24, Kk, Kk, C, scale=0.1).requires_grad_()
+    b = bf(24).requires_grad_()
+    y = ops.conv2d_nhwc(x, w, b, S, P)
+    g = bf(*y.shape)
+    y.backward(g)
+    xf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, w, b)]
+    yf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), bf_, S, P).permute(0, 2, 3, 1)
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2
+    for t, tf in ((x, xf), (w, wf), (b, bf_)):
+        assert rel_err(t.grad, tf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_batchnorm(cuda, relu):
+    torch.manual_seed(16)
+    x = bf(4, 9, 9, 40).requires_grad_()
+    w, b = bf(40).requires_grad_(), bf(40).requires_grad_()
+    rm, rv = torch.zeros(40, device="cuda"), torch.ones(40, device="cuda")
+    y = ops.batch_norm_nhwc(x, w, b, rm, rv, True, 0.1, 1e-5, relu)
+    g = bf(*y.shape)
+    y.backward(g)
+    xf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, w, b)]
+    rm2, rv2 = torch.zeros(40, device="cuda"), torch.ones(40, device="cuda")
+    yf = F.batch_norm(xf.permute(0, 3, 1, 2), rm2, rv2, wf, bf_, True, 0.1, 1e-5).permute(0, 2, 3, 1)
+    if relu:
+        yf = F.relu(yf)
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2
+    assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
+    for t, tf in ((x, xf), (w, wf), (b, bf_)):
+        assert rel_err(t.grad, tf.grad) < 3e-2
+
+
+def test_pools(cuda):
+    torch.manual_seed(17)
+    x = bf(2, 17, 17, 16).requires_grad_()
+    y = ops.maxpool_nhwc(x, 3, 2, 1)
+    g = bf(*y.shape)
+    y.backward(g)
+    xf = x.detach().float().requires_grad_()
+    yf = F.max_pool2d(xf.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2 and rel_err(x.grad, xf.grad) < 1e-2
+    x2 = bf(3, 7, 7, 32).requires_grad_()
+    a = ops.avgpool_nhwc(x2)
+    a.sum().backward()
+    assert rel_err(a, x2.detach().float().mean((1, 2))) < 1e-2
+    assert torch.allclose(x2.grad.float(), torch.full_like(x2.grad.float(), 1 / 49), rtol=1e-2)
