@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra torch.profiler steps (not timed)")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="capture the whole training step as one hipGraph (auto: on for 1 process)")
     args = ap.parse_args()
 
     from replicann_amd import _ext
@@ -51,7 +53,8 @@ def main():
         raise RuntimeError(f"native extension missing: {_ext.load_error()}")
 
     cfg = TrainConfig(model=args.model, batch_size=args.batch, seq_len=args.seq, steps=10**9,
-                      warmup_steps=10, lr=6e-4, bucket_mb=args.bucket_mb, log_every=10**9)
+                      warmup_steps=10, lr=6e-4, bucket_mb=args.bucket_mb, log_every=10**9,
+                      graph=args.graph)
     tr = Trainer(cfg)
     world = tr.world
     dev = tr.device
@@ -61,7 +64,7 @@ def main():
             torch.cuda.synchronize(dev)
 
     for i in range(args.warmup):
-        loss = tr.step(tr.lr_at(i))
+        loss = tr.step()
     sync()
     first_loss = float(loss) if args.warmup else float("nan")
 
@@ -70,7 +73,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = tr.step(tr.lr_at(args.warmup + i))
+        loss = tr.step()
     sync()
     if world > 1:
         dist.barrier()
@@ -116,6 +119,7 @@ def main():
             "parallelism": f"dp{world}",
             "tokens_per_s": round(value * args.seq, 1),
             "optimizer": "fused AdamW (fp32 master) + grad-norm clip",
+            "hipgraph": tr._graph is not None,
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         },
     }

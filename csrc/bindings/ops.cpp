@@ -24,13 +24,14 @@ void rn_act_fwd(const void*, void*, long, int, hipStream_t);
 void rn_act_bwd(const void*, const void*, void*, long, int, hipStream_t);
 void rn_dropout(const void*, void*, long, float, uint64_t, hipStream_t);
 void rn_add(const void*, const void*, void*, long, int, hipStream_t);
-void rn_bias_act_grad(const void*, const void*, void*, float*, float*, int, int, int, int, hipStream_t);
+void rn_bias_act_grad(const void*, const void*, void*, float*, void*, float*, int, int, int, int, hipStream_t);
 int rn_bias_act_grad_splits(int, int);
 int rn_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
               hipStream_t);
 int rn_ln_bwd_waves(int);
+long rn_ln_bwd_ws(int, int);
 int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
-              float*, float*, int, int, hipStream_t);
+              void*, void*, float*, int, int, hipStream_t);
 void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
 void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
 void rn_xent_fwd(const void*, const int64_t*, float*, float*, int, int, int, long, hipStream_t);
@@ -39,13 +40,14 @@ void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, 
 void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
 int rn_norm_ws_floats();
 void rn_sumsq(const void*, long, int, float*, float*, hipStream_t);
+void rn_opt_prep(float*, float, float, float, float, int, float, float, float, hipStream_t);
 int rn_adamw(void*, float*, const void*, int, float*, float*, const uint8_t*, float*, long, float, float, float, float,
-             float, float, float, float, float, hipStream_t);
-void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, long, float, float, float, int, int, float,
-            float, hipStream_t);
+             float, float, hipStream_t);
+void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, long, float, float, int, float, float,
+            hipStream_t);
 long rn_gemm_ws_floats(int, int, int);
-int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, float*, int, int, int, long, long, long,
-            int, int, int, int, int, int, hipStream_t);
+int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, float*, const float*, int, int, int,
+            long, long, long, int, int, int, int, int, int, int, hipStream_t);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
                 int, int, float, int, float, uint64_t, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
@@ -82,7 +84,7 @@ const void* optr(const optional<Tensor>& t) { return (t && t->defined()) ? t->da
 // ------------------------------------------------------------------ GEMM
 Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<Tensor>& bias,
             const optional<Tensor>& residual, int64_t act, const optional<Tensor>& preact, const optional<Tensor>& out,
-            bool accumulate, int64_t split_k, bool out_fp32) {
+            bool accumulate, int64_t split_k, bool out_fp32, const optional<Tensor>& alpha, int64_t cfg) {
     CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(b);
     GUARD(a);
     TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm expects 2-D operands");
@@ -133,24 +135,27 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     if (!ta && A.stride(0) % 8 != 0) A = A.contiguous();
     if (tb && B.stride(0) % 8 != 0) B = B.contiguous();
     if (c.stride(0) % 4 != 0 && (bias || residual)) { /* epilogue handles unaligned via scalar path */ }
+    if (alpha && alpha->defined()) TORCH_CHECK(alpha->scalar_type() == at::kFloat && alpha->is_cuda());
     int rc = rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
                      preact && preact->defined() ? preact->data_ptr() : nullptr, split > 1 ? ws.data_ptr<float>() : nullptr,
-                     (int)M, (int)N, (int)Kp, A.stride(0), B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32,
-                     accumulate, cur_stream());
+                     alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr, (int)M, (int)N, (int)Kp, A.stride(0),
+                     B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32, accumulate, (int)cfg, cur_stream());
     TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
     return c;
 }
 
+// returns (dH, db) with db in bf16 (the parameter dtype)
 std::tuple<Tensor, Tensor> bias_act_grad(const Tensor& dy, const optional<Tensor>& h, int64_t act, bool want_bias) {
     CHECK_CUDA(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
     GUARD(dy);
     const int M = dy.size(0), N = dy.size(1);
     Tensor dh = act != 0 ? at::empty_like(dy) : dy;
-    Tensor db = at::empty({want_bias ? N : 0}, dy.options().dtype(at::kFloat));
-    Tensor part = at::empty({want_bias ? (int64_t)rn_bias_act_grad_splits(M, N) * N : 1}, dy.options().dtype(at::kFloat));
+    Tensor db = at::empty({want_bias ? N : 0}, dy.options());
+    Tensor part = at::empty({want_bias ? (int64_t)(rn_bias_act_grad_splits(M, N) + 32) * N : 1},
+                            dy.options().dtype(at::kFloat));
     if (act != 0) { TORCH_CHECK(h && h->defined(), "activation grad needs the pre-activation"); CHECK_CONTIG(*h); }
     if (M > 0)
-        rn_bias_act_grad(dy.data_ptr(), optr(h), dh.data_ptr(), want_bias ? db.data_ptr<float>() : nullptr,
+        rn_bias_act_grad(dy.data_ptr(), optr(h), dh.data_ptr(), nullptr, want_bias ? db.data_ptr() : nullptr,
                          part.data_ptr<float>(), M, N, (int)act, want_bias, cur_stream());
     else if (want_bias) db.zero_();
     return {dh, db};
@@ -236,14 +241,13 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optiona
     CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(h); GUARD(dy);
     const int M = dy.size(0), E = dy.size(1);
     Tensor dx = at::empty_like(dy);
-    Tensor dw = at::empty({E}, dy.options().dtype(at::kFloat));
-    Tensor db = at::empty({E}, dy.options().dtype(at::kFloat));
-    const int W = rn_ln_bwd_waves(M);
-    Tensor part = at::empty({2 * (int64_t)W * E}, dy.options().dtype(at::kFloat));
+    Tensor dw = at::empty({E}, w.options());  // parameter dtype (bf16)
+    Tensor db = at::empty({E}, w.options());
+    Tensor part = at::empty({rn_ln_bwd_ws(M, E)}, dy.options().dtype(at::kFloat));
     if (M) {
         int rc = rn_ln_bwd(dy.data_ptr(), optr(gh), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
-                           rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
-                           part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)W * E, M, E, cur_stream());
+                           rstd.data_ptr<float>(), dx.data_ptr(), nullptr, nullptr, dw.data_ptr(), db.data_ptr(),
+                           part.data_ptr<float>(), M, E, cur_stream());
         TORCH_CHECK(rc == 0, "layernorm_bwd: unsupported E=", E);
     } else { dw.zero_(); db.zero_(); }
     return {dx, dw, db};
@@ -285,25 +289,30 @@ void sumsq(const Tensor& g, const Tensor& normbuf) {
     rn_sumsq(g.data_ptr(), g.numel(), g.scalar_type() == at::kBFloat16, part.data_ptr<float>(), normbuf.data_ptr<float>(),
              cur_stream());
 }
+void opt_prep(const Tensor& state, double base_lr, double warmup, double total, double min_ratio, bool cosine,
+              double lr_override, double b1, double b2) {
+    GUARD(state);
+    TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 8);
+    rn_opt_prep(state.data_ptr<float>(), (float)base_lr, (float)warmup, (float)total, (float)min_ratio, cosine,
+                (float)lr_override, (float)b1, (float)b2, cur_stream());
+}
 void adamw_step(const Tensor& p, const Tensor& master, const Tensor& g, const Tensor& m, const Tensor& v,
-                const Tensor& wdm, const Tensor& normbuf, double lr, double b1, double b2, double eps, double wd,
-                double bc1, double bc2, double gscale, double clip) {
+                const Tensor& wdm, const Tensor& state, double b1, double b2, double eps, double wd, double gscale,
+                double clip) {
     CHECK_BF16(p); GUARD(p);
     TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat);
     TORCH_CHECK(p.numel() == master.numel() && p.numel() == g.numel() && wdm.numel() * 64 >= p.numel());
     int rc = rn_adamw(p.data_ptr(), master.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16,
-                      m.data_ptr<float>(), v.data_ptr<float>(), wdm.data_ptr<uint8_t>(), normbuf.data_ptr<float>(),
-                      p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2,
-                      (float)gscale, (float)clip, cur_stream());
+                      m.data_ptr<float>(), v.data_ptr<float>(), wdm.data_ptr<uint8_t>(), state.data_ptr<float>(),
+                      p.numel(), (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale, (float)clip, cur_stream());
     TORCH_CHECK(rc == 0, "adamw: flat buffer length must be a multiple of 8");
 }
 void sgd_step(const Tensor& p, const Tensor& master, const Tensor& g, const Tensor& buf, const Tensor& wdm,
-              const Tensor& normbuf, double lr, double mom, double wd, bool nesterov, bool first, double gscale,
-              double clip) {
+              const Tensor& state, double mom, double wd, bool nesterov, double gscale, double clip) {
     CHECK_BF16(p); GUARD(p);
     rn_sgd(p.data_ptr(), master.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16, buf.data_ptr<float>(),
-           wdm.data_ptr<uint8_t>(), normbuf.data_ptr<float>(), p.numel(), (float)lr, (float)mom, (float)wd, nesterov,
-           first, (float)gscale, (float)clip, cur_stream());
+           wdm.data_ptr<uint8_t>(), state.data_ptr<float>(), p.numel(), (float)mom, (float)wd, nesterov, (float)gscale,
+           (float)clip, cur_stream());
 }
 
 // ------------------------------------------------------------------ attention
@@ -457,7 +466,7 @@ int64_t native_version() { return 1; }
 
 TORCH_LIBRARY(replicann, m) {
     m.def("gemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, Tensor? residual, int act, Tensor? preact, "
-          "Tensor? out, bool accumulate, int split_k, bool out_fp32) -> Tensor");
+          "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1) -> Tensor");
     m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
@@ -472,10 +481,12 @@ TORCH_LIBRARY(replicann, m) {
     m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
     m.def("embedding_bwd(Tensor dx, Tensor ids, int V, int Tp) -> (Tensor, Tensor)");
     m.def("sumsq(Tensor g, Tensor(a!) normbuf) -> ()");
-    m.def("adamw_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) m, Tensor(d!) v, Tensor wdm, Tensor(e!) normbuf, "
-          "float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, float clip) -> ()");
-    m.def("sgd_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) buf, Tensor wdm, Tensor(e!) normbuf, float lr, "
-          "float mom, float wd, bool nesterov, bool first, float gscale, float clip) -> ()");
+    m.def("opt_prep(Tensor(a!) state, float base_lr, float warmup, float total, float min_ratio, bool cosine, "
+          "float lr_override, float b1, float b2) -> ()");
+    m.def("adamw_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) m, Tensor(d!) v, Tensor wdm, Tensor(e!) state, "
+          "float b1, float b2, float eps, float wd, float gscale, float clip) -> ()");
+    m.def("sgd_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) buf, Tensor wdm, Tensor(e!) state, "
+          "float mom, float wd, bool nesterov, float gscale, float clip) -> ()");
     m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? bias, float scale, bool causal, float p, int seed) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
           "bool causal, float p, int seed) -> (Tensor, Tensor, Tensor)");
@@ -510,6 +521,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("embedding_fwd", &embedding_fwd);
     m.impl("embedding_bwd", &embedding_bwd);
     m.impl("sumsq", &sumsq);
+    m.impl("opt_prep", &opt_prep);
     m.impl("adamw_step", &adamw_step);
     m.impl("sgd_step", &sgd_step);
     m.impl("attn_fwd", &attn_fwd);

@@ -78,18 +78,20 @@ RN_DEV float hash_uniform(uint64_t seed, uint64_t idx) {
     return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
 }
 
-// tanh-approximate GELU and its derivative
+// tanh-approximate GELU and its derivative, via the identity
+//   0.5·x·(1 + tanh(u)) = x·σ(2u),  u = √(2/π)(x + 0.044715x³)
+// → one v_exp_f32 + one v_rcp_f32 per element (no libm tanhf).
+RN_DEV float fast_sigmoid(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 RN_DEV float gelu_f(float x) {
-    const float c = 0.7978845608028654f;
-    float u = c * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
+    const float c2 = 2.f * 0.7978845608028654f;
+    return x * fast_sigmoid(c2 * (x + 0.044715f * x * x * x));
 }
 RN_DEV float gelu_grad_f(float x) {
     const float c = 0.7978845608028654f;
-    float x2 = x * x;
-    float u = c * (x + 0.044715f * x2 * x);
-    float t = tanhf(u);
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * c * (1.f + 3.f * 0.044715f * x2);
+    const float x2 = x * x;
+    const float s = fast_sigmoid(2.f * c * (x + 0.044715f * x2 * x));
+    // d/dx = s + 2·x·s·(1-s)·c·(1 + 3·0.044715·x²)
+    return s + 2.f * x * s * (1.f - s) * c * (1.f + 0.134145f * x2);
 }
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
@@ -110,3 +112,50 @@ RN_DEV float act_grad_f(float x) {
 #define HIP_CHECK_LAUNCH() (void)hipGetLastError()
 
 static inline int rn_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------
+// Deterministic parallel column reduction of an fp32 [R][C] partial matrix:
+// stage 1 grid (ceil(C/64), S) — each wave sums a strided subset of rows for 64
+// columns (256-B coalesced rows), 4 waves combine in LDS → tmp[S][C];
+// stage 2 one thread per column sums the S stage-1 rows in fixed order and
+// writes fp32 and/or bf16.  Fixed summation order → bitwise reproducible.
+// ---------------------------------------------------------------------------
+constexpr int RN_COLRED_S = 32;
+
+namespace {  // internal linkage: every TU gets its own copy
+
+__global__ void __launch_bounds__(256) rn_colred1_k(const float* __restrict__ in, int R, int C,
+                                                    float* __restrict__ tmp) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    const int S = gridDim.y;
+    const int r0 = (int)((long)R * blockIdx.y / S), r1 = (int)((long)R * (blockIdx.y + 1) / S);
+    float s = 0.f;
+    if (c < C)
+        for (int r = r0 + w; r < r1; r += 4) s += in[(long)r * C + c];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && c < C) tmp[(long)blockIdx.y * C + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+__global__ void rn_colred2_k(const float* __restrict__ tmp, int S, int C, float* __restrict__ out32,
+                             __bf16* __restrict__ out16) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int i = 0; i < S; ++i) s += tmp[(long)i * C + c];
+    if (out32) out32[c] = s;
+    if (out16) out16[c] = (__bf16)s;
+}
+
+// tmp must hold RN_COLRED_S * C floats
+static inline void rn_colreduce(const float* in, int R, int C, float* tmp, float* out32, __bf16* out16,
+                                hipStream_t st) {
+    int S = R < RN_COLRED_S ? (R > 0 ? R : 1) : RN_COLRED_S;
+    dim3 g((C + 63) / 64, S);
+    rn_colred1_k<<<g, 256, 0, st>>>(in, R, C, tmp);
+    rn_colred2_k<<<(C + 255) / 256, 256, 0, st>>>(tmp, S, C, out32, out16);
+}
+
+}  // namespace

@@ -1,0 +1,317 @@
+// Templated MFMA GEMM kernels (see csrc/kernels/gemm_bf16.hip for the design notes).
+// Instantiated per tile config in gemm_cfg*.hip so the configs compile in parallel.
+#pragma once
+#include <algorithm>
+#include "common.h"
+
+namespace rn_gemm_detail {
+
+constexpr int BK = 64;
+constexpr int GROUP_M = 8;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct GemmArgs {
+    const bf16* A;
+    const bf16* B;
+    void* C;
+    const bf16* bias;
+    const bf16* res;
+    bf16* pre;
+    float* ws;
+    const float* alpha;  // optional device scalar multiplying op(A)·op(B)
+    int M, N, K;
+    long lda, ldb, ldc;
+    int tiles_m, tiles_n, split, k_per_split;
+    int out_f32, accumulate;
+};
+
+RN_DEV int swz_kc(int r) { return (r >> 1) & 7; }
+RN_DEV int swz_mn(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+RN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+    // readfirstlane keeps the descriptor provably wave-uniform (no waterfall loops, guide T20)
+    const uint64_t bp = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+}
+
+// Stage one ROWS(mn)×64(k) operand tile into LDS with NW waves.
+//   KC:  global element (mn, k) at base[mn*ld + k]; image [ROWS][64] (128-B rows)
+//   !KC: global element (mn, k) at base[k*ld + mn]; image = ROWS/128 sub-images [64 k][128 mn]
+template <bool KC, int ROWS, int NW>
+RN_DEV void stage(const bf16* base, long ld, int mn_lim, int k_lim, char* lds, int wave, int lane) {
+    __amdgpu_buffer_rsrc_t rsrc = make_rsrc(base);
+    constexpr int NINS = ROWS * 128 / 1024;  // 1 KiB per wave-instruction
+    constexpr int PER = NINS / NW;
+    static_assert(NINS % NW == 0, "tile / wave mismatch");
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int ins = wave * PER + i;
+        uint32_t voff;
+        if constexpr (KC) {
+            const int r = ins * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz_kc(r);
+            const int k = cg * 8;
+            const bool ok = (r < mn_lim) && (k < k_lim);
+            voff = ok ? (uint32_t)(((long)r * ld + k) * 2) : 0xFFFFFFF0u;
+        } else {
+            const int sub = ins >> 4, within = ins & 15;
+            const int r = within * 4 + (lane >> 4);
+            const int cg = (lane & 15) ^ swz_mn(r);
+            const int mn = sub * 128 + cg * 8;
+            const bool ok = (r < k_lim) && (mn < mn_lim);
+            voff = ok ? (uint32_t)(((long)r * ld + mn) * 2) : 0xFFFFFFF0u;
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
+    }
+}
+
+// fragment: 8 consecutive k (k-step s: k = s*32 + 8*(lane>>4) + 0..7) of row/col
+// mnbase + (lane & 15) within the tile.
+template <bool KC>
+RN_DEV s16x8 frag(const char* lds, int mnbase, int s, int lane) {
+    if constexpr (KC) {
+        const int row = mnbase + (lane & 15);
+        const int chunk = s * 4 + (lane >> 4);
+        return *reinterpret_cast<const s16x8*>(lds + row * 128 + ((chunk ^ swz_kc(row)) << 4));
+    } else {
+        const char* sub = lds + (mnbase >> 7) * 16384;
+        const int mnl = mnbase & 127;
+        const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+        const int c = (mnl >> 3) + (p >> 1);
+        const int k0 = s * 32 + 8 * g + q;
+        const int k1 = k0 + 4;
+        const char* a0 = sub + k0 * 256 + ((c ^ swz_mn(k0)) << 4) + (p & 1) * 8;
+        const char* a1 = sub + k1 * 256 + ((c ^ swz_mn(k1)) << 4) + (p & 1) * 8;
+        s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+        s16x8 r;
+        r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+        r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+        return r;
+    }
+}
+
+RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, int& tn) {
+    // XCD remap (bijective for any nblocks): blocks sharing bid%8 get a contiguous id range
+    const int xcd = bid & 7, loc = bid >> 3;
+    const int q = nblocks >> 3, r = nblocks & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    // grouped ordering: GROUP_M tile-rows share B panels
+    const int per_group = GROUP_M * tiles_n;
+    const int gid = id / per_group;
+    const int first_m = gid * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int in = id % per_group;
+    tm = first_m + in % gsz;
+    tn = in / gsz;
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT>
+__global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
+    constexpr int NW = WM * WN;
+    constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+
+    const int tiles = p.tiles_m * p.tiles_n;
+    const int split_id = SPLIT ? blockIdx.x / tiles : 0;
+    const int tb = SPLIT ? blockIdx.x % tiles : blockIdx.x;
+    int tm, tn;
+    map_tile(tb, tiles, p.tiles_m, p.tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = split_id * p.k_per_split;
+    const int kend = min(p.K, kbeg + p.k_per_split);
+    const int nk = (kend - kbeg + BK - 1) / BK;
+
+    auto a_base = [&](int k0) -> const bf16* {
+        return AK ? p.A + (long)m0 * p.lda + k0 : p.A + (long)k0 * p.lda + m0;
+    };
+    auto b_base = [&](int k0) -> const bf16* {
+        return BK_ ? p.B + (long)n0 * p.ldb + k0 : p.B + (long)k0 * p.ldb + n0;
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    if (nk > 0) {
+        stage<AK, BM, NW>(a_base(kbeg), p.lda, p.M - m0, kend - kbeg, smem, wave, lane);
+        stage<BK_, BN, NW>(b_base(kbeg), p.ldb, p.N - n0, kend - kbeg, smem + A_BYTES, wave, lane);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();  // vmcnt(0) + barrier: stage kt landed; stage kt-1 fully consumed
+        const int cur = kt & 1;
+        if (kt + 1 < nk) {
+            const int k0 = kbeg + (kt + 1) * BK;
+            char* nb = smem + (cur ^ 1) * STAGE;
+            stage<AK, BM, NW>(a_base(k0), p.lda, p.M - m0, kend - k0, nb, wave, lane);
+            stage<BK_, BN, NW>(b_base(k0), p.ldb, p.N - n0, kend - k0, nb + A_BYTES, wave, lane);
+        }
+        const char* la = smem + cur * STAGE;
+        const char* lb = la + A_BYTES;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            s16x8 af[FM], bfr[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) bfr[j] = frag<BK_>(lb, wn * (BN / WN) + j * 16, s, lane);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) af[i] = frag<AK>(la, wm * (BM / WM) + i * 16, s, lane);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) ----
+    const float alpha = p.alpha ? *p.alpha : 1.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+            if (n >= p.N) continue;
+            float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
+            if constexpr (SPLIT) {
+                float* w = p.ws + ((long)split_id * p.M + m) * p.N + n;
+                if (n + 3 < p.N) *reinterpret_cast<float4*>(w) = make_float4(v[0], v[1], v[2], v[3]);
+                else for (int t = 0; t < 4 && n + t < p.N; ++t) w[t] = v[t];
+                continue;
+            } else {
+                const bool full = (n + 3 < p.N);
+                if (p.bias) {
+                    if (full) {
+                        bf16x4 b = *reinterpret_cast<const bf16x4*>(p.bias + n);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) v[t] += (float)b[t];
+                    } else for (int t = 0; t < 4 && n + t < p.N; ++t) v[t] += (float)p.bias[n + t];
+                }
+                if constexpr (ACT != ACT_NONE) {
+                    if (p.pre) {
+                        bf16* pp = p.pre + (long)m * p.ldc + n;
+                        if (full) {
+                            bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+                            *reinterpret_cast<bf16x4*>(pp) = o;
+                        } else for (int t = 0; t < 4 && n + t < p.N; ++t) pp[t] = (bf16)v[t];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v[t] = act_f<ACT>(v[t]);
+                }
+                if (p.res) {
+                    const bf16* rp = p.res + (long)m * p.ldc + n;
+                    if (full) {
+                        bf16x4 r = *reinterpret_cast<const bf16x4*>(rp);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) v[t] += (float)r[t];
+                    } else for (int t = 0; t < 4 && n + t < p.N; ++t) v[t] += (float)rp[t];
+                }
+                if (p.out_f32) {
+                    float* cp = (float*)p.C + (long)m * p.ldc + n;
+                    if (full) {
+                        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+                        if (p.accumulate) { float4 c = *reinterpret_cast<float4*>(cp); o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w; }
+                        *reinterpret_cast<float4*>(cp) = o;
+                    } else for (int t = 0; t < 4 && n + t < p.N; ++t) cp[t] = v[t] + (p.accumulate ? cp[t] : 0.f);
+                } else {
+                    bf16* cp = (bf16*)p.C + (long)m * p.ldc + n;
+                    if (full) {
+                        if (p.accumulate) {
+                            bf16x4 c = *reinterpret_cast<const bf16x4*>(cp);
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) v[t] += (float)c[t];
+                        }
+                        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+                        *reinterpret_cast<bf16x4*>(cp) = o;
+                    } else for (int t = 0; t < 4 && n + t < p.N; ++t) cp[t] = (bf16)(v[t] + (p.accumulate ? (float)cp[t] : 0.f));
+                }
+            }
+        }
+    }
+}
+
+// Sum split-K slabs (fixed order) + epilogue.  4 consecutive columns per thread.
+template <int ACT>
+__global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
+    const long total4 = ((long)p.M * p.N + 3) / 4;
+    for (long q = blockIdx.x * 256L + threadIdx.x; q < total4; q += (long)gridDim.x * 256) {
+        const long e0 = q * 4;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        const long MN = (long)p.M * p.N;
+        const bool vec = (p.N % 4 == 0);
+        for (int s = 0; s < p.split; ++s) {
+            const float* w = p.ws + s * MN + e0;
+            if (vec) { float4 t = *reinterpret_cast<const float4*>(w); v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w; }
+            else for (int t = 0; t < 4 && e0 + t < MN; ++t) v[t] += w[t];
+        }
+        for (int t = 0; t < 4; ++t) {
+            const long e = e0 + t;
+            if (e >= MN) break;
+            const int m = e / p.N, n = e % p.N;
+            float x = v[t];
+            if (p.bias) x += (float)p.bias[n];
+            if constexpr (ACT != ACT_NONE) {
+                if (p.pre) p.pre[(long)m * p.ldc + n] = (bf16)x;
+                x = act_f<ACT>(x);
+            }
+            if (p.res) x += (float)p.res[(long)m * p.ldc + n];
+            if (p.out_f32) {
+                float* cp = (float*)p.C + (long)m * p.ldc + n;
+                *cp = x + (p.accumulate ? *cp : 0.f);
+            } else {
+                bf16* cp = (bf16*)p.C + (long)m * p.ldc + n;
+                *cp = (bf16)(x + (p.accumulate ? (float)*cp : 0.f));
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT>
+void launch_t(GemmArgs& a, hipStream_t st) {
+    constexpr int NT = WM * WN * 64;
+    const size_t lds = 2 * (BM + BN) * BK * 2;
+    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false>;
+    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true>;
+    static bool attr = false;
+    if (!attr) {  // >64 KiB of dynamic LDS must be opted into, once per instantiation
+        attr = true;
+        (void)hipFuncSetAttribute((const void*)kmain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)ksplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    const int tiles = a.tiles_m * a.tiles_n;
+    if (a.split > 1) {
+        ksplit<<<tiles * a.split, NT, lds, st>>>(a);
+        long total4 = ((long)a.M * a.N + 3) / 4;
+        int g = (int)std::min<long>((total4 + 255) / 256, 4096);
+        splitk_reduce_k<ACT><<<g, 256, 0, st>>>(a);
+    } else {
+        kmain<<<tiles, NT, lds, st>>>(a);
+    }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_cfg(GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
+    a.tiles_m = (a.M + BM - 1) / BM;
+    a.tiles_n = (a.N + BN - 1) / BN;
+#define RN_L(AKv, BKv)                                                                             \
+    if (act == ACT_GELU) launch_t<BM, BN, WM, WN, AKv, BKv, ACT_GELU>(a, st);                     \
+    else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, AKv, BKv, ACT_RELU>(a, st);                \
+    else launch_t<BM, BN, WM, WN, AKv, BKv, ACT_NONE>(a, st);
+    if (ak && bk) { RN_L(true, true) }
+    else if (ak && !bk) { RN_L(true, false) }
+    else if (!ak && bk) { RN_L(false, true) }
+    else { RN_L(false, false) }
+#undef RN_L
+}
+
+}  // namespace rn_gemm_detail

@@ -134,14 +134,6 @@ __global__ void __launch_bounds__(TPB) bias_act_grad_k(const bf16* __restrict__ 
     }
 }
 
-__global__ void colsum_finish_k(const float* __restrict__ part, float* __restrict__ out, int S, int N) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= N) return;
-    float s = 0.f;
-    for (int i = 0; i < S; ++i) s += part[(long)i * N + c];
-    out[c] = s;
-}
-
 }  // namespace
 
 extern "C" {
@@ -168,9 +160,9 @@ void rn_add(const void* a, const void* b, void* y, long n, int relu, hipStream_t
     else add_k<false><<<g, TPB, 0, st>>>((const bf16*)a, (const bf16*)b, (bf16*)y, n);
 }
 
-// part: workspace of >= splits*N floats.  Returns nothing; db (fp32, N) written if want_bias.
-void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, float* part, int M, int N, int act,
-                      int want_bias, hipStream_t st) {
+// part: workspace of >= (splits + RN_COLRED_S) * N floats.  db (fp32) / db16 (bf16) written if want_bias.
+void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, void* db16, float* part, int M, int N,
+                      int act, int want_bias, hipStream_t st) {
     int cblocks = (N + 511) / 512;
     int splits = 1;
     while (cblocks * splits < 512 && M / (splits * 2) >= 32) splits *= 2;
@@ -181,7 +173,7 @@ void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, float*
     else if (act == ACT_RELU) { if (want_bias) RN_BAG(ACT_RELU, true); else RN_BAG(ACT_RELU, false); }
     else { if (want_bias) RN_BAG(ACT_NONE, true); else return; }
 #undef RN_BAG
-    if (want_bias) colsum_finish_k<<<(N + 255) / 256, 256, 0, st>>>(part, db, splits, N);
+    if (want_bias) rn_colreduce(part, splits, N, part + (long)splits * N, db, (bf16*)db16, st);
 }
 
 int rn_bias_act_grad_splits(int M, int N) {

@@ -106,9 +106,9 @@ template <typename GT>
 __global__ void __launch_bounds__(256) adamw_k(bf16* __restrict__ p, float* __restrict__ master,
                                                const GT* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
                                                const uint8_t* __restrict__ wdm, float* __restrict__ normbuf, long n,
-                                               float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
-                                               float grad_scale, float clip) {
+                                               float b1, float b2, float eps, float wd, float grad_scale, float clip) {
     const float coef = clip_coef(normbuf, grad_scale, clip);
+    const float lr = normbuf[3], bc1 = normbuf[4], bc2 = normbuf[5];
     if (coef < 0.f) {
         if (blockIdx.x == 0 && threadIdx.x == 0) normbuf[1] = 1.f;  // step skipped (non-finite grads)
         return;
@@ -152,9 +152,11 @@ __global__ void __launch_bounds__(256) adamw_k(bf16* __restrict__ p, float* __re
 template <typename GT>
 __global__ void __launch_bounds__(256) sgd_k(bf16* __restrict__ p, float* __restrict__ master, const GT* __restrict__ g,
                                              float* __restrict__ buf, const uint8_t* __restrict__ wdm,
-                                             float* __restrict__ normbuf, long n, float lr, float mom, float wd,
-                                             int nesterov, int first, float grad_scale, float clip) {
+                                             float* __restrict__ normbuf, long n, float mom, float wd,
+                                             int nesterov, float grad_scale, float clip) {
     const float coef = clip_coef(normbuf, grad_scale, clip);
+    const float lr = normbuf[3];
+    const int first = normbuf[2] == 1.f;
     if (coef < 0.f) {
         if (blockIdx.x == 0 && threadIdx.x == 0) normbuf[1] = 1.f;
         return;
@@ -171,6 +173,28 @@ __global__ void __launch_bounds__(256) sgd_k(bf16* __restrict__ p, float* __rest
         master[e] = w;
         p[e] = f2bf(w);
     }
+}
+
+// Optimizer step prologue (1 thread): step counter, LR schedule and Adam bias
+// corrections live in device memory, so a captured hipGraph replays correct
+// per-step hyper-parameters.  state: [sumsq, skipped, t, lr, bc1, bc2]
+__global__ void opt_prep_k(float* __restrict__ st, float base_lr, float warmup, float total, float min_ratio,
+                           int cosine, float lr_override, float b1, float b2) {
+    const float t = st[2] + 1.f;
+    st[2] = t;
+    float lr = base_lr;
+    if (lr_override >= 0.f) lr = lr_override;
+    else if (cosine) {
+        const float i = t - 1.f;
+        if (i < warmup) lr = base_lr * (i + 1.f) / warmup;
+        else {
+            float x = fminf(1.f, (i - warmup) / fmaxf(1.f, total - warmup));
+            lr = base_lr * (min_ratio + (1.f - min_ratio) * 0.5f * (1.f + cosf(3.14159265358979f * x)));
+        }
+    }
+    st[3] = lr;
+    st[4] = 1.f - powf(b1, t);
+    st[5] = 1.f - powf(b2, t);
 }
 
 inline int grid_for(long work) {
@@ -211,30 +235,34 @@ void rn_sumsq(const void* g, long n, int is_bf16, float* part, float* normbuf, h
     sumsq_final_k<<<1, 256, 0, st>>>(part, gb, normbuf);
 }
 
+void rn_opt_prep(float* state, float base_lr, float warmup, float total, float min_ratio, int cosine,
+                 float lr_override, float b1, float b2, hipStream_t st) {
+    opt_prep_k<<<1, 1, 0, st>>>(state, base_lr, warmup, total, min_ratio, cosine, lr_override, b1, b2);
+}
+
 int rn_adamw(void* p, float* master, const void* g, int g_bf16, float* m, float* v, const uint8_t* wdm,
-             float* normbuf, long n, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
-             float grad_scale, float clip, hipStream_t st) {
+             float* state, long n, float b1, float b2, float eps, float wd, float grad_scale, float clip,
+             hipStream_t st) {
     if (n % 8) return -1;
     int gb = grid_for(n / 8);
     if (g_bf16)
-        adamw_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, m, v, wdm, normbuf, n, lr, b1, b2, eps,
-                                          wd, bc1, bc2, grad_scale, clip);
+        adamw_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, m, v, wdm, state, n, b1, b2, eps, wd,
+                                          grad_scale, clip);
     else
-        adamw_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, m, v, wdm, normbuf, n, lr, b1, b2, eps,
-                                           wd, bc1, bc2, grad_scale, clip);
+        adamw_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, m, v, wdm, state, n, b1, b2, eps, wd,
+                                           grad_scale, clip);
     return 0;
 }
 
-void rn_sgd(void* p, float* master, const void* g, int g_bf16, float* buf, const uint8_t* wdm, float* normbuf,
-            long n, float lr, float mom, float wd, int nesterov, int first, float grad_scale, float clip,
-            hipStream_t st) {
+void rn_sgd(void* p, float* master, const void* g, int g_bf16, float* buf, const uint8_t* wdm, float* state, long n,
+            float mom, float wd, int nesterov, float grad_scale, float clip, hipStream_t st) {
     int gb = grid_for(n);
     if (g_bf16)
-        sgd_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, buf, wdm, normbuf, n, lr, mom, wd, nesterov,
-                                        first, grad_scale, clip);
+        sgd_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, buf, wdm, state, n, mom, wd, nesterov,
+                                        grad_scale, clip);
     else
-        sgd_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, buf, wdm, normbuf, n, lr, mom, wd,
-                                         nesterov, first, grad_scale, clip);
+        sgd_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, buf, wdm, state, n, mom, wd, nesterov,
+                                         grad_scale, clip);
 }
 
 }  // extern "C"

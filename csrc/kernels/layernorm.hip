@@ -137,16 +137,6 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
     }
 }
 
-__global__ void ln_finish_k(const float* __restrict__ pdw, const float* __restrict__ pdb, float* __restrict__ dw,
-                            float* __restrict__ db, int W, int E) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= E) return;
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < W; ++i) { a += pdw[(long)i * E + c]; b += pdb[(long)i * E + c]; }
-    dw[c] = a;
-    db[c] = b;
-}
-
 }  // namespace
 
 extern "C" {
@@ -171,8 +161,13 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
 int rn_ln_bwd_waves(int M) { int W = M < 2048 ? M : 2048; return ((W + 3) / 4) * 4; }
 
 // pdw/pdb workspace: rn_ln_bwd_waves(M) * E floats each.
+long rn_ln_bwd_ws(int M, int E) { return 2L * rn_ln_bwd_waves(M) * E + 2L * RN_COLRED_S * E; }
+
+// ws: rn_ln_bwd_ws(M, E) floats.  dw/db (fp32) and dw16/db16 (bf16) outputs, any may be null.
 int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, const float* mean, const float* rstd,
-              void* dx, float* dw, float* db, float* pdw, float* pdb, int M, int E, hipStream_t st) {
+              void* dx, float* dw, float* db, void* dw16, void* db16, float* ws, int M, int E, hipStream_t st) {
+    float* pdw = ws;
+    float* pdb = ws + (long)rn_ln_bwd_waves(M) * E;
     if (E % 8 != 0 || E > 8192) return -1;
     int nv = rn_ln_nv(E);
     int W = rn_ln_bwd_waves(M);
@@ -183,7 +178,10 @@ int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, cons
     else RN_LNB2(16)
 #undef RN_LNB2
 #undef RN_LNB
-    ln_finish_k<<<(E + 255) / 256, 256, 0, st>>>(pdw, pdb, dw, db, W, E);
+    // pdw/pdb are followed by 2 * RN_COLRED_S * E floats of scratch (see rn_ln_bwd_ws)
+    float* tmp = pdb + (long)W * E;
+    rn_colreduce(pdw, W, E, tmp, dw, (bf16*)dw16, st);
+    rn_colreduce(pdb, W, E, tmp + RN_COLRED_S * E, db, (bf16*)db16, st);
     return 0;
 }
 

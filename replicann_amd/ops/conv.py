@@ -44,7 +44,7 @@ class _ConvFn(torch.autograd.Function):
         w2 = weight.reshape(OC, K)
         if Kp != K:
             w2 = F.pad(w2, (0, Kp - K))
-        y = ops.gemm(cols, w2.contiguous(), False, True, bias, None, 0, None, None, False, 0, False)
+        y = ops.gemm(cols, w2.contiguous(), False, True, bias, None, 0, None, None, False, 0, False, None, -1)
         ctx.save_for_backward(x, cols, w2)
         ctx.meta = (N, H, W, C, OC, KH, KW, OH, OW, K, Kp, stride, pad, bias is not None)
         return y.reshape(N, OH, OW, OC)

@@ -53,18 +53,22 @@ def _act_grad_ref(dy: torch.Tensor, h: torch.Tensor, act: int) -> torch.Tensor:
 # raw GEMM entry point (used by linear, conv2d, attention fallbacks)
 # --------------------------------------------------------------------------
 def gemm(a, b, *, ta=False, tb=False, bias=None, residual=None, act=ACT_NONE, preact=None,
-         out=None, accumulate=False, split_k=0, out_dtype=None):
-    """C = act(op(A) @ op(B) + bias) + residual  (op = transpose if flag set).
+         out=None, accumulate=False, split_k=0, out_dtype=None, alpha=None, cfg=-1):
+    """C = act(alpha · op(A) @ op(B) + bias) + residual  (op = transpose if flag set).
 
     A, B are 2-D row-major bf16.  On CPU it is the ATen reference.
     ``accumulate`` adds into ``out`` (fp32 or bf16) instead of overwriting.
+    ``alpha`` is an optional 1-element fp32 DEVICE tensor (read in the epilogue,
+    graph-safe).  ``cfg`` forces a tile config (-1 = auto; 0..3 see gemm_bf16.hip).
     """
     if _ext.use_native(a):
         return _ext.ops().gemm(a, b, ta, tb, bias, residual, act, preact, out, accumulate, split_k,
-                               out_dtype == torch.float32)
+                               out_dtype == torch.float32, alpha, cfg)
     A = a.t() if ta else a
     B = b.t() if tb else b
     h = A.float() @ B.float()
+    if alpha is not None:
+        h = h * alpha.float()
     if bias is not None:
         h = h + bias.float()
     if preact is not None:
@@ -115,7 +119,7 @@ class _LinearFn(torch.autograd.Function):
         if act != ACT_NONE:
             preact = torch.empty(x2.shape[0], weight.shape[0], device=x.device, dtype=x.dtype)
         if native:
-            y = _ext.ops().gemm(x2, weight, False, True, bias, res2, act, preact, None, False, 0, False)
+            y = _ext.ops().gemm(x2, weight, False, True, bias, res2, act, preact, None, False, 0, False, None, -1)
         else:
             y = gemm(x2, weight, tb=True, bias=bias, residual=res2, act=act, preact=preact,
                      out_dtype=x.dtype)

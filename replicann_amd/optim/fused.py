@@ -3,6 +3,10 @@
 Mixed-precision policy (N23): model parameters live in bf16 (what the GEMMs
 read), the optimizer owns an fp32 master copy and fp32 moments.  One step is:
 
+0. ``opt_prep`` (1 thread): step counter, LR schedule (constant or warmup +
+   cosine) and Adam bias corrections are computed IN DEVICE MEMORY, so a
+   captured hipGraph of the whole training step replays correct per-step
+   hyper-parameters;
 1. ``grad_norm`` kernel: Σ g² over the flat bf16 gradient → a device scalar
    (block partials + a fixed-order final reduce: deterministic);
 2. ONE update kernel over every parameter: reads g (bf16), applies the DDP
@@ -35,7 +39,9 @@ class _FlatOptimizer:
         self.step_count = 0
         dev = flat.data.device
         self.master = flat.data.float() if flat.data.dtype != torch.float32 else flat.data
-        self.norm_buf = torch.zeros(2, dtype=torch.float32, device=dev)  # [‖g‖², skipped flag]
+        # device state: [‖g‖², skipped flag, step t, lr, bc1, bc2, -, -]
+        self.norm_buf = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.schedule = None  # (warmup, total, min_ratio) → warmup + cosine; None → constant lr
         self._wd_elem = None
 
     @property
@@ -58,6 +64,26 @@ class _FlatOptimizer:
     def zero_grad(self):
         self.flat.zero_grad()
 
+    def set_schedule(self, warmup, total, min_ratio=0.1):
+        """Warmup + cosine decay, evaluated on device each step (graph-safe)."""
+        self.schedule = (float(warmup), float(total), float(min_ratio))
+
+    def _host_lr(self, lr):
+        if lr is not None:
+            return lr
+        if self.schedule is None:
+            return self.lr
+        w, t, r = self.schedule
+        return cosine_lr(self.step_count - 1, self.lr, int(w), int(t), r)
+
+    def _prep(self, lr, b1=0.0, b2=0.0):
+        w, t, r = self.schedule if self.schedule is not None else (0.0, 1.0, 1.0)
+        _ext.ops().opt_prep(self.norm_buf, self.lr, w, t, r, self.schedule is not None,
+                            -1.0 if lr is None else float(lr), b1, b2)
+
+    def skipped_last_step(self):
+        return bool(self.norm_buf[1].item())
+
 
 class FusedAdamW(_FlatOptimizer):
     def __init__(self, flat: FlatParams, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
@@ -68,19 +94,21 @@ class FusedAdamW(_FlatOptimizer):
         self.v = torch.zeros_like(self.master)
 
     def step(self, lr=None):
-        lr = self.lr if lr is None else lr
+        """One update.  ``lr`` overrides the schedule for this step (eager use only:
+        under graph capture leave it None so the device schedule is used)."""
         self.step_count += 1
         b1, b2 = self.betas
-        bc1 = 1 - b1 ** self.step_count
-        bc2 = 1 - b2 ** self.step_count
         clip = self.max_grad_norm if self.max_grad_norm else 0.0
         if self.native:
             ops = _ext.ops()
+            self._prep(lr, b1, b2)
             ops.sumsq(self.flat.grad, self.norm_buf)
             ops.adamw_step(self.flat.data, self.master, self.flat.grad, self.m, self.v, self.flat.wd_mask,
-                           self.norm_buf, lr, b1, b2, self.eps, self.weight_decay, bc1, bc2,
-                           self.grad_scale, clip)
+                           self.norm_buf, b1, b2, self.eps, self.weight_decay, self.grad_scale, clip)
             return
+        lr = self._host_lr(lr)
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
         g = self.flat.grad.float() * self.grad_scale
         norm = g.pow(2).sum().sqrt()
         if not torch.isfinite(norm):
@@ -100,6 +128,7 @@ class FusedAdamW(_FlatOptimizer):
 
     def load_state_dict(self, sd):
         self.step_count = sd["step"]
+        self.norm_buf[2] = float(self.step_count)
         self.master.copy_(sd["master"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
@@ -117,17 +146,17 @@ class FusedSGD(_FlatOptimizer):
         self.buf = torch.zeros_like(self.master)
 
     def step(self, lr=None):
-        lr = self.lr if lr is None else lr
         self.step_count += 1
         clip = self.max_grad_norm if self.max_grad_norm else 0.0
         first = self.step_count == 1
         if self.native:
             ops = _ext.ops()
+            self._prep(lr)
             ops.sumsq(self.flat.grad, self.norm_buf)
             ops.sgd_step(self.flat.data, self.master, self.flat.grad, self.buf, self.flat.wd_mask,
-                         self.norm_buf, lr, self.momentum, self.weight_decay, self.nesterov, first,
-                         self.grad_scale, clip)
+                         self.norm_buf, self.momentum, self.weight_decay, self.nesterov, self.grad_scale, clip)
             return
+        lr = self._host_lr(lr)
         g = self.flat.grad.float() * self.grad_scale
         norm = g.pow(2).sum().sqrt()
         if not torch.isfinite(norm):
@@ -149,6 +178,7 @@ class FusedSGD(_FlatOptimizer):
 
     def load_state_dict(self, sd):
         self.step_count = sd["step"]
+        self.norm_buf[2] = float(self.step_count)
         self.master.copy_(sd["master"])
         self.buf.copy_(sd["buf"])
         self.flat.data.copy_(self.master)

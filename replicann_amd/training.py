@@ -74,6 +74,7 @@ class TrainConfig:
     grad_accum: int = 1
     max_grad_norm: float = 1.0
     bucket_mb: float = 64.0
+    graph: str = "auto"           # auto | on | off — capture the whole step in one hipGraph
     log_every: int = 10
     metrics_path: str | None = None
     checkpoint: str | None = None
@@ -106,7 +107,9 @@ class Trainer:
         else:
             self.opt = FusedSGD(self.flat, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
                                 max_grad_norm=cfg.max_grad_norm, grad_scale=gs)
+        self.opt.set_schedule(cfg.warmup_steps, max(cfg.steps, 1), cfg.min_lr_ratio)
         self.step_idx = 0
+        self._graph = None
         if cfg.resume:
             self.step_idx, _ = load_checkpoint(cfg.resume, self.model, self.opt)
             if self.ddp is not None:
@@ -135,14 +138,12 @@ class Trainer:
     def samples_per_step(self):
         return self.cfg.batch_size * self.cfg.grad_accum * self.world
 
-    def step(self, lr=None):
-        """One optimizer step; returns the (device) loss of the last micro-batch."""
+    def _step_body(self, batches, lr=None):
         c = self.cfg
         self.opt.zero_grad()
         loss = None
-        for micro in range(c.grad_accum):
-            x, y = next(self.data)
-            sync_ctx = (self.ddp.no_sync() if (self.ddp is not None and micro < c.grad_accum - 1)
+        for micro, (x, y) in enumerate(batches):
+            sync_ctx = (self.ddp.no_sync() if (self.ddp is not None and micro < len(batches) - 1)
                         else contextlib.nullcontext())
             with sync_ctx:
                 with phase("forward"):
@@ -154,6 +155,57 @@ class Trainer:
                 self.ddp.finish()
         with phase("optimizer"):
             self.opt.step(lr)
+        return loss.detach()
+
+    def graph_enabled(self):
+        c = self.cfg
+        if c.graph == "off" or self.device.type != "cuda":
+            return False
+        if c.graph == "on":
+            return True
+        # auto: single process, no stochastic ops whose seeds would freeze in a graph
+        dropout = getattr(getattr(self.model, "config", None), "dropout", 0.0)
+        return self.world == 1 and not dropout
+
+    def _capture(self):
+        """Capture zero_grad → fwd → bwd → (all-reduce) → optimizer as ONE hipGraph.
+
+        Inputs are copied into static buffers before each replay; the LR
+        schedule / bias corrections are device-side, so replays are exact.
+        The warm-up iterations on the side stream are real training steps."""
+        c = self.cfg
+        self._static = [tuple(t.clone() for t in next(self.data)) for _ in range(c.grad_accum)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._step_body(self._static)
+                self.step_idx += 1
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._static_loss = self._step_body(self._static)
+        self._graph = g
+
+    def step(self, lr=None):
+        """One optimizer step; returns the (device) loss of the last micro-batch.
+
+        ``lr`` (eager mode only) overrides the device-side schedule."""
+        c = self.cfg
+        if lr is None and self.graph_enabled():
+            if self._graph is None:
+                self._capture()
+            for (sx, sy) in self._static:
+                x, y = next(self.data)
+                sx.copy_(x, non_blocking=True)
+                sy.copy_(y, non_blocking=True)
+            self._graph.replay()
+            self.opt.step_count += 1
+            self.step_idx += 1
+            return self._static_loss
+        batches = [next(self.data) for _ in range(c.grad_accum)]
+        loss = self._step_body(batches, lr)
         self.step_idx += 1
         return loss
 
@@ -164,14 +216,16 @@ class Trainer:
     def run(self):
         c = self.cfg
         t0 = time.time()
+        start = self.step_idx
         last = None
-        for i in range(self.step_idx, c.steps):
-            loss = self.step(self.lr_at(i))
-            if (i + 1) % c.log_every == 0 or i + 1 == c.steps:
+        while self.step_idx < c.steps:
+            loss = self.step()
+            i = self.step_idx
+            if i % c.log_every == 0 or i >= c.steps:
                 lv = float(loss)
                 dt = time.time() - t0
-                self.logger.log(step=i + 1, loss=round(lv, 5), samples_per_s=round(
-                    self.samples_per_step() * (i + 1 - self.step_idx) / max(dt, 1e-9), 2))
+                self.logger.log(step=i, loss=round(lv, 5), lr=round(float(self.opt._host_lr(None)), 8),
+                                samples_per_s=round(self.samples_per_step() * (i - start) / max(dt, 1e-9), 2))
                 last = lv
         if c.checkpoint:
             save_checkpoint(c.checkpoint, self.model, self.opt, c.steps, asdict(c))

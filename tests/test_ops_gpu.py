@@ -26,16 +26,24 @@ def test_native_loaded(cuda):
 
 
 # ----------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 96), (1000, 384, 520), (64, 24, 8)])
-def test_gemm_layouts(cuda, ta, tb, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 96), (1000, 384, 520), (64, 24, 8), (520, 776, 1088)])
+def test_gemm_layouts(cuda, ta, tb, M, N, K, cfg):
     torch.manual_seed(0)
     a = bf(K, M) if ta else bf(M, K)
     b = bf(N, K) if tb else bf(K, N)
     ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
-    out = ops.gemm(a, b, ta=ta, tb=tb)
+    out = ops.gemm(a, b, ta=ta, tb=tb, cfg=cfg)
     assert out.shape == (M, N)
     assert rel_err(out, ref) < 1e-2
+
+
+def test_gemm_alpha(cuda):
+    a, b = bf(300, 128), bf(200, 128)
+    alpha = torch.tensor([0.25], device="cuda")
+    out = ops.gemm(a, b, tb=True, alpha=alpha)
+    assert rel_err(out, 0.25 * (a.float() @ b.float().t())) < 1e-2
 
 
 def test_gemm_identity_asymmetric(cuda):
@@ -62,13 +70,13 @@ def test_gemm_epilogue(cuda, act):
         assert rel_err(pre, h) < 1e-2
 
 
-@pytest.mark.parametrize("split", [2, 4, 8])
-def test_gemm_splitk_fp32_accumulate(cuda, split):
+@pytest.mark.parametrize("split,cfg", [(2, 0), (4, 1), (8, -1), (3, 2)])
+def test_gemm_splitk_fp32_accumulate(cuda, split, cfg):
     torch.manual_seed(2)
     M, N, K = 192, 320, 4096
     a, b = bf(K, M), bf(K, N)
     ref = a.float().t() @ b.float()
-    out = ops.gemm(a, b, ta=True, split_k=split, out_dtype=torch.float32)
+    out = ops.gemm(a, b, ta=True, split_k=split, out_dtype=torch.float32, cfg=cfg)
     assert out.dtype == torch.float32 and rel_err(out, ref) < 5e-3
     acc = torch.ones(M, N, device="cuda")
     ops.gemm(a, b, ta=True, split_k=split, out=acc, accumulate=True)
