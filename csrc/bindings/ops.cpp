@@ -24,17 +24,17 @@ void rn_act_fwd(const void*, void*, long, int, hipStream_t);
 void rn_act_bwd(const void*, const void*, void*, long, int, hipStream_t);
 void rn_dropout(const void*, void*, long, float, uint64_t, hipStream_t);
 void rn_add(const void*, const void*, void*, long, int, hipStream_t);
-void rn_bias_act_grad(const void*, const void*, void*, float*, void*, float*, int, int, int, int, hipStream_t);
+void rn_bias_act_grad(const void*, const void*, void*, float*, void*, float*, int, int, int, int, int, hipStream_t);
 int rn_bias_act_grad_splits(int, int);
 int rn_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
               hipStream_t);
 int rn_ln_bwd_waves(int);
 long rn_ln_bwd_ws(int, int);
 int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
-              void*, void*, float*, int, int, hipStream_t);
+              void*, void*, float*, int, int, int, hipStream_t);
 void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
 void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
-void rn_xent_fwd(const void*, const int64_t*, float*, float*, int, int, int, long, hipStream_t);
+void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int, hipStream_t);
 void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
 void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, hipStream_t);
 void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
@@ -113,9 +113,11 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         TORCH_CHECK(preact->size(0) == M && preact->size(1) == N && preact->stride(0) == c.stride(0));
     }
     if (M == 0 || N == 0) return c;
-    int split = (int)std::max<int64_t>(1, split_k);
+    int split = split_k < 0 ? -1 : (int)std::max<int64_t>(1, split_k);
     Tensor ws;
-    if (split > 1) ws = at::empty({rn_gemm_ws_floats(M, N, split)}, a.options().dtype(at::kFloat));
+    // auto split (-1) may pick up to 32 slabs: size the workspace for the worst case only when K allows it
+    const int max_split = split < 0 ? (int)std::min<int64_t>(32, std::max<int64_t>(1, K / 512)) : split;
+    if (max_split > 1) ws = at::empty({rn_gemm_ws_floats(M, N, max_split)}, a.options().dtype(at::kFloat));
     // K must be a multiple of 8 (16-B rows); pad both operands with zeros otherwise
     Tensor A = a, B = b;
     int64_t Kp = K;
@@ -137,7 +139,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     if (c.stride(0) % 4 != 0 && (bias || residual)) { /* epilogue handles unaligned via scalar path */ }
     if (alpha && alpha->defined()) TORCH_CHECK(alpha->scalar_type() == at::kFloat && alpha->is_cuda());
     int rc = rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
-                     preact && preact->defined() ? preact->data_ptr() : nullptr, split > 1 ? ws.data_ptr<float>() : nullptr,
+                     preact && preact->defined() ? preact->data_ptr() : nullptr, max_split > 1 ? ws.data_ptr<float>() : nullptr,
                      alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr, (int)M, (int)N, (int)Kp, A.stride(0),
                      B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32, accumulate, (int)cfg, cur_stream());
     TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
@@ -145,19 +147,22 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
 }
 
 // returns (dH, db) with db in bf16 (the parameter dtype)
-std::tuple<Tensor, Tensor> bias_act_grad(const Tensor& dy, const optional<Tensor>& h, int64_t act, bool want_bias) {
+std::tuple<Tensor, Tensor> bias_act_grad(const Tensor& dy, const optional<Tensor>& h, int64_t act, bool want_bias,
+                                         const optional<Tensor>& db_accum) {
     CHECK_CUDA(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
     GUARD(dy);
     const int M = dy.size(0), N = dy.size(1);
     Tensor dh = act != 0 ? at::empty_like(dy) : dy;
-    Tensor db = at::empty({want_bias ? N : 0}, dy.options());
+    const bool accum = db_accum && db_accum->defined();
+    if (accum) { CHECK_BF16(*db_accum); TORCH_CHECK(db_accum->numel() == N && db_accum->is_contiguous()); }
+    Tensor db = accum ? *db_accum : at::empty({want_bias ? N : 0}, dy.options());
     Tensor part = at::empty({want_bias ? (int64_t)(rn_bias_act_grad_splits(M, N) + 32) * N : 1},
                             dy.options().dtype(at::kFloat));
     if (act != 0) { TORCH_CHECK(h && h->defined(), "activation grad needs the pre-activation"); CHECK_CONTIG(*h); }
     if (M > 0)
         rn_bias_act_grad(dy.data_ptr(), optr(h), dh.data_ptr(), nullptr, want_bias ? db.data_ptr() : nullptr,
-                         part.data_ptr<float>(), M, N, (int)act, want_bias, cur_stream());
-    else if (want_bias) db.zero_();
+                         part.data_ptr<float>(), M, N, (int)act, want_bias, accum, cur_stream());
+    else if (want_bias && !accum) db.zero_();
     return {dh, db};
 }
 
@@ -201,14 +206,15 @@ Tensor softmax_bwd(const Tensor& dy, const Tensor& y, double scale) {
     if (dy.numel()) rn_softmax_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), y.size(0), y.size(1), (float)scale, cur_stream());
     return dx;
 }
-std::tuple<Tensor, Tensor> xent_fwd(const Tensor& logits, const Tensor& target, int64_t nvalid, int64_t ignore) {
+std::tuple<Tensor, Tensor> xent_fwd(const Tensor& logits, const Tensor& target, int64_t nvalid, int64_t ignore,
+                                    bool write_grad) {
     CHECK_BF16(logits); CHECK_CONTIG(logits); GUARD(logits);
     TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous());
     const int M = logits.size(0), V = logits.size(1);
     Tensor loss = at::empty({M}, logits.options().dtype(at::kFloat));
     Tensor lse = at::empty({M}, logits.options().dtype(at::kFloat));
     if (M) rn_xent_fwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), M, V,
-                       (int)nvalid, (long)ignore, cur_stream());
+                       (int)nvalid, (long)ignore, write_grad, cur_stream());
     return {loss, lse};
 }
 void xent_bwd(const Tensor& logits, const Tensor& target, const Tensor& lse, const Tensor& gscale, const Tensor& grad,
@@ -237,19 +243,21 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const 
     return {y, h, mean, rstd};
 }
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optional<Tensor>& gh, const Tensor& h,
-                                                 const Tensor& w, const Tensor& mean, const Tensor& rstd) {
+                                                 const Tensor& w, const Tensor& mean, const Tensor& rstd,
+                                                 const optional<Tensor>& dw_accum, const optional<Tensor>& db_accum) {
     CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(h); GUARD(dy);
     const int M = dy.size(0), E = dy.size(1);
     Tensor dx = at::empty_like(dy);
-    Tensor dw = at::empty({E}, w.options());  // parameter dtype (bf16)
-    Tensor db = at::empty({E}, w.options());
+    const bool accum = dw_accum && dw_accum->defined() && db_accum && db_accum->defined();
+    Tensor dw = accum ? *dw_accum : at::empty({E}, w.options());  // parameter dtype (bf16)
+    Tensor db = accum ? *db_accum : at::empty({E}, w.options());
     Tensor part = at::empty({rn_ln_bwd_ws(M, E)}, dy.options().dtype(at::kFloat));
     if (M) {
         int rc = rn_ln_bwd(dy.data_ptr(), optr(gh), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), dx.data_ptr(), nullptr, nullptr, dw.data_ptr(), db.data_ptr(),
-                           part.data_ptr<float>(), M, E, cur_stream());
+                           part.data_ptr<float>(), M, E, accum, cur_stream());
         TORCH_CHECK(rc == 0, "layernorm_bwd: unsupported E=", E);
-    } else { dw.zero_(); db.zero_(); }
+    } else if (!accum) { dw.zero_(); db.zero_(); }
     return {dx, dw, db};
 }
 
@@ -467,17 +475,18 @@ int64_t native_version() { return 1; }
 TORCH_LIBRARY(replicann, m) {
     m.def("gemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, Tensor? residual, int act, Tensor? preact, "
           "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1) -> Tensor");
-    m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias) -> (Tensor, Tensor)");
+    m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias, Tensor(a!)? db_accum=None) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
     m.def("dropout_fwd(Tensor x, float p, int seed) -> Tensor");
     m.def("add_act(Tensor a, Tensor b, bool relu) -> Tensor");
     m.def("softmax_fwd(Tensor x, float scale) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y, float scale) -> Tensor");
-    m.def("xent_fwd(Tensor logits, Tensor target, int nvalid, int ignore) -> (Tensor, Tensor)");
+    m.def("xent_fwd(Tensor(a!) logits, Tensor target, int nvalid, int ignore, bool write_grad=False) -> (Tensor, Tensor)");
     m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale, Tensor(a!) grad, int nvalid, int ignore) -> ()");
     m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
-    m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
+    m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd, "
+          "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None) -> (Tensor, Tensor, Tensor)");
     m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
     m.def("embedding_bwd(Tensor dx, Tensor ids, int V, int Tp) -> (Tensor, Tensor)");
     m.def("sumsq(Tensor g, Tensor(a!) normbuf) -> ()");

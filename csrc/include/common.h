@@ -140,22 +140,22 @@ __global__ void __launch_bounds__(256) rn_colred1_k(const float* __restrict__ in
 }
 
 __global__ void rn_colred2_k(const float* __restrict__ tmp, int S, int C, float* __restrict__ out32,
-                             __bf16* __restrict__ out16) {
+                             __bf16* __restrict__ out16, int accum) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     float s = 0.f;
     for (int i = 0; i < S; ++i) s += tmp[(long)i * C + c];
-    if (out32) out32[c] = s;
-    if (out16) out16[c] = (__bf16)s;
+    if (out32) out32[c] = s + (accum ? out32[c] : 0.f);
+    if (out16) out16[c] = (__bf16)(s + (accum ? (float)out16[c] : 0.f));
 }
 
-// tmp must hold RN_COLRED_S * C floats
+// tmp must hold RN_COLRED_S * C floats.  accum: add into the outputs (gradient accumulation).
 static inline void rn_colreduce(const float* in, int R, int C, float* tmp, float* out32, __bf16* out16,
-                                hipStream_t st) {
+                                hipStream_t st, int accum = 0) {
     int S = R < RN_COLRED_S ? (R > 0 ? R : 1) : RN_COLRED_S;
     dim3 g((C + 63) / 64, S);
     rn_colred1_k<<<g, 256, 0, st>>>(in, R, C, tmp);
-    rn_colred2_k<<<(C + 255) / 256, 256, 0, st>>>(tmp, S, C, out32, out16);
+    rn_colred2_k<<<(C + 255) / 256, 256, 0, st>>>(tmp, S, C, out32, out16, accum);
 }
 
 }  // namespace

@@ -20,9 +20,9 @@
 //   * online softmax in exp2 domain; causal tiles above the diagonal are
 //     skipped, diagonal tiles masked; heaviest causal blocks launch first;
 //   * dropout on P by a stateless counter hash, regenerated in the backward;
-//   * backward = delta kernel (rowsum dO·O) + dK/dV kernel (one workgroup per
-//     64 keys, loops over queries) + dQ kernel (one workgroup per 64 queries,
-//     loops over keys): no atomics, bitwise deterministic.
+//   * backward = dQ kernel (one workgroup per 64 queries, loops over keys; also
+//     emits delta = rowsum(dO·O) from registers) + dK/dV kernel (one workgroup
+//     per 64 keys, loops over queries): no atomics, bitwise deterministic.
 // Generic path (any D ≤ 256, used by the reference-parity blocks with small
 // head sizes): straightforward per-query-row kernels with fp32 scores in LDS.
 #include "common.h"
@@ -440,7 +440,24 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
     }
     const bool qok = qg < p.Tq;
     const float lse2 = qok ? p.lse[((long)b * p.H + h) * p.Tq + qg] * LOG2E : INFINITY;
-    const float dl = qok ? p.delta[((long)b * p.H + h) * p.Tq + qg] : 0.f;
+    // delta = rowsum(dO ∘ O), computed here from the dO fragments already in
+    // registers (no separate delta kernel); written out for the dK/dV kernel.
+    float dl;
+    {
+        const bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
+        float part = 0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            s16x8 of = gload16(obase + (long)qg * p.o_st + s * 32 + g * 8, qok);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                part += (float)__builtin_bit_cast(bf16, (short)of[j]) * (float)__builtin_bit_cast(bf16, (short)df[s][j]);
+        }
+        part += __shfl_xor(part, 16, 64);
+        part += __shfl_xor(part, 32, 64);
+        dl = part;
+        if (qok && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qg] = dl;
+    }
     f32x4 dqacc[4];
 #pragma unroll
     for (int jd = 0; jd < 4; ++jd) dqacc[jd] = (f32x4){0, 0, 0, 0};
@@ -688,11 +705,11 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
                       (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
                       (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
     if (fast) {
-        attn_delta_k<<<(int)(((long)B * Tq * H + 255) / 256), 256, 0, st>>>(a);
-        dim3 g1((Tk + 63) / 64, B * H);
-        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 32768, st, a);
+        // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2((Tq + 63) / 64, B * H);
         RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
+        dim3 g1((Tk + 63) / 64, B * H);
+        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 32768, st, a);
     } else {
         if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
         dim3 grid(Tq, B * H);

@@ -162,7 +162,7 @@ void rn_add(const void* a, const void* b, void* y, long n, int relu, hipStream_t
 
 // part: workspace of >= (splits + RN_COLRED_S) * N floats.  db (fp32) / db16 (bf16) written if want_bias.
 void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, void* db16, float* part, int M, int N,
-                      int act, int want_bias, hipStream_t st) {
+                      int act, int want_bias, int accum, hipStream_t st) {
     int cblocks = (N + 511) / 512;
     int splits = 1;
     while (cblocks * splits < 512 && M / (splits * 2) >= 32) splits *= 2;
@@ -173,7 +173,7 @@ void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, void* 
     else if (act == ACT_RELU) { if (want_bias) RN_BAG(ACT_RELU, true); else RN_BAG(ACT_RELU, false); }
     else { if (want_bias) RN_BAG(ACT_NONE, true); else return; }
 #undef RN_BAG
-    if (want_bias) rn_colreduce(part, splits, N, part + (long)splits * N, db, (bf16*)db16, st);
+    if (want_bias) rn_colreduce(part, splits, N, part + (long)splits * N, db, (bf16*)db16, st, accum);
 }
 
 int rn_bias_act_grad_splits(int M, int N) {

@@ -55,15 +55,33 @@ namespace {
 
 inline long ntiles(int M, int N, int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
 
-// Heuristic tile choice: the biggest tile that still yields ~a full wave of CUs.
-int pick_cfg(int M, int N, int split) {
-    const long t256 = ntiles(M, N, 256, 256) * split;
-    if (t256 >= 224) return 1;
-    const long t_mw = ntiles(M, N, 256, 128) * split, t_nw = ntiles(M, N, 128, 256) * split;
-    if (t_mw >= 224 || t_nw >= 224) return t_mw >= t_nw ? 2 : 3;
-    return 0;
-}
+// Tile-config / split-K chooser: a wave-quantisation cost model calibrated on
+// MI355X measurements of this kernel (scripts/microbench.py).  A 128² block runs
+// 2 per CU, a 256² block 1 per CU and ~13 % faster per FLOP (half the L2→LDS
+// bytes per FLOP); a launch takes ceil(tiles / resident slots) rounds.
+struct Choice { int cfg, split; };
 
+inline Choice pick(int M, int N, int K, int split_req) {
+    const double flop_s_cu = 2.9e12;  // effective per-CU bf16 rate of the 128² config
+    const double cand_rate[4] = {1.0, 1.13, 1.0, 1.0};
+    const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, slots[4] = {512, 256, 256, 256};
+    Choice best = {0, 1};
+    double best_t = 1e30;
+    for (int c = 0; c < 4; ++c) {
+        for (int sp = 1; sp <= 32; sp *= 2) {
+            if (split_req > 0 && sp != split_req) continue;
+            if (split_req <= 0 && sp > 1 && K / sp < 512) break;
+            const int kps = ((K + sp - 1) / sp + 63) / 64 * 64;
+            const long tiles = ntiles(M, N, bm[c], bn[c]) * sp;
+            const long rounds = (tiles + slots[c] - 1) / slots[c];
+            const double per_block = 2.0 * bm[c] * bn[c] * kps / (flop_s_cu * cand_rate[c]) * (c == 0 ? 2.0 : 1.0);
+            double t = rounds * per_block;
+            if (sp > 1) t += ((double)M * N * (4.0 * sp + 2.0)) / 4.0e12 + 3e-6;
+            if (t < best_t * 0.98) { best_t = t; best = {c, sp}; }
+        }
+    }
+    return best;
+}
 }  // namespace
 
 extern "C" {
@@ -74,7 +92,7 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 // C[M,N] = act(alpha · op(A)[M,K] · op(B)[K,N] + bias) + res.
 //   trans_a = 0: A stored [M][lda] (K contiguous);   1: A stored [K][lda] (M contiguous)
 //   trans_b = 0: B stored [K][ldb] (N contiguous);   1: B stored [N][ldb] (K contiguous)
-//   cfg: -1 auto, 0 = 128x128, 1 = 256x256, 2 = 256x128, 3 = 128x256
+//   cfg: -1 auto, 0 = 128x128, 1 = 256x256, 2 = 256x128, 3 = 128x256;  split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
@@ -87,6 +105,11 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     GemmArgs a;
     a.A = (const bf16*)A; a.B = (const bf16*)B; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
     a.pre = (bf16*)pre; a.ws = ws; a.alpha = alpha; a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+    if (cfg < 0 || split < 0) {
+        Choice ch = pick(M, N, K, split);
+        if (cfg < 0) cfg = ch.cfg;
+        if (split < 0) split = ch.split;
+    }
     a.split = split < 1 ? 1 : split;
     int kps = (K + a.split - 1) / a.split;
     kps = (kps + BK - 1) / BK * BK;
@@ -94,7 +117,6 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     a.split = (K + kps - 1) / kps;
     a.out_f32 = out_f32; a.accumulate = accumulate;
     const bool ak = !trans_a, bk = trans_b;
-    if (cfg < 0) cfg = pick_cfg(M, N, a.split);
     switch (cfg) {
         case 1: rn_gemm_launch_cfg1(a, ak, bk, act, st); break;
         case 2: rn_gemm_launch_cfg2(a, ak, bk, act, st); break;

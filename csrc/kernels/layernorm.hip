@@ -165,7 +165,8 @@ long rn_ln_bwd_ws(int M, int E) { return 2L * rn_ln_bwd_waves(M) * E + 2L * RN_C
 
 // ws: rn_ln_bwd_ws(M, E) floats.  dw/db (fp32) and dw16/db16 (bf16) outputs, any may be null.
 int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, const float* mean, const float* rstd,
-              void* dx, float* dw, float* db, void* dw16, void* db16, float* ws, int M, int E, hipStream_t st) {
+              void* dx, float* dw, float* db, void* dw16, void* db16, float* ws, int M, int E, int accum,
+              hipStream_t st) {
     float* pdw = ws;
     float* pdb = ws + (long)rn_ln_bwd_waves(M) * E;
     if (E % 8 != 0 || E > 8192) return -1;
@@ -180,8 +181,8 @@ int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, cons
 #undef RN_LNB
     // pdw/pdb are followed by 2 * RN_COLRED_S * E floats of scratch (see rn_ln_bwd_ws)
     float* tmp = pdb + (long)W * E;
-    rn_colreduce(pdw, W, E, tmp, dw, (bf16*)dw16, st);
-    rn_colreduce(pdb, W, E, tmp + RN_COLRED_S * E, db, (bf16*)db16, st);
+    rn_colreduce(pdw, W, E, tmp, dw, (bf16*)dw16, st, accum);
+    rn_colreduce(pdb, W, E, tmp + RN_COLRED_S * E, db, (bf16*)db16, st, accum);
     return 0;
 }
 

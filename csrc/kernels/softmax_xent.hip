@@ -87,18 +87,44 @@ __global__ void __launch_bounds__(TPB) softmax_bwd_k(const bf16* __restrict__ dy
         dx[base + i] = f2bf(scale * bf2f(y[base + i]) * (bf2f(dy[base + i]) - d));
 }
 
-__global__ void __launch_bounds__(TPB) xent_fwd_k(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+// GRAD: also overwrite the row with the UNSCALED gradient softmax - onehot (0 in
+// padded columns / ignored rows); the caller folds g/n into the consumers (the
+// LM-head GEMM epilogues' alpha), so the logits are read from HBM once per step.
+template <bool GRAD>
+__global__ void __launch_bounds__(TPB) xent_fwd_k(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                   float* __restrict__ loss, float* __restrict__ lse_out, int V,
                                                   int nvalid, long ignore) {
     __shared__ float sm[16];
-    const bf16* row = logits + (long)blockIdx.x * V;
+    bf16* row = logits + (long)blockIdx.x * V;
     float m, s;
     row_ms(row, nvalid, 1.f, m, s, sm);
+    const float lse = m + __logf(s);
+    const long t = tgt[blockIdx.x];
+    const bool ign = (t == ignore || t < 0 || t >= nvalid);
     if (threadIdx.x == 0) {
-        float lse = m + __logf(s);
         lse_out[blockIdx.x] = lse;
-        long t = tgt[blockIdx.x];
-        loss[blockIdx.x] = (t == ignore || t < 0 || t >= nvalid) ? 0.f : lse - bf2f(row[t]);
+        loss[blockIdx.x] = ign ? 0.f : lse - bf2f(row[t]);
+    }
+    if constexpr (GRAD) {
+        __syncthreads();  // the target logit was read above before anyone overwrites it
+        const float z = ign ? 0.f : 1.f;
+        if (V % 8 == 0) {
+            for (int i = threadIdx.x; i < V / 8; i += TPB) {
+                float f[8];
+                load8(row + i * 8, f);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int c = i * 8 + j;
+                    f[j] = (c < nvalid ? __expf(f[j] - lse) - (c == t ? 1.f : 0.f) : 0.f) * z;
+                }
+                store8(row + i * 8, f);
+            }
+        } else {
+            for (int c = threadIdx.x; c < V; c += TPB) {
+                const float p = c < nvalid ? __expf(bf2f(row[c]) - lse) - (c == t ? 1.f : 0.f) : 0.f;
+                row[c] = f2bf(p * z);
+            }
+        }
     }
 }
 
@@ -141,9 +167,10 @@ void rn_softmax_fwd(const void* x, void* y, int M, int N, float scale, hipStream
 void rn_softmax_bwd(const void* dy, const void* y, void* dx, int M, int N, float scale, hipStream_t st) {
     softmax_bwd_k<<<M, TPB, 0, st>>>((const bf16*)dy, (const bf16*)y, (bf16*)dx, N, scale);
 }
-void rn_xent_fwd(const void* logits, const int64_t* tgt, float* loss, float* lse, int M, int V, int nvalid,
-                 long ignore, hipStream_t st) {
-    xent_fwd_k<<<M, TPB, 0, st>>>((const bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
+void rn_xent_fwd(void* logits, const int64_t* tgt, float* loss, float* lse, int M, int V, int nvalid, long ignore,
+                 int write_grad, hipStream_t st) {
+    if (write_grad) xent_fwd_k<true><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
+    else xent_fwd_k<false><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
 }
 void rn_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* grad, int M,
                  int V, int nvalid, long ignore, hipStream_t st) {

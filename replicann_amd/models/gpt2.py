@@ -63,6 +63,7 @@ class GPT2(nn.Module):
         nn.init.normal_(self.wpe, std=0.01)
         with torch.no_grad():
             self.wte[cfg.vocab_size:].zero_()
+        self.wte._rn_shared = True  # tied: embedding + LM head both contribute gradients
         self.h = nn.ModuleList(
             PreLNBlock(cfg.n_embd, cfg.n_head, causal=True, dropout=cfg.dropout, n_layer=cfg.n_layer,
                        eps=cfg.ln_eps)
@@ -91,11 +92,9 @@ class GPT2(nn.Module):
         With ``targets`` only the loss is returned (logits are consumed in place).
         """
         h = self.hidden(idx)
-        logits = ops.linear(h, self.wte)
         if targets is None:
-            return logits[..., : self.config.vocab_size]
-        return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1),
-                                 n_valid_cols=self.config.vocab_size, inplace_grad=True)
+            return ops.linear(h, self.wte)[..., : self.config.vocab_size]
+        return ops.linear_cross_entropy(h, self.wte, targets, n_valid_cols=self.config.vocab_size)
 
     def flops_per_token(self, T=None):
         """Training FLOPs per token (fwd+bwd): 6·N_matmul + attention (causal)."""

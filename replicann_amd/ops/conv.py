@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _ext
-from .linear import gemm, _pick_split_k
+from .linear import gemm
 
 
 def _out_hw(H, W, kh, kw, stride, pad):
@@ -60,8 +60,7 @@ class _ConvFn(torch.autograd.Function):
             _, gb = ops.bias_act_grad(gy2, None, 0, True)
             gb = gb.to(w2.dtype)
         if ctx.needs_input_grad[1]:
-            sk = _pick_split_k(OC, Kp, gy2.shape[0])
-            gw = gemm(gy2, cols, ta=True, split_k=sk, out_dtype=w2.dtype)[:, :K].reshape(OC, KH, KW, C)
+            gw = gemm(gy2, cols, ta=True, split_k=-1, out_dtype=w2.dtype)[:, :K].reshape(OC, KH, KW, C)
         if ctx.needs_input_grad[0]:
             dcols = gemm(gy2, w2, out_dtype=x.dtype)
             if KH == 1 and KW == 1 and stride == 1 and pad == 0 and Kp == K:

@@ -96,6 +96,22 @@ def bias_act_grad(dy2d, h2d, act, want_bias):
     return dh, db
 
 
+def _direct_grad(p):
+    """The flat-buffer ``.grad`` view of parameter ``p`` if its gradient may be
+    accumulated directly by a backward kernel (GEMM epilogue / reduction with
+    ``accumulate``), bypassing autograd's AccumulateGrad add.  Only parameters
+    that are used once per forward qualify (tied weights are flagged shared)."""
+    f = getattr(p, "_rn_flat", None)
+    if f is None or not f.direct or getattr(p, "_rn_shared", False) or p.grad is None:
+        return None
+    return p.grad
+
+
+def _notify(p):
+    """Tell the flat buffer (and thus DDP's bucketing) that ``p``'s gradient is final."""
+    p._rn_flat.mark_ready(p)
+
+
 def _pick_split_k(m_out: int, n_out: int, k: int) -> int:
     tiles = math.ceil(m_out / 128) * math.ceil(n_out / 128)
     if tiles >= 512 or k < 1024:
@@ -124,6 +140,7 @@ class _LinearFn(torch.autograd.Function):
             y = gemm(x2, weight, tb=True, bias=bias, residual=res2, act=act, preact=preact,
                      out_dtype=x.dtype)
         ctx.save_for_backward(x2, weight, preact)
+        ctx.bias_ref = bias
         ctx.act = act
         ctx.has_bias = bias is not None
         ctx.has_res = residual is not None
@@ -133,17 +150,32 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x2, weight, preact = ctx.saved_tensors
+        bias = ctx.bias_ref
         gy2 = gy.reshape(-1, weight.shape[0])
         if not gy2.is_contiguous():
             gy2 = gy2.contiguous()
-        dh, db = bias_act_grad(gy2, preact, ctx.act, ctx.has_bias)
-        gx = gw = None
+        native = _ext.use_native(gy2)
+        gx = gw = gb = None
+        db_acc = _direct_grad(bias) if (native and ctx.has_bias and ctx.needs_input_grad[2]) else None
+        if native:
+            dh, db = _ext.ops().bias_act_grad(gy2, preact if ctx.act != ACT_NONE else None, ctx.act,
+                                              ctx.has_bias and ctx.needs_input_grad[2], db_acc)
+        else:
+            dh, db = bias_act_grad(gy2, preact, ctx.act, ctx.has_bias)
         if ctx.needs_input_grad[0]:
             gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
-            sk = _pick_split_k(weight.shape[0], weight.shape[1], x2.shape[0])
-            gw = gemm(dh, x2, ta=True, split_k=sk, out_dtype=weight.dtype)
-        gb = db.to(weight.dtype) if (db is not None and ctx.needs_input_grad[2]) else None
+            w_acc = _direct_grad(weight) if native else None
+            if w_acc is not None:  # accumulate straight into the flat gradient buffer
+                gemm(dh, x2, ta=True, split_k=-1, out=w_acc, accumulate=True)
+                _notify(weight)
+            else:
+                gw = gemm(dh, x2, ta=True, split_k=-1, out_dtype=weight.dtype)  # split-K chosen natively
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            if db_acc is not None:
+                _notify(bias)
+            else:
+                gb = db.to(weight.dtype)
         gres = gy if ctx.has_res else None
         return gx, gw, gb, None, gres
 

@@ -22,7 +22,7 @@ from .. import _ext
 class _XentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, n_valid_cols, ignore_index, inplace_grad):
-        loss_rows, lse = _ext.ops().xent_fwd(logits, target, n_valid_cols, ignore_index)
+        loss_rows, lse = _ext.ops().xent_fwd(logits, target, n_valid_cols, ignore_index, False)
         n = (target != ignore_index).sum().clamp_min(1).float()
         ctx.save_for_backward(logits, target, lse, n)
         ctx.n_valid_cols, ctx.ignore_index, ctx.inplace = n_valid_cols, ignore_index, inplace_grad
@@ -48,3 +48,54 @@ def cross_entropy(logits, target, *, n_valid_cols=None, ignore_index=-100, inpla
             lg = lg.contiguous()
         return _XentFn.apply(lg, tg.long().contiguous(), nv, ignore_index, inplace_grad)
     return F.cross_entropy(lg[:, :nv].float(), tg.long(), ignore_index=ignore_index)
+
+
+class _LinearXentFn(torch.autograd.Function):
+    """LM head + cross-entropy fused at the autograd level:
+    logits = h·Wᵀ (MFMA GEMM) → CE forward writes the UNSCALED gradient
+    (softmax − onehot) over the logits in place → backward runs the two LM-head
+    GEMMs on that buffer with alpha = g / n_valid read from device memory in
+    their epilogues.  The 1.6 GB logits tensor of a GPT-2 step is written once
+    and read twice (CE pass + the two backward GEMMs read it anyway)."""
+
+    @staticmethod
+    def forward(ctx, h, weight, target, n_valid_cols, ignore_index):
+        ops = _ext.ops()
+        shp = h.shape
+        h2 = h.reshape(-1, shp[-1]).contiguous()
+        logits = ops.gemm(h2, weight, False, True, None, None, 0, None, None, False, 0, False, None, -1)
+        tg = target.reshape(-1).long().contiguous()
+        loss_rows, _ = ops.xent_fwd(logits, tg, n_valid_cols, ignore_index, True)
+        n = (tg != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(h2, weight, logits, n)
+        ctx.shp = shp
+        return loss_rows.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        from .linear import _direct_grad, _notify
+        h2, weight, dlogits, n = ctx.saved_tensors
+        alpha = (g.float() / n).reshape(1)
+        ops = _ext.ops()
+        gh = gw = None
+        if ctx.needs_input_grad[0]:
+            gh = ops.gemm(dlogits, weight, False, False, None, None, 0, None, None, False, 0, False, alpha, -1)
+            gh = gh.reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            acc = _direct_grad(weight)
+            if acc is not None:
+                ops.gemm(dlogits, h2, True, False, None, None, 0, None, acc, True, -1, False, alpha, -1)
+                _notify(weight)
+            else:
+                gw = ops.gemm(dlogits, h2, True, False, None, None, 0, None, None, False, -1, False, alpha, -1)
+        return gh, gw, None, None, None
+
+
+def linear_cross_entropy(h, weight, target, *, n_valid_cols=None, ignore_index=-100):
+    """mean CE(h·weightᵀ, target) without materialising a separate logits gradient."""
+    nv = weight.shape[0] if n_valid_cols is None else n_valid_cols
+    if _ext.use_native(h):
+        return _LinearXentFn.apply(h, weight, target, nv, ignore_index)
+    logits = F.linear(h, weight)
+    return F.cross_entropy(logits.reshape(-1, logits.shape[-1])[:, :nv].float(), target.reshape(-1),
+                           ignore_index=ignore_index)

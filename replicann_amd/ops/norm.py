@@ -30,6 +30,7 @@ class _LayerNormFn(torch.autograd.Function):
         r2 = residual.reshape(-1, E).contiguous() if residual is not None else None
         y, h, mean, rstd = _ext.ops().layernorm_fwd(x2, r2, weight, bias, eps)
         ctx.save_for_backward(x2 if residual is None else h, weight, mean, rstd)
+        ctx.bias_ref = bias
         ctx.has_res = residual is not None
         ctx.has_bias = bias is not None
         ctx.shp = shp
@@ -39,12 +40,22 @@ class _LayerNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, gh=None):
+        from .linear import _direct_grad, _notify
         h, weight, mean, rstd = ctx.saved_tensors
+        bias = ctx.bias_ref
         E = ctx.shp[-1]
         gy2 = gy.reshape(-1, E).contiguous()
         gh2 = gh.reshape(-1, E).contiguous() if gh is not None else None
-        dx, dw, db = _ext.ops().layernorm_bwd(gy2, gh2, h, weight, mean, rstd)
+        dw_acc = _direct_grad(weight)
+        db_acc = _direct_grad(bias) if bias is not None else None
+        direct = dw_acc is not None and db_acc is not None
+        dx, dw, db = _ext.ops().layernorm_bwd(gy2, gh2, h, weight, mean, rstd, dw_acc if direct else None,
+                                              db_acc if direct else None)
         dx = dx.reshape(ctx.shp)
+        if direct:  # gradients already accumulated in the flat buffer
+            _notify(weight)
+            _notify(bias)
+            return dx, None, None, None, dx if ctx.has_res else None
         return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None,
                 dx if ctx.has_res else None)
 

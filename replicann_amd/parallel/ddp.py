@@ -77,6 +77,7 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         self._seen = set()
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p, _, _ in segs]
+        flat.ready_hooks.append(self._hook)  # parameters whose grads are accumulated directly by kernels
 
     # ------------------------------------------------------------------
     def _broadcast_state(self):

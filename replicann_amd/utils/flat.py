@@ -28,7 +28,7 @@ def _round(n: int, a: int = ALIGN) -> int:
 
 
 class FlatParams:
-    def __init__(self, module: nn.Module, dtype=None, device=None, grad_dtype=None):
+    def __init__(self, module: nn.Module, dtype=None, device=None, grad_dtype=None, direct=True):
         self.params = [p for p in module.parameters() if p.requires_grad]
         if not self.params:
             raise ValueError("module has no trainable parameters")
@@ -52,6 +52,14 @@ class FlatParams:
         self.names = {}
         for name, p in module.named_parameters():
             self.names[id(p)] = name
+        # Direct gradient accumulation: backward kernels of single-use parameters
+        # write/accumulate straight into the flat .grad views and then call
+        # mark_ready() (which drives DDP bucketing) instead of going through
+        # autograd's AccumulateGrad add.
+        self.direct = direct
+        self.ready_hooks = []
+        for p in self.params:
+            p._rn_flat = self
         # per-64-element-granule weight-decay flag (matrices decay; vectors don't)
         wd = torch.zeros(off // ALIGN, dtype=torch.uint8)
         for p, o in zip(self.params, self.offsets):
@@ -65,6 +73,10 @@ class FlatParams:
         for p, o in zip(self.params, self.offsets):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:o + 1].data_ptr():
                 p.grad = self.grad[o:o + p.numel()].view(p.shape)
+
+    def mark_ready(self, p):
+        for h in self.ready_hooks:
+            h(p)
 
     def segments(self):
         """[(param, offset, numel)] in layout order."""

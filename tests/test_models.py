@@ -114,3 +114,28 @@ def test_reference_block_train_step_gpu(cuda):
     y = m(torch.randn(2, 64, 256, device="cuda", dtype=torch.bfloat16))
     y.float().pow(2).mean().backward()
     assert all(p.grad is not None and torch.isfinite(p.grad.float()).all() for p in m.parameters())
+
+
+@pytest.mark.gpu
+def test_direct_grad_accumulation_matches_autograd(cuda):
+    """Flat-buffer direct accumulation (kernels write .grad) == plain autograd grads, incl. 2x accumulation."""
+    import copy
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(3)
+    m1 = R.GPT2(R.GPT2Config.tiny(n_embd=256, n_head=4)).cuda()
+    for p in m1.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    m2 = copy.deepcopy(m1)
+    flat = FlatParams(m1)
+    x, y = _lm_batch(m1.config, B=2, T=64, dev="cuda")
+    flat.zero_grad()
+    m1(x, y).backward()
+    g1 = {n: p.grad.detach().float().clone() for n, p in m1.named_parameters()}
+    m1(x, y).backward()  # accumulate a second time
+    m2(x, y).backward()
+    for n, p in m2.named_parameters():
+        ref = p.grad.float()
+        err = ((g1[n] - ref).norm() / (ref.norm() + 1e-6)).item()
+        assert err < 2e-2, (n, err)
+        err2 = ((dict(m1.named_parameters())[n].grad.float() - 2 * ref).norm() / (2 * ref.norm() + 1e-6)).item()
+        assert err2 < 3e-2, (n, err2)
