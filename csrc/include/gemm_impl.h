@@ -109,7 +109,7 @@ RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, in
     tn = in / gsz;
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT, bool PIPE>
 __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     constexpr int NW = WM * WN;
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -142,6 +142,85 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+    if constexpr (PIPE) {
+        // Software-pipelined main loop: 4 MFMA phases per K-tile (k-step s × M-half),
+        // the fragments of phase i+1 are read from LDS while phase i's MFMAs run,
+        // ONE barrier per K-tile (before the last phase) that (a) retires the
+        // LDS-DMA of tile kt+1 issued a whole tile earlier and (b) frees buffer
+        // kt&1 for the DMA of tile kt+2, after which the first fragments of tile
+        // kt+1 are read under the last phase's MFMAs: no LDS-latency bubble at the
+        // tile seam.  sched_barrier pins the load-before-MFMA order per phase.
+        constexpr int HM = FM / 2;
+        static_assert(FM % 2 == 0, "pipelined loop splits the wave's M fragments in two halves");
+        s16x8 A0[HM], A1[HM], B0[FN], B1[FN];
+#define RN_LDA(DST, LA, MH, S)                                                        \
+        _Pragma("unroll") for (int i_ = 0; i_ < HM; ++i_)                          \
+            DST[i_] = frag<AK>(LA, wm * (BM / WM) + ((MH) * HM + i_) * 16, S, lane);
+#define RN_LDB(DST, LB, S)                                                            \
+        _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                          \
+            DST[j_] = frag<BK_>(LB, wn * (BN / WN) + j_ * 16, S, lane);
+#define RN_MMA(A, B, MH)                                                              \
+        _Pragma("unroll") for (int i_ = 0; i_ < HM; ++i_)                          \
+        _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                          \
+            acc[(MH) * HM + i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B[j_], A[i_], acc[(MH) * HM + i_][j_], 0, 0, 0);
+        if (nk > 0) {
+            stage<AK, BM, NW>(a_base(kbeg), p.lda, p.M - m0, kend - kbeg, smem, wave, lane);
+            stage<BK_, BN, NW>(b_base(kbeg), p.ldb, p.N - n0, kend - kbeg, smem + A_BYTES, wave, lane);
+        }
+        __syncthreads();
+        if (nk > 1) {
+            const int k0 = kbeg + BK;
+            stage<AK, BM, NW>(a_base(k0), p.lda, p.M - m0, kend - k0, smem + STAGE, wave, lane);
+            stage<BK_, BN, NW>(b_base(k0), p.ldb, p.N - n0, kend - k0, smem + STAGE + A_BYTES, wave, lane);
+        }
+        if (nk > 0) {
+            RN_LDA(A0, smem, 0, 0)
+            RN_LDB(B0, smem + A_BYTES, 0)
+        }
+        for (int kt = 0; kt < nk; ++kt) {
+            const char* la = smem + (kt & 1) * STAGE;
+            const char* lb = la + A_BYTES;
+            // phase 0: first MFMA row before issuing the next reads, so the wait the
+            // compiler places at the loop head (it cannot count LDS reads across the
+            // back-edge) only covers A0/B0, which landed under the previous phase 3
+            _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)
+                acc[0][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B0[j_], A0[0], acc[0][j_], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            RN_LDA(A1, la, 1, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            _Pragma("unroll") for (int i_ = 1; i_ < HM; ++i_)
+            _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)
+                acc[i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B0[j_], A0[i_], acc[i_][j_], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            RN_LDA(A0, la, 0, 1)
+            RN_LDB(B1, lb, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            RN_MMA(A1, B0, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            RN_LDA(A1, la, 1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            RN_MMA(A0, B1, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();  // all reads of buffer kt&1 retired; tile kt+1 landed (vmcnt(0))
+            if (kt + 2 < nk) {
+                const int k0 = kbeg + (kt + 2) * BK;
+                char* nb = smem + (kt & 1) * STAGE;
+                stage<AK, BM, NW>(a_base(k0), p.lda, p.M - m0, kend - k0, nb, wave, lane);
+                stage<BK_, BN, NW>(b_base(k0), p.ldb, p.N - n0, kend - k0, nb + A_BYTES, wave, lane);
+            }
+            if (kt + 1 < nk) {
+                const char* na = smem + ((kt + 1) & 1) * STAGE;
+                RN_LDA(A0, na, 0, 0)
+                RN_LDB(B0, na + A_BYTES, 0)
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            RN_MMA(A1, B1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#undef RN_LDA
+#undef RN_LDB
+#undef RN_MMA
+    } else {
     if (nk > 0) {
         stage<AK, BM, NW>(a_base(kbeg), p.lda, p.M - m0, kend - kbeg, smem, wave, lane);
         stage<BK_, BN, NW>(b_base(kbeg), p.ldb, p.N - n0, kend - kbeg, smem + A_BYTES, wave, lane);
@@ -170,6 +249,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                 for (int j = 0; j < FN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
+    }
     }
 
     // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) ----
@@ -276,12 +356,12 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT>
+template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT>
 void launch_t(GemmArgs& a, hipStream_t st) {
     constexpr int NT = WM * WN * 64;
     const size_t lds = 2 * (BM + BN) * BK * 2;
-    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false>;
-    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true>;
+    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE>;
+    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE>;
     static bool attr = false;
     if (!attr) {  // >64 KiB of dynamic LDS must be opted into, once per instantiation
         attr = true;
@@ -299,14 +379,14 @@ void launch_t(GemmArgs& a, hipStream_t st) {
     }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool PIPE>
 void launch_cfg(GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
     a.tiles_m = (a.M + BM - 1) / BM;
     a.tiles_n = (a.N + BN - 1) / BN;
 #define RN_L(AKv, BKv)                                                                             \
-    if (act == ACT_GELU) launch_t<BM, BN, WM, WN, AKv, BKv, ACT_GELU>(a, st);                     \
-    else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, AKv, BKv, ACT_RELU>(a, st);                \
-    else launch_t<BM, BN, WM, WN, AKv, BKv, ACT_NONE>(a, st);
+    if (act == ACT_GELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_GELU>(a, st);               \
+    else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_RELU>(a, st);          \
+    else launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_NONE>(a, st);
     if (ak && bk) { RN_L(true, true) }
     else if (ak && !bk) { RN_L(true, false) }
     else if (!ak && bk) { RN_L(false, true) }

@@ -50,6 +50,8 @@ void rn_gemm_launch_cfg0(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg1(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg2(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg3(GemmArgs&, bool, bool, int, hipStream_t);
+void rn_gemm_launch_cfg4(GemmArgs&, bool, bool, int, hipStream_t);
+void rn_gemm_launch_cfg5(GemmArgs&, bool, bool, int, hipStream_t);
 
 namespace {
 
@@ -92,7 +94,8 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 // C[M,N] = act(alpha · op(A)[M,K] · op(B)[K,N] + bias) + res.
 //   trans_a = 0: A stored [M][lda] (K contiguous);   1: A stored [K][lda] (M contiguous)
 //   trans_b = 0: B stored [K][ldb] (N contiguous);   1: B stored [N][ldb] (K contiguous)
-//   cfg: -1 auto, 0 = 128x128, 1 = 256x256, 2 = 256x128, 3 = 128x256;  split: -1 auto, 0/1 none
+//   cfg: -1 auto, 0 = 128x128, 1 = 256x256 pipelined, 2 = 256x128 pipelined, 3 = 128x256,
+//        4 = 256x256 simple, 5 = 128x128 pipelined;  split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
@@ -121,6 +124,8 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
         case 1: rn_gemm_launch_cfg1(a, ak, bk, act, st); break;
         case 2: rn_gemm_launch_cfg2(a, ak, bk, act, st); break;
         case 3: rn_gemm_launch_cfg3(a, ak, bk, act, st); break;
+        case 4: rn_gemm_launch_cfg4(a, ak, bk, act, st); break;
+        case 5: rn_gemm_launch_cfg5(a, ak, bk, act, st); break;
         default: rn_gemm_launch_cfg0(a, ak, bk, act, st); break;
     }
     return 0;

@@ -1,6 +1,6 @@
-// GEMM tile config 1: 256x256 block tile, 2x4 waves (instantiation unit).
+// GEMM tile config 1: 256x256 block tile, 2x4 waves, pipelined main loop.
 #include "gemm_impl.h"
 
 void rn_gemm_launch_cfg1(rn_gemm_detail::GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
-    rn_gemm_detail::launch_cfg<256, 256, 2, 4>(a, ak, bk, act, st);
+    rn_gemm_detail::launch_cfg<256, 256, 2, 4, true>(a, ak, bk, act, st);
 }

@@ -28,6 +28,7 @@ for step in "$@"; do
     bench_eager) run bench_eager 600 python bench.py --steps 10 --warmup 3 --graph off ;;
     tprof) run tprof 600 python bench.py --steps 3 --warmup 2 --profile-steps 2 ;;
     microbench) run microbench 600 python scripts/microbench.py ;;
+    mbgemm) run mbgemm 600 python scripts/microbench.py gemm ;;
     stock) run stock 600 python scripts/bench_stock_torch.py --steps 10 --warmup 3 ;;
     *) run custom 600 bash -c "$step" ;;
   esac
