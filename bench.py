@@ -26,6 +26,12 @@ import torch
 import torch.distributed as dist
 
 METRIC = "train-step samples/sec (whole node), GPT-2-small DDP at 1/2/4/8 MI355X"
+OTHER_METRICS = {  # secondary BASELINE.json configs (same harness)
+    "gpt2-medium": "train-step samples/sec (whole node), GPT-2-medium bf16",
+    "gpt2-medium-fp8": "train-step samples/sec (whole node), GPT-2-medium fp8 forward GEMMs",
+    "vit-b16": "train-step images/sec (whole node), ViT-B/16 bf16 DDP",
+    "resnet18": "train-step images/sec (whole node), ResNet-18 bf16",
+}
 BASELINE_VALUE = None  # the reference publishes no number
 
 
@@ -35,7 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-small")
-    ap.add_argument("--batch", type=int, default=16, help="per-GPU micro-batch (sequences)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU micro-batch (default 16 seqs / 128 images)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra torch.profiler steps (not timed)")
@@ -52,7 +58,12 @@ def main():
     if torch.cuda.is_available() and not _ext.available():
         raise RuntimeError(f"native extension missing: {_ext.load_error()}")
 
+    is_lm = args.model.startswith("gpt2")
+    if args.batch is None:
+        args.batch = 16 if is_lm else (128 if args.model.startswith("vit") else 256)
     cfg = TrainConfig(model=args.model, batch_size=args.batch, seq_len=args.seq, steps=10**9,
+                      optimizer="adamw" if not args.model.startswith("resnet") else "sgd",
+                      weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,
                       warmup_steps=10, lr=6e-4, bucket_mb=args.bucket_mb, log_every=10**9,
                       graph=args.graph)
     tr = Trainer(cfg)
@@ -99,9 +110,9 @@ def main():
     samples = cfg.batch_size * world * args.steps
     value = samples / elapsed
     out = {
-        "metric": METRIC,
+        "metric": METRIC if args.model == "gpt2-small" else OTHER_METRICS.get(args.model, args.model),
         "value": round(value, 3),
-        "unit": "samples/s",
+        "unit": "samples/s" if is_lm else "images/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -115,10 +126,11 @@ def main():
             "model": args.model,
             "global_batch": cfg.batch_size * world,
             "micro_batch_per_gpu": cfg.batch_size,
-            "seq_len": args.seq,
+            "seq_len": args.seq if is_lm else None,
             "parallelism": f"dp{world}",
-            "tokens_per_s": round(value * args.seq, 1),
-            "optimizer": "fused AdamW (fp32 master) + grad-norm clip",
+            "tokens_per_s": round(value * args.seq, 1) if is_lm else None,
+            "optimizer": ("fused AdamW" if cfg.optimizer == "adamw" else "fused SGD-momentum")
+            + " (fp32 master) + grad-norm clip",
             "hipgraph": tr._graph is not None,
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         },

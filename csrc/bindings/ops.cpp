@@ -61,6 +61,10 @@ void rn_maxpool_bwd(const void*, const void*, const void*, void*, int, int, int,
                     hipStream_t);
 void rn_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
 void rn_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
+void rn_fp8_quantize(const void*, long, void*, float*, hipStream_t);
+void rn_fp8_dequantize(const void*, long, const float*, void*, hipStream_t);
+int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
+                int, int, int, long, long, long, int, hipStream_t);
 long rn_bn_ws_floats(int, int);
 void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, float*, float*, float*, int, int, float,
                float, int, hipStream_t);
@@ -468,6 +472,37 @@ std::tuple<Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor&
     return {dx, dw, db};
 }
 
+// ------------------------------------------------------------------ fp8
+std::tuple<Tensor, Tensor> fp8_quantize(const Tensor& x) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    Tensor q = at::empty(x.sizes(), x.options().dtype(at::kByte));
+    Tensor state = at::empty({4}, x.options().dtype(at::kFloat));
+    rn_fp8_quantize(x.data_ptr(), x.numel(), q.data_ptr(), state.data_ptr<float>(), cur_stream());
+    return {q, state};
+}
+Tensor fp8_dequantize(const Tensor& q, const Tensor& state) {
+    GUARD(q);
+    Tensor y = at::empty(q.sizes(), q.options().dtype(at::kBFloat16));
+    rn_fp8_dequantize(q.data_ptr(), q.numel(), state.data_ptr<float>(), y.data_ptr(), cur_stream());
+    return y;
+}
+Tensor gemm_fp8(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb, const optional<Tensor>& bias,
+                const optional<Tensor>& residual, int64_t act, const optional<Tensor>& preact) {
+    GUARD(a8);
+    TORCH_CHECK(a8.scalar_type() == at::kByte && b8.scalar_type() == at::kByte, "fp8 operands are uint8 storage");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.size(1) == b8.size(1) && a8.is_contiguous() && b8.is_contiguous());
+    const int M = a8.size(0), N = b8.size(0), K = a8.size(1);
+    Tensor c = at::empty({M, N}, a8.options().dtype(at::kBFloat16));
+    Tensor alpha = at::empty({1}, a8.options().dtype(at::kFloat));
+    if (residual && residual->defined()) { CHECK_BF16(*residual); TORCH_CHECK(residual->is_contiguous()); }
+    int rc = rn_gemm_fp8(a8.data_ptr(), b8.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
+                         preact && preact->defined() ? preact->data_ptr() : nullptr, sa.data_ptr<float>(),
+                         sb.data_ptr<float>(), alpha.data_ptr<float>(), M, N, K, a8.stride(0), b8.stride(0), c.stride(0),
+                         (int)act, cur_stream());
+    TORCH_CHECK(rc == 0, "gemm_fp8: K and row strides must be multiples of 16, got K=", K);
+    return c;
+}
+
 int64_t native_version() { return 1; }
 
 }  // namespace
@@ -511,6 +546,9 @@ TORCH_LIBRARY(replicann, m) {
           "-> (Tensor, Tensor, Tensor)");
     m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu) -> Tensor");
     m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu) -> (Tensor, Tensor, Tensor)");
+    m.def("fp8_quantize(Tensor x) -> (Tensor, Tensor)");
+    m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
+    m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("native_version() -> int");
 }
 
@@ -545,6 +583,9 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("batchnorm_fwd", &batchnorm_fwd);
     m.impl("batchnorm_eval", &batchnorm_eval);
     m.impl("batchnorm_bwd", &batchnorm_bwd);
+    m.impl("fp8_quantize", &fp8_quantize);
+    m.impl("fp8_dequantize", &fp8_dequantize);
+    m.impl("gemm_fp8", &gemm_fp8);
 }
 
 TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {

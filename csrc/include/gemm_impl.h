@@ -27,7 +27,7 @@ struct GemmArgs {
 };
 
 RN_DEV int swz_kc(int r) { return (r >> 1) & 7; }
-RN_DEV int swz_mn(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+RN_DEV int swz_mn(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }
 
 RN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
     // readfirstlane keeps the descriptor provably wave-uniform (no waterfall loops, guide T20)
@@ -38,8 +38,15 @@ RN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
 }
 
 // Stage one ROWS(mn)×64(k) operand tile into LDS with NW waves.
-//   KC:  global element (mn, k) at base[mn*ld + k]; image [ROWS][64] (128-B rows)
-//   !KC: global element (mn, k) at base[k*ld + mn]; image = ROWS/128 sub-images [64 k][128 mn]
+//   KC:  global element (mn, k) at base[mn*ld + k]; image [ROWS][64 k] (128-B rows),
+//        16-B chunk c of row r at c ^ swz_kc(r), read with ds_read_b128.
+//   !KC: global element (mn, k) at base[k*ld + mn]; image = ROWS/64 sub-images
+//        [64 k][64 mn] (128-B rows), chunk c of k-row r at c ^ swz_mn(r), read with
+//        ds_read_b64_tr_b16.  swz_mn maps the 8 k-rows one 32-lane half reads
+//        ({0..3, 8..11} + const) to 8 distinct (row parity, chunk pair) slots of the
+//        256-B bank row: conflict-free.  Any multiple of 64 columns works (192 too).
+// The XOR is applied to the per-lane GLOBAL source address (the DMA destination
+// is lane-linear, guide rule 21) and again on the read address.
 template <bool KC, int ROWS, int NW>
 RN_DEV void stage(const bf16* base, long ld, int mn_lim, int k_lim, char* lds, int wave, int lane) {
     __amdgpu_buffer_rsrc_t rsrc = make_rsrc(base);
@@ -57,10 +64,10 @@ RN_DEV void stage(const bf16* base, long ld, int mn_lim, int k_lim, char* lds, i
             const bool ok = (r < mn_lim) && (k < k_lim);
             voff = ok ? (uint32_t)(((long)r * ld + k) * 2) : 0xFFFFFFF0u;
         } else {
-            const int sub = ins >> 4, within = ins & 15;
-            const int r = within * 4 + (lane >> 4);
-            const int cg = (lane & 15) ^ swz_mn(r);
-            const int mn = sub * 128 + cg * 8;
+            const int sub = ins >> 3, within = ins & 7;
+            const int r = within * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz_mn(r);
+            const int mn = sub * 64 + cg * 8;
             const bool ok = (r < k_lim) && (mn < mn_lim);
             voff = ok ? (uint32_t)(((long)r * ld + mn) * 2) : 0xFFFFFFF0u;
         }
@@ -77,14 +84,14 @@ RN_DEV s16x8 frag(const char* lds, int mnbase, int s, int lane) {
         const int chunk = s * 4 + (lane >> 4);
         return *reinterpret_cast<const s16x8*>(lds + row * 128 + ((chunk ^ swz_kc(row)) << 4));
     } else {
-        const char* sub = lds + (mnbase >> 7) * 16384;
-        const int mnl = mnbase & 127;
+        const char* sub = lds + (mnbase >> 6) * 8192;
+        const int mnl = mnbase & 63;
         const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
         const int c = (mnl >> 3) + (p >> 1);
         const int k0 = s * 32 + 8 * g + q;
         const int k1 = k0 + 4;
-        const char* a0 = sub + k0 * 256 + ((c ^ swz_mn(k0)) << 4) + (p & 1) * 8;
-        const char* a1 = sub + k1 * 256 + ((c ^ swz_mn(k1)) << 4) + (p & 1) * 8;
+        const char* a0 = sub + k0 * 128 + ((c ^ swz_mn(k0)) << 4) + (p & 1) * 8;
+        const char* a1 = sub + k1 * 128 + ((c ^ swz_mn(k1)) << 4) + (p & 1) * 8;
         s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
         s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
         s16x8 r;
@@ -109,7 +116,21 @@ RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, in
     tn = in / gsz;
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT, bool PIPE>
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// fp8 fragment for v_mfma_scale_f32_16x16x128_f8f6f4: 32 consecutive e4m3 bytes
+// (k = 32*(lane>>4) + 0..31) of row mnbase + (lane&15) = 16-B chunks 2g, 2g+1 of
+// the same K-contiguous 128-B-row LDS image the bf16 path uses.
+RN_DEV i32x8 frag8(const char* lds, int mnbase, int lane) {
+    const int row = mnbase + (lane & 15), g = lane >> 4;
+    const char* rp = lds + row * 128;
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(rp + (((2 * g) ^ swz_kc(row)) << 4));
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(rp + (((2 * g + 1) ^ swz_kc(row)) << 4));
+    return (i32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT, bool PIPE, bool FP8 = false>
 __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     constexpr int NW = WM * WN;
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -236,6 +257,22 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
         }
         const char* la = smem + cur * STAGE;
         const char* lb = la + A_BYTES;
+        if constexpr (FP8) {
+            // one 16x16x128 block-scaled MFMA per fragment pair per 128-deep fp8 K-tile
+            // (unit E8M0 block scales; the per-tensor scales enter through alpha)
+            i32x8 af[FM], bfr[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) bfr[j] = frag8(lb, wn * (BN / WN) + j * 16, lane);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) af[i] = frag8(la, wm * (BM / WM) + i * 16, lane);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0,
+                                                                                 127, 0, 127);
+            continue;
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             s16x8 af[FM], bfr[FN];
@@ -252,8 +289,81 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     }
     }
 
-    // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) ----
     const float alpha = p.alpha ? *p.alpha : 1.f;
+
+    // ---- LDS-staged epilogue (bf16 output, N % 8 == 0) ----
+    // The accumulator layout gives each lane 4 consecutive columns of ONE row, so
+    // direct stores write 16 rows × 32 B per wave-instruction.  Instead the tile is
+    // staged through LDS (row stride BN*2+16 B: 2-way at worst on the b64 writes)
+    // and written back as whole rows, 16 B per lane, with residual / accumulate
+    // read the same coalesced way.  For short-K GEMMs (K = 768) the store tail is
+    // otherwise as long as the main loop.
+    if constexpr (!SPLIT) {
+        if (!p.out_f32 && (p.N % 8) == 0 && (p.ldc % 8) == 0) {
+            constexpr int STRIDE = BN * 2 + 16;
+            constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+            const int mlim = min(BM, p.M - m0), nlim = min(BN, p.N - n0);
+            for (int pass = (ACT != ACT_NONE && p.pre) ? 0 : 1; pass < 2; ++pass) {
+                __syncthreads();  // main-loop LDS reads (or the previous pass's reads) retired
+#pragma unroll
+                for (int i = 0; i < FM; ++i) {
+                    const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+                        float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha,
+                                      acc[i][j][3] * alpha};
+                        if (p.bias && n0 + nl < p.N) {
+                            bf16x4 b = *reinterpret_cast<const bf16x4*>(p.bias + n0 + nl);
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) v[t] += (float)b[t];
+                        }
+                        if constexpr (ACT != ACT_NONE) {
+                            if (pass == 1) {
+#pragma unroll
+                                for (int t = 0; t < 4; ++t) v[t] = act_f<ACT>(v[t]);
+                            }
+                        }
+                        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+                        *reinterpret_cast<bf16x4*>(smem + ml * STRIDE + nl * 2) = o;
+                    }
+                }
+                __syncthreads();
+                bf16* dst = pass == 0 ? p.pre : (bf16*)p.C;
+                const bool addres = pass == 1 && p.res;
+                const bool accum = pass == 1 && p.accumulate;
+                for (int q = threadIdx.x; q < BM * CPR; q += NW * 64) {
+                    const int r = q / CPR, cc = q % CPR;
+                    if (r >= mlim || cc * 8 >= nlim) continue;
+                    s16x8 v = *reinterpret_cast<const s16x8*>(smem + r * STRIDE + cc * 16);
+                    const long goff = (long)(m0 + r) * p.ldc + n0 + cc * 8;
+                    if (addres || accum) {
+                        float f[8];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) f[t] = (float)__builtin_bit_cast(bf16, (short)v[t]);
+                        if (addres) {
+                            float rr[8];
+                            load8(p.res + goff, rr);
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) f[t] += rr[t];
+                        }
+                        if (accum) {
+                            float cc8[8];
+                            load8(dst + goff, cc8);
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) f[t] += cc8[t];
+                        }
+                        store8(dst + goff, f);
+                    } else {
+                        *reinterpret_cast<s16x8*>(dst + goff) = v;
+                    }
+                }
+            }
+            return;
+        }
+    }
+
+    // ---- direct epilogue: lane owns C[m][n..n+3] for each (i, j) ----
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
         const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
@@ -359,7 +469,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
 template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT>
 void launch_t(GemmArgs& a, hipStream_t st) {
     constexpr int NT = WM * WN * 64;
-    const size_t lds = 2 * (BM + BN) * BK * 2;
+    const size_t lds = std::max<size_t>(2 * (BM + BN) * BK * 2, (size_t)BM * (BN * 2 + 16));
     auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE>;
     auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE>;
     static bool attr = false;
@@ -392,6 +502,23 @@ void launch_cfg(GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
     else if (!ak && bk) { RN_L(false, true) }
     else { RN_L(false, false) }
 #undef RN_L
+}
+
+// fp8 e4m3 NT GEMM (both operands K-contiguous): staged as "bf16 pairs", so the
+// caller passes K, lda, ldb in units of 2 bytes.
+template <int BM, int BN, int WM, int WN, int ACT>
+void launch_fp8_t(GemmArgs& a, hipStream_t st) {
+    constexpr int NT = WM * WN * 64;
+    const size_t lds = std::max<size_t>(2 * (BM + BN) * BK * 2, (size_t)BM * (BN * 2 + 16));
+    auto kmain = gemm_k<BM, BN, WM, WN, true, true, ACT, false, false, true>;
+    static bool attr = false;
+    if (!attr) {
+        attr = true;
+        (void)hipFuncSetAttribute((const void*)kmain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    a.tiles_m = (a.M + BM - 1) / BM;
+    a.tiles_n = (a.N + BN - 1) / BN;
+    kmain<<<a.tiles_m * a.tiles_n, NT, lds, st>>>(a);
 }
 
 }  // namespace rn_gemm_detail

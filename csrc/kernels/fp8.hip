@@ -1,0 +1,107 @@
+// FP8 (OCP e4m3fn — gfx950's format, not the MI300 fnuz variant) support — N3.
+//
+// * amax / quantise kernels with per-tensor "current" scaling: scale = amax/448,
+//   the quantised tensor q satisfies x ≈ q · scale; amax is reduced on device
+//   (block max → one atomicMax per block on the float bits, non-negative so
+//   integer order == float order); the quantise kernel derives the scale from
+//   the device amax itself, so the whole sequence is graph-capturable.
+// * the GEMM runs on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales:
+//   2x the bf16 MFMA rate per clock (MI355X_MICROARCH.md §Matrix cores), with the
+//   product of the two tensor scales applied as the epilogue alpha.
+#include "gemm_impl.h"
+
+namespace {
+
+constexpr float E4M3_MAX = 448.f;
+
+__global__ void __launch_bounds__(256) amax_k(const bf16* __restrict__ x, long n, float* __restrict__ state) {
+    __shared__ float sm[16];
+    float m = 0.f;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[j]));
+    }
+    for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        m = fmaxf(m, fabsf(bf2f(x[i])));
+    m = block_max(m, sm);
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
+}
+
+// state: [scale, amax, ...]; writes scale = amax/448 (1 if amax == 0) and q = x/scale as e4m3
+__global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
+                                               float* __restrict__ state) {
+    const float amax = state[1];
+    const float scale = amax > 0.f ? amax / E4M3_MAX : 1.f;
+    const float inv = 1.f / scale;
+    if (blockIdx.x == 0 && threadIdx.x == 0) state[0] = scale;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(x + i * 8, f);
+        int w0 = 0, w1 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(f[j] * inv, -E4M3_MAX), E4M3_MAX);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+        *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    }
+    for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float f = fminf(fmaxf(bf2f(x[i]) * inv, -E4M3_MAX), E4M3_MAX);
+        q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(f, 0.f, 0, false) & 0xFF);
+    }
+}
+
+__global__ void dequant_k(const uint8_t* __restrict__ q, long n, const float* __restrict__ state,
+                          bf16* __restrict__ y) {
+    const float scale = state[0];
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        y[i] = (bf16)(__builtin_amdgcn_cvt_f32_fp8((int)q[i], 0) * scale);
+}
+
+// alpha = sa * sb on device
+__global__ void scale_mul_k(const float* __restrict__ sa, const float* __restrict__ sb, float* __restrict__ alpha) {
+    alpha[0] = sa[0] * sb[0];
+}
+
+inline int gridn(long n) {
+    long g = (n + 255) / 256;
+    return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
+
+}  // namespace
+
+extern "C" {
+
+// state must hold >= 2 floats; it is (re)initialised here (memset node + 2 kernels).
+void rn_fp8_quantize(const void* x, long n, void* q, float* state, hipStream_t st) {
+    (void)hipMemsetAsync(state, 0, 2 * sizeof(float), st);
+    amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
+    quant_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
+}
+
+void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
+    dequant_k<<<gridn(n), 256, 0, st>>>((const uint8_t*)q, n, state, (bf16*)y);
+}
+
+// C[M,N] (bf16) = act(sa·sb · A8[M,K] · B8[N,K]ᵀ + bias) + res ; K % 16 == 0, lda/ldb in bytes % 16 == 0
+int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const void* res, void* pre,
+                const float* sa, const float* sb, float* alpha_ws, int M, int N, int K, long lda, long ldb, long ldc,
+                int act, hipStream_t st) {
+    if (K % 16 || lda % 16 || ldb % 16) return -1;
+    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
+    rn_gemm_detail::GemmArgs a;
+    a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
+    a.pre = (bf16*)pre; a.ws = nullptr; a.alpha = alpha_ws;
+    a.M = M; a.N = N; a.K = K / 2; a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
+    a.split = 1; a.k_per_split = ((K / 2) + 63) / 64 * 64; a.out_f32 = 0; a.accumulate = 0;
+    using namespace rn_gemm_detail;
+    if (act == ACT_GELU) launch_fp8_t<256, 192, 2, 4, ACT_GELU>(a, st);
+    else if (act == ACT_RELU) launch_fp8_t<256, 192, 2, 4, ACT_RELU>(a, st);
+    else launch_fp8_t<256, 192, 2, 4, ACT_NONE>(a, st);
+    return 0;
+}
+
+}  // extern "C"

@@ -52,6 +52,7 @@ void rn_gemm_launch_cfg2(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg3(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg4(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg5(GemmArgs&, bool, bool, int, hipStream_t);
+void rn_gemm_launch_cfg6(GemmArgs&, bool, bool, int, hipStream_t);
 
 namespace {
 
@@ -65,21 +66,25 @@ struct Choice { int cfg, split; };
 
 inline Choice pick(int M, int N, int K, int split_req) {
     const double flop_s_cu = 2.9e12;  // effective per-CU bf16 rate of the 128² config
-    const double cand_rate[4] = {1.0, 1.13, 1.0, 1.0};
-    const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, slots[4] = {512, 256, 256, 256};
+    // candidates: cfg id, BM, BN, resident blocks (slots), relative per-CU rate
+    const int cid[4] = {0, 1, 6, 2};
+    const int bm[4] = {128, 256, 256, 256}, bn[4] = {128, 256, 192, 128}, slots[4] = {512, 256, 256, 256};
+    const double rate[4] = {1.0, 1.16, 1.0, 0.9};
     Choice best = {0, 1};
     double best_t = 1e30;
     for (int c = 0; c < 4; ++c) {
         for (int sp = 1; sp <= 32; sp *= 2) {
             if (split_req > 0 && sp != split_req) continue;
             if (split_req <= 0 && sp > 1 && K / sp < 512) break;
+            // split-K only when the unsplit grid cannot fill the resident slots
+            if (split_req <= 0 && sp > 1 && ntiles(M, N, bm[c], bn[c]) >= slots[c]) break;
             const int kps = ((K + sp - 1) / sp + 63) / 64 * 64;
             const long tiles = ntiles(M, N, bm[c], bn[c]) * sp;
             const long rounds = (tiles + slots[c] - 1) / slots[c];
-            const double per_block = 2.0 * bm[c] * bn[c] * kps / (flop_s_cu * cand_rate[c]) * (c == 0 ? 2.0 : 1.0);
-            double t = rounds * per_block;
+            const double per_block = 2.0 * bm[c] * bn[c] * kps / (flop_s_cu * rate[c]) * (c == 0 ? 2.0 : 1.0);
+            double t = rounds * per_block + 2.5e-6;  // + prologue/epilogue per launch
             if (sp > 1) t += ((double)M * N * (4.0 * sp + 2.0)) / 4.0e12 + 3e-6;
-            if (t < best_t * 0.98) { best_t = t; best = {c, sp}; }
+            if (t < best_t * 0.98) { best_t = t; best = {cid[c], sp}; }
         }
     }
     return best;
@@ -95,7 +100,7 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 //   trans_a = 0: A stored [M][lda] (K contiguous);   1: A stored [K][lda] (M contiguous)
 //   trans_b = 0: B stored [K][ldb] (N contiguous);   1: B stored [N][ldb] (K contiguous)
 //   cfg: -1 auto, 0 = 128x128, 1 = 256x256 pipelined, 2 = 256x128 pipelined, 3 = 128x256,
-//        4 = 256x256 simple, 5 = 128x128 pipelined;  split: -1 auto, 0/1 none
+//        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined;  split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
@@ -126,6 +131,7 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
         case 3: rn_gemm_launch_cfg3(a, ak, bk, act, st); break;
         case 4: rn_gemm_launch_cfg4(a, ak, bk, act, st); break;
         case 5: rn_gemm_launch_cfg5(a, ak, bk, act, st); break;
+        case 6: rn_gemm_launch_cfg6(a, ak, bk, act, st); break;
         default: rn_gemm_launch_cfg0(a, ak, bk, act, st); break;
     }
     return 0;

@@ -26,16 +26,21 @@ from .. import ops
 
 
 class Linear(nn.Module):
-    """nn.Linear-compatible parameters (weight (out, in), bias (out,)) on the MFMA GEMM."""
+    """nn.Linear-compatible parameters (weight (out, in), bias (out,)) on the MFMA GEMM.
 
-    def __init__(self, in_features, out_features, bias=True, std=0.02):
+    ``fp8=True`` runs the forward GEMM in fp8 e4m3 (ops.linear_fp8)."""
+
+    def __init__(self, in_features, out_features, bias=True, std=0.02, fp8=False):
         super().__init__()
         self.in_features, self.out_features = in_features, out_features
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
         self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
+        self.fp8 = fp8
         nn.init.normal_(self.weight, std=std)
 
     def forward(self, x, act=None, residual=None):
+        if self.fp8:
+            return ops.linear_fp8(x, self.weight, self.bias, act=act, residual=residual)
         return ops.linear(x, self.weight, self.bias, act=act, residual=residual)
 
 
@@ -51,11 +56,11 @@ class LayerNorm(nn.Module):
 
 
 class Attention(nn.Module):
-    def __init__(self, n_embd, n_head, causal, attn_dropout=0.0, resid_dropout=0.0, n_layer=12):
+    def __init__(self, n_embd, n_head, causal, attn_dropout=0.0, resid_dropout=0.0, n_layer=12, fp8=False):
         super().__init__()
         self.n_head, self.causal = n_head, causal
-        self.c_attn = Linear(n_embd, 3 * n_embd)
-        self.c_proj = Linear(n_embd, n_embd, std=0.02 / math.sqrt(2 * n_layer))
+        self.c_attn = Linear(n_embd, 3 * n_embd, fp8=fp8)
+        self.c_proj = Linear(n_embd, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
         self.attn_dropout, self.resid_dropout = attn_dropout, resid_dropout
 
     def forward(self, h, residual):
@@ -70,10 +75,10 @@ class Attention(nn.Module):
 
 
 class MLP(nn.Module):
-    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12):
+    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12, fp8=False):
         super().__init__()
-        self.c_fc = Linear(n_embd, hidden)
-        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer))
+        self.c_fc = Linear(n_embd, hidden, fp8=fp8)
+        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
         self.dropout = dropout
 
     def forward(self, h, residual):
@@ -84,12 +89,12 @@ class MLP(nn.Module):
 
 
 class PreLNBlock(nn.Module):
-    def __init__(self, n_embd, n_head, causal, mlp_ratio=4, dropout=0.0, n_layer=12, eps=1e-5):
+    def __init__(self, n_embd, n_head, causal, mlp_ratio=4, dropout=0.0, n_layer=12, eps=1e-5, fp8=False):
         super().__init__()
         self.ln_1 = LayerNorm(n_embd, eps)
-        self.attn = Attention(n_embd, n_head, causal, dropout, dropout, n_layer)
+        self.attn = Attention(n_embd, n_head, causal, dropout, dropout, n_layer, fp8=fp8)
         self.ln_2 = LayerNorm(n_embd, eps)
-        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer)
+        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer, fp8=fp8)
 
     def forward(self, x):
         x = self.attn(self.ln_1(x), residual=x)

@@ -35,6 +35,7 @@ class GPT2Config:
     vocab_pad: int = 50304
     dropout: float = 0.0
     ln_eps: float = 1e-5
+    fp8: bool = False  # fp8 e4m3 forward GEMMs in the transformer blocks ("fp8 weights" config)
 
     @staticmethod
     def small(**kw):
@@ -66,7 +67,7 @@ class GPT2(nn.Module):
         self.wte._rn_shared = True  # tied: embedding + LM head both contribute gradients
         self.h = nn.ModuleList(
             PreLNBlock(cfg.n_embd, cfg.n_head, causal=True, dropout=cfg.dropout, n_layer=cfg.n_layer,
-                       eps=cfg.ln_eps)
+                       eps=cfg.ln_eps, fp8=cfg.fp8)
             for _ in range(cfg.n_layer)
         )
         self.ln_f = LayerNorm(cfg.n_embd, cfg.ln_eps)

@@ -30,7 +30,7 @@ from .utils.flat import FlatParams
 from .utils.metrics import MetricsLogger, is_rank0, phase
 
 MODEL_KINDS = {
-    "gpt2-small": "lm", "gpt2-medium": "lm", "gpt2-tiny": "lm",
+    "gpt2-small": "lm", "gpt2-medium": "lm", "gpt2-medium-fp8": "lm", "gpt2-tiny": "lm",
     "vit-b16": "image", "vit-tiny": "image",
     "resnet18": "image", "resnet18-tiny": "image",
     "mlp": "mnist",
@@ -42,6 +42,8 @@ def build_model(name, **kw):
         return models.GPT2(models.GPT2Config.small(**kw))
     if name == "gpt2-medium":
         return models.GPT2(models.GPT2Config.medium(**kw))
+    if name == "gpt2-medium-fp8":
+        return models.GPT2(models.GPT2Config.medium(fp8=True, **kw))
     if name == "gpt2-tiny":
         return models.GPT2(models.GPT2Config.tiny(**kw))
     if name == "vit-b16":

@@ -24,6 +24,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     bench_small) run bench_small 600 python bench.py --steps 5 --warmup 2 --batch 4 ;;
+    bench_configs) run bench_med 600 python bench.py --model gpt2-medium --steps 5 --warmup 2 && run bench_med_fp8 600 python bench.py --model gpt2-medium-fp8 --steps 5 --warmup 2 && run bench_vit 600 python bench.py --model vit-b16 --steps 5 --warmup 2 && run bench_resnet 600 python bench.py --model resnet18 --steps 5 --warmup 2 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 2 ;;
     bench_eager) run bench_eager 600 python bench.py --steps 10 --warmup 3 --graph off ;;
     tprof) run tprof 600 python bench.py --steps 3 --warmup 2 --profile-steps 2 ;;

@@ -55,7 +55,7 @@ def main():
         fl = 2 * m * n * k
         t_r = min(timeit(ref) for _ in range(3))
         cfg_t = {}
-        for cfg in (-1, 0, 1, 2, 3, 4, 5):
+        for cfg in (-1, 0, 1, 2, 5, 6):
             for s_ in sorted({-1, 1, 2, 4}) if ta else [0]:
                 ours = lambda: ops.gemm(a, b, ta=ta, tb=tb, split_k=s_, cfg=cfg)
                 err = ((ours().float() - ref().float()).norm() / ref().float().norm()).item()

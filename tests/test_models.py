@@ -139,3 +139,13 @@ def test_direct_grad_accumulation_matches_autograd(cuda):
         assert err < 2e-2, (n, err)
         err2 = ((dict(m1.named_parameters())[n].grad.float() - 2 * ref).norm() / (2 * ref.norm() + 1e-6)).item()
         assert err2 < 3e-2, (n, err2)
+
+
+@pytest.mark.gpu
+def test_gpt2_fp8_train_steps(cuda):
+    torch.manual_seed(4)
+    cfg = TrainConfig(model="gpt2-tiny", batch_size=4, seq_len=128, steps=6, lr=1e-3, warmup_steps=1,
+                      log_every=1000, model_kwargs={"fp8": True, "n_embd": 256, "n_head": 4})
+    tr = Trainer(cfg)
+    losses = [float(tr.step()) for _ in range(6)]
+    assert all(torch.isfinite(torch.tensor(losses))) and losses[-1] < losses[0]

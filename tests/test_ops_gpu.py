@@ -26,7 +26,7 @@ def test_native_loaded(cuda):
 
 
 # ----------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 96), (1000, 384, 520), (64, 24, 8), (520, 776, 1088)])
 def test_gemm_layouts(cuda, ta, tb, M, N, K, cfg):
@@ -323,3 +323,41 @@ def test_pools(cuda):
     a.sum().backward()
     assert rel_err(a, x2.detach().float().mean((1, 2))) < 1e-2
     assert torch.allclose(x2.grad.float(), torch.full_like(x2.grad.float(), 1 / 49), rtol=1e-2)
+
+
+# ----------------------------------------------------------------- fp8
+def test_fp8_quantize_roundtrip(cuda):
+    torch.manual_seed(20)
+    x = bf(300, 264, scale=3.0)
+    q, st = ops.quantize_fp8(x)
+    assert q.dtype == torch.uint8 and abs(st[0].item() - x.float().abs().max().item() / 448) < 1e-3
+    y = ops.dequantize_fp8(q, st)
+    assert rel_err(y, x) < 0.05
+    # bit-compatible with torch's OCP e4m3fn
+    ref = (x.float() / st[0]).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert (q == ref).float().mean().item() > 0.99
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (300, 200, 528), (1024, 768, 1024)])
+def test_gemm_fp8_matches_dequantized_reference(cuda, M, N, K):
+    torch.manual_seed(21)
+    a, b = bf(M, K), bf(N, K, scale=0.2)
+    qa, sa = ops.quantize_fp8(a)
+    qb, sb = ops.quantize_fp8(b)
+    out = torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, None, None, 0, None)
+    ref = ops.dequantize_fp8(qa, sa).float() @ ops.dequantize_fp8(qb, sb).float().t()
+    assert rel_err(out, ref) < 1e-2  # exact products; only accumulation order + bf16 output differ
+    assert rel_err(out, a.float() @ b.float().t()) < 0.08  # vs the unquantised product
+
+
+def test_linear_fp8_autograd(cuda):
+    torch.manual_seed(22)
+    x = bf(4, 64, 256).requires_grad_()
+    w = bf(512, 256, scale=0.05).requires_grad_()
+    b = bf(512).requires_grad_()
+    r = bf(4, 64, 512)
+    y = ops.linear_fp8(x, w, b, act="gelu", residual=r)
+    yref = ops.linear(x.detach(), w.detach(), b.detach(), act="gelu", residual=r)
+    assert rel_err(y, yref) < 0.05
+    y.float().pow(2).mean().backward()
+    assert all(torch.isfinite(t.grad.float()).all() for t in (x, w, b))
