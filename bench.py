@@ -136,6 +136,10 @@ def main():
         },
     }
     if tr.rank == 0:
+        if dev.type == "cuda":  # the measured per-shape GEMM configs (runtime autotuner)
+            os.makedirs("gpurun_out", exist_ok=True)
+            with open(f"gpurun_out/gemm_tuning_{args.model}.json", "w") as f:
+                f.write(torch.ops.replicann.gemm_tuning_table())
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -12,7 +12,12 @@
 #include <torch/library.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <optional>
+#include <sstream>
 #include <tuple>
 #include <vector>
 
@@ -86,6 +91,46 @@ inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradi
 const void* optr(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_ptr() : nullptr; }
 
 // ------------------------------------------------------------------ GEMM
+// Measured tile-config / split-K selection.  The first eager call of every GEMM
+// shape times the candidate configs on the current stream (into a scratch output;
+// the real call then runs once with the winner) and caches the choice.  Calls made
+// while the stream is being captured into a hipGraph never tune: they use the
+// cache, or the native cost model.  REPLICANN_GEMM_AUTOTUNE=0 disables tuning.
+struct TuneKey {
+    int64_t M, N, K;
+    int ta, tb, act, f32, autosplit;
+    bool operator<(const TuneKey& o) const {
+        return std::tie(M, N, K, ta, tb, act, f32, autosplit) < std::tie(o.M, o.N, o.K, o.ta, o.tb, o.act, o.f32, o.autosplit);
+    }
+};
+static std::map<TuneKey, std::pair<int, int>> g_tune;
+static std::mutex g_tune_mu;
+
+static bool autotune_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("REPLICANN_GEMM_AUTOTUNE");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
+std::string gemm_tuning_table() {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    std::ostringstream os;
+    os << "[";
+    bool first = true;
+    for (auto& kv : g_tune) {
+        const TuneKey& k = kv.first;
+        os << (first ? "" : ",") << "{\"M\":" << k.M << ",\"N\":" << k.N << ",\"K\":" << k.K << ",\"ta\":" << k.ta
+           << ",\"tb\":" << k.tb << ",\"act\":" << k.act << ",\"cfg\":" << kv.second.first << ",\"split\":"
+           << kv.second.second << "}";
+        first = false;
+    }
+    os << "]";
+    return os.str();
+}
+
 Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<Tensor>& bias,
             const optional<Tensor>& residual, int64_t act, const optional<Tensor>& preact, const optional<Tensor>& out,
             bool accumulate, int64_t split_k, bool out_fp32, const optional<Tensor>& alpha, int64_t cfg) {
@@ -142,8 +187,65 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     if (tb && B.stride(0) % 8 != 0) B = B.contiguous();
     if (c.stride(0) % 4 != 0 && (bias || residual)) { /* epilogue handles unaligned via scalar path */ }
     if (alpha && alpha->defined()) TORCH_CHECK(alpha->scalar_type() == at::kFloat && alpha->is_cuda());
+    if (cfg < 0 && split_k <= 0) {
+        const TuneKey key{M, N, Kp, (int)ta, (int)tb, (int)act, (int)out_fp32, split_k < 0 ? 1 : 0};
+        bool hit = false;
+        {
+            std::lock_guard<std::mutex> lk(g_tune_mu);
+            auto it = g_tune.find(key);
+            if (it != g_tune.end()) { cfg = it->second.first; split = it->second.second; hit = true; }
+        }
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(cur_stream(), &cap);
+        if (!hit && autotune_enabled() && cap == hipStreamCaptureStatusNone) {
+            Tensor scratch = at::empty({M, N}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
+            const int cfgs[4] = {0, 1, 6, 2};
+            const int splits[5] = {1, 2, 4, 8, 16};
+            const int nsplit = split_k < 0 ? 5 : 1;
+            Tensor tws = at::empty({rn_gemm_ws_floats(M, N, 16)}, a.options().dtype(at::kFloat));
+            hipEvent_t e0, e1;
+            (void)hipEventCreate(&e0);
+            (void)hipEventCreate(&e1);
+            float best_ms = 1e30f;
+            int best_cfg = 0, best_split = 1;
+            for (int ci = 0; ci < 4; ++ci) {
+                for (int si = 0; si < nsplit; ++si) {
+                    const int sp = splits[si];
+                    if (sp > 1 && Kp / sp < 256) break;
+                    auto run = [&]() {
+                        return rn_gemm(A.data_ptr(), B.data_ptr(), scratch.data_ptr(), optr(bias), optr(residual), nullptr,
+                                       tws.data_ptr<float>(), alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr,
+                                       (int)M, (int)N, (int)Kp, A.stride(0), B.stride(0), scratch.stride(0), ta, tb, (int)act,
+                                       sp, out_fp32, 0, cfgs[ci], cur_stream());
+                    };
+                    if (run() != 0) continue;
+                    (void)hipEventRecord(e0, cur_stream());
+                    for (int r = 0; r < 3; ++r) run();
+                    (void)hipEventRecord(e1, cur_stream());
+                    (void)hipEventSynchronize(e1);
+                    float ms = 0.f;
+                    (void)hipEventElapsedTime(&ms, e0, e1);
+                    if (ms < best_ms) { best_ms = ms; best_cfg = cfgs[ci]; best_split = sp; }
+                }
+            }
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            {
+                std::lock_guard<std::mutex> lk(g_tune_mu);
+                g_tune[key] = {best_cfg, best_split};
+            }
+            if (std::getenv("REPLICANN_GEMM_VERBOSE"))
+                std::fprintf(stderr, "[replicann gemm tune] M=%ld N=%ld K=%ld ta=%d tb=%d act=%ld -> cfg %d split %d (%.3f ms)\n",
+                             (long)M, (long)N, (long)Kp, (int)ta, (int)tb, (long)act, best_cfg, best_split, best_ms / 3);
+            cfg = best_cfg;
+            split = best_split;
+        }
+        if (split > 1 && max_split < split) ws = at::empty({rn_gemm_ws_floats(M, N, split)}, a.options().dtype(at::kFloat));
+    }
+    const int ws_split = split > 1 ? split : max_split;
+    if (ws_split > 1 && !ws.defined()) ws = at::empty({rn_gemm_ws_floats(M, N, ws_split)}, a.options().dtype(at::kFloat));
     int rc = rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
-                     preact && preact->defined() ? preact->data_ptr() : nullptr, max_split > 1 ? ws.data_ptr<float>() : nullptr,
+                     preact && preact->defined() ? preact->data_ptr() : nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr,
                      alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr, (int)M, (int)N, (int)Kp, A.stride(0),
                      B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32, accumulate, (int)cfg, cur_stream());
     TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
@@ -550,6 +652,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("native_version() -> int");
+    m.def("gemm_tuning_table() -> str");
 }
 
 TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
@@ -590,4 +693,5 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
 
 TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {
     m.impl("native_version", &native_version);
+    m.impl("gemm_tuning_table", &gemm_tuning_table);
 }

@@ -9,13 +9,16 @@ the stock-PyTorch comparison bench and is never set by tests.)
 
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 from pathlib import Path
 
 import torch
 
 _SO = Path(__file__).resolve().parent / "_C.so"
 _state = {"loaded": False, "error": None}
+_tls = threading.local()
 
 
 def load() -> bool:
@@ -52,6 +55,18 @@ def aten_fallback_allowed() -> bool:
     return os.environ.get("REPLICANN_ALLOW_ATEN_FALLBACK", "0") == "1"
 
 
+@contextlib.contextmanager
+def reference_path():
+    """Run GPU tensors through the plain-ATen reference math instead of the HIP
+    kernels (validation only: full-size fp32 loss-trajectory checks on the GPU)."""
+    prev = getattr(_tls, "ref", False)
+    _tls.ref = True
+    try:
+        yield
+    finally:
+        _tls.ref = prev
+
+
 def use_native(*tensors) -> bool:
     """True if this call must run on the HIP kernels.
 
@@ -65,7 +80,7 @@ def use_native(*tensors) -> bool:
             break
     if dev is None or dev.type != "cuda":
         return False
-    if aten_fallback_allowed():
+    if aten_fallback_allowed() or getattr(_tls, "ref", False):
         return False
     if not load():
         raise RuntimeError(

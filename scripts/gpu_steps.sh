@@ -21,6 +21,8 @@ for step in "$@"; do
     opsk) run opsk 900 python -m pytest tests/test_ops_gpu.py -q ;;
     models) run models 600 python -m pytest tests/test_models.py -m gpu -q ;;
     gpu_all) run gpu_all 1200 python -m pytest tests -m gpu -q ;;
+    conv) run conv 900 python -m pytest tests/test_convergence_gpu.py -q ;;
+    traj) run traj 900 python scripts/check_trajectory.py --model gpt2-small gpt2-medium vit-b16 resnet18 --steps 8 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     bench_small) run bench_small 600 python bench.py --steps 5 --warmup 2 --batch 4 ;;

@@ -70,6 +70,21 @@ def main():
         res.append(r)
     if len(sys.argv) > 1 and sys.argv[1] == "gemm":
         return
+    # fp8 (block-scaled MFMA) vs bf16 on GPT-2-medium forward shapes
+    for name, m, n, k in (("med_qkv", M, 3072, 1024), ("med_fc", M, 4096, 1024), ("med_fc2", M, 1024, 4096),
+                          ("med_proj", M, 1024, 1024)):
+        a, b = bf(m, k), bf(n, k)
+        qa, sa = ops.quantize_fp8(a)
+        qb, sb = ops.quantize_fp8(b)
+        f8 = lambda: torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, None, None, 0, None)
+        q8 = lambda: ops.quantize_fp8(a)
+        b16 = lambda: ops.gemm(a, b, tb=True)
+        fl = 2 * m * n * k
+        t8, tq, t16 = (min(timeit(f) for _ in range(2)) for f in (f8, q8, b16))
+        r = dict(op=f"fp8_{name}", fp8_gemm_tflops=fl / t8 / 1e9, bf16_gemm_tflops=fl / t16 / 1e9,
+                 fp8_ms=t8, quant_act_ms=tq, bf16_ms=t16)
+        print(json.dumps(r), flush=True)
+        res.append(r)
     # attention fwd / bwd (B=16, H=12, T=1024, D=64, causal)
     B, T, H, D = 16, 1024, 12, 64
     qkv = bf(B, T, 3, H, D).requires_grad_()
