@@ -11,14 +11,13 @@ from __future__ import annotations
 
 import contextlib
 import os
-import threading
 from pathlib import Path
 
 import torch
 
 _SO = Path(__file__).resolve().parent / "_C.so"
 _state = {"loaded": False, "error": None}
-_tls = threading.local()
+_ref = {"on": False}  # process-wide: autograd runs backward on its own device threads
 
 
 def load() -> bool:
@@ -59,12 +58,12 @@ def aten_fallback_allowed() -> bool:
 def reference_path():
     """Run GPU tensors through the plain-ATen reference math instead of the HIP
     kernels (validation only: full-size fp32 loss-trajectory checks on the GPU)."""
-    prev = getattr(_tls, "ref", False)
-    _tls.ref = True
+    prev = _ref["on"]
+    _ref["on"] = True
     try:
         yield
     finally:
-        _tls.ref = prev
+        _ref["on"] = prev
 
 
 def use_native(*tensors) -> bool:
@@ -80,7 +79,7 @@ def use_native(*tensors) -> bool:
             break
     if dev is None or dev.type != "cuda":
         return False
-    if aten_fallback_allowed() or getattr(_tls, "ref", False):
+    if aten_fallback_allowed() or _ref["on"]:
         return False
     if not load():
         raise RuntimeError(

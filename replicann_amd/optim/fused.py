@@ -81,6 +81,16 @@ class _FlatOptimizer:
         _ext.ops().opt_prep(self.norm_buf, self.lr, w, t, r, self.schedule is not None,
                             -1.0 if lr is None else float(lr), b1, b2)
 
+    def state_tensors(self):
+        """Every device tensor a step mutates (parameters, master, moments, device state)."""
+        ts = [self.flat.data, self.norm_buf] + [t for t in self._extra_state() if t is not None]
+        if self.master is not self.flat.data:
+            ts.append(self.master)
+        return ts
+
+    def _extra_state(self):
+        return []
+
     def skipped_last_step(self):
         return bool(self.norm_buf[1].item())
 
@@ -122,6 +132,9 @@ class FusedAdamW(_FlatOptimizer):
         self.master.add_(upd, alpha=-lr)
         if self.master is not self.flat.data:
             self.flat.data.copy_(self.master)
+
+    def _extra_state(self):
+        return [self.m, self.v]
 
     def state_dict(self):
         return {"step": self.step_count, "master": self.master, "m": self.m, "v": self.v, "lr": self.lr}
@@ -172,6 +185,9 @@ class FusedSGD(_FlatOptimizer):
         self.master.add_(d, alpha=-lr)
         if self.master is not self.flat.data:
             self.flat.data.copy_(self.master)
+
+    def _extra_state(self):
+        return [self.buf]
 
     def state_dict(self):
         return {"step": self.step_count, "master": self.master, "buf": self.buf, "lr": self.lr}

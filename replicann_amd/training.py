@@ -174,21 +174,32 @@ class Trainer:
 
         Inputs are copied into static buffers before each replay; the LR
         schedule / bias corrections are device-side, so replays are exact.
-        The warm-up iterations on the side stream are real training steps."""
+        Two warm-up iterations run first on a side stream (they trigger the
+        GEMM autotuner and every lazy allocation outside the capture); the
+        training state they touch is snapshotted and restored, so graph mode
+        follows exactly the same step sequence as eager mode."""
         c = self.cfg
         self._static = [tuple(t.clone() for t in next(self.data)) for _ in range(c.grad_accum)]
+        state = self.opt.state_tensors() + [b for b in self.model.buffers()]
+        snap = [t.clone() for t in state]
+        count = self.opt.step_count
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
                 self._step_body(self._static)
-                self.step_idx += 1
         torch.cuda.current_stream().wait_stream(s)
+        for t, v in zip(state, snap):
+            t.copy_(v)
+        self.opt.step_count = count
         torch.cuda.synchronize()
+        del snap
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._static_loss = self._step_body(self._static)
+        self.opt.step_count = count  # capture only recorded the step; replays count themselves
         self._graph = g
+        self._static_fresh = True  # the static buffers already hold this step's batch
 
     def step(self, lr=None):
         """One optimizer step; returns the (device) loss of the last micro-batch.
@@ -198,10 +209,12 @@ class Trainer:
         if lr is None and self.graph_enabled():
             if self._graph is None:
                 self._capture()
-            for (sx, sy) in self._static:
-                x, y = next(self.data)
-                sx.copy_(x, non_blocking=True)
-                sy.copy_(y, non_blocking=True)
+            if not self._static_fresh:
+                for (sx, sy) in self._static:
+                    x, y = next(self.data)
+                    sx.copy_(x, non_blocking=True)
+                    sy.copy_(y, non_blocking=True)
+            self._static_fresh = False
             self._graph.replay()
             self.opt.step_count += 1
             self.step_idx += 1

@@ -16,9 +16,10 @@ from replicann_amd.training import TrainConfig, Trainer
 pytestmark = pytest.mark.gpu
 
 
-def _losses(model, steps, ref, **kw):
-    cfg = TrainConfig(model=model, steps=steps, warmup_steps=2, lr=1e-3, log_every=10**9,
-                      dtype="fp32" if ref else "bf16", graph="off" if ref else "auto", **kw)
+def _losses(model, steps, ref, graph="auto", **kw):
+    kw = {"lr": 1e-3, **kw}
+    cfg = TrainConfig(model=model, steps=steps, warmup_steps=2, log_every=10**9,
+                      dtype="fp32" if ref else "bf16", graph="off" if ref else graph, **kw)
     out = []
     if ref:
         with _ext.reference_path():
@@ -45,6 +46,13 @@ def test_loss_trajectory_matches_fp32_reference(cuda, model, kw, tol):
     rel = [abs(a - b) / abs(b) for a, b in zip(nat, ref)]
     assert max(rel) < tol, list(zip(nat, ref))
     assert nat[-1] < nat[0]  # pool of fixed batches: the model must fit it
+
+
+def test_graph_replay_matches_eager(cuda):
+    kw = dict(batch_size=8, seq_len=128)
+    g = _losses("gpt2-tiny", 6, False, graph="on", **kw)
+    e = _losses("gpt2-tiny", 6, False, graph="off", **kw)
+    assert max(abs(a - b) for a, b in zip(g, e)) < 2e-3, list(zip(g, e))
 
 
 def rel_err(a, b):
