@@ -36,12 +36,13 @@ int rn_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, 
 int rn_ln_bwd_waves(int);
 long rn_ln_bwd_ws(int, int);
 int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
-              void*, void*, float*, int, int, int, hipStream_t);
+              void*, void*, void*, float*, int, int, int, hipStream_t);
 void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
 void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
 void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int, hipStream_t);
 void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
 void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, hipStream_t);
+void rn_emb_bwd_acc(const int64_t*, const void*, float*, unsigned*, void*, void*, int, int, int, hipStream_t);
 void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
 int rn_norm_ws_floats();
 void rn_sumsq(const void*, long, int, float*, float*, hipStream_t);
@@ -350,8 +351,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const 
 }
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optional<Tensor>& gh, const Tensor& h,
                                                  const Tensor& w, const Tensor& mean, const Tensor& rstd,
-                                                 const optional<Tensor>& dw_accum, const optional<Tensor>& db_accum) {
+                                                 const optional<Tensor>& dw_accum, const optional<Tensor>& db_accum,
+                                                 const optional<Tensor>& dxs_accum) {
     CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(h); GUARD(dy);
+    if (dxs_accum && dxs_accum->defined()) {
+        CHECK_BF16(*dxs_accum);
+        TORCH_CHECK(dxs_accum->numel() == dy.size(1) && dxs_accum->is_contiguous());
+    }
     const int M = dy.size(0), E = dy.size(1);
     Tensor dx = at::empty_like(dy);
     const bool accum = dw_accum && dw_accum->defined() && db_accum && db_accum->defined();
@@ -361,6 +367,7 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optiona
     if (M) {
         int rc = rn_ln_bwd(dy.data_ptr(), optr(gh), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), dx.data_ptr(), nullptr, nullptr, dw.data_ptr(), db.data_ptr(),
+                           (dxs_accum && dxs_accum->defined()) ? dxs_accum->data_ptr() : nullptr,
                            part.data_ptr<float>(), M, E, accum, cur_stream());
         TORCH_CHECK(rc == 0, "layernorm_bwd: unsupported E=", E);
     } else if (!accum) { dw.zero_(); db.zero_(); }
@@ -393,6 +400,44 @@ std::tuple<Tensor, Tensor> embedding_bwd(const Tensor& dx, const Tensor& ids, in
     rn_emb_bwd(ids.data_ptr<int64_t>(), dx.data_ptr(), d32.data_ptr<float>(), dwte.data_ptr(), Tp ? dwpe.data_ptr() : nullptr,
                B, T, (int)Tp, (int)V, E, cur_stream());
     return {dwte, dwpe};
+}
+
+// Direct-accumulate embedding backward: gwte/gwpe (flat gradient views) += scatter.
+// The fp32 scratch and owner table are persistent per (device, V, E) and are left
+// in their initial state by every call, so the op is hipGraph-capturable.
+void embedding_bwd_acc(const Tensor& dx, const Tensor& ids, const Tensor& gwte, const optional<Tensor>& gwpe) {
+    CHECK_BF16(dx); CHECK_CONTIG(dx); CHECK_BF16(gwte); CHECK_CONTIG(gwte); GUARD(dx);
+    TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous());
+    const int64_t V = gwte.size(0), E = gwte.size(1);
+    TORCH_CHECK(dx.size(-1) == E && E % 4 == 0, "embedding_bwd_acc: width mismatch / E % 4");
+    const int T = ids.dim() >= 2 ? ids.size(-1) : ids.numel();
+    const int B = ids.numel() / std::max(T, 1);
+    if (gwpe && gwpe->defined()) {
+        CHECK_BF16(*gwpe); CHECK_CONTIG(*gwpe);
+        TORCH_CHECK(gwpe->size(0) >= T && gwpe->size(1) == E);
+    }
+    static std::map<std::tuple<int, int64_t, int64_t>, std::pair<Tensor, Tensor>> scratch;
+    static std::mutex mu;
+    std::pair<Tensor, Tensor> buf;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto key = std::make_tuple((int)dx.get_device(), V, E);
+        auto it = scratch.find(key);
+        if (it == scratch.end()) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            (void)hipStreamIsCapturing(cur_stream(), &cs);
+            TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                        "embedding_bwd_acc: first call must be eager (scratch allocation)");
+            Tensor d32 = at::zeros({V * E}, dx.options().dtype(at::kFloat));
+            Tensor own = at::full({V}, -1, dx.options().dtype(at::kInt));
+            it = scratch.emplace(key, std::make_pair(d32, own)).first;
+        }
+        buf = it->second;
+    }
+    if (ids.numel())
+        rn_emb_bwd_acc(ids.data_ptr<int64_t>(), dx.data_ptr(), buf.first.data_ptr<float>(),
+                       reinterpret_cast<unsigned*>(buf.second.data_ptr<int>()), gwte.data_ptr(),
+                       (gwpe && gwpe->defined()) ? gwpe->data_ptr() : nullptr, B, T, (int)E, cur_stream());
 }
 
 // ------------------------------------------------------------------ optimizers
@@ -623,9 +668,10 @@ TORCH_LIBRARY(replicann, m) {
     m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale, Tensor(a!) grad, int nvalid, int ignore) -> ()");
     m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd, "
-          "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None) -> (Tensor, Tensor, Tensor)");
+          "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None, Tensor(c!)? dxs_accum=None) -> (Tensor, Tensor, Tensor)");
     m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
     m.def("embedding_bwd(Tensor dx, Tensor ids, int V, int Tp) -> (Tensor, Tensor)");
+    m.def("embedding_bwd_acc(Tensor dx, Tensor ids, Tensor(a!) gwte, Tensor(b!)? gwpe) -> ()");
     m.def("sumsq(Tensor g, Tensor(a!) normbuf) -> ()");
     m.def("opt_prep(Tensor(a!) state, float base_lr, float warmup, float total, float min_ratio, bool cosine, "
           "float lr_override, float b1, float b2) -> ()");
@@ -670,6 +716,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("layernorm_bwd", &layernorm_bwd);
     m.impl("embedding_fwd", &embedding_fwd);
     m.impl("embedding_bwd", &embedding_bwd);
+    m.impl("embedding_bwd_acc", &embedding_bwd_acc);
     m.impl("sumsq", &sumsq);
     m.impl("opt_prep", &opt_prep);
     m.impl("adamw_step", &adamw_step);

@@ -139,23 +139,91 @@ __global__ void __launch_bounds__(256) rn_colred1_k(const float* __restrict__ in
     if (w == 0 && c < C) tmp[(long)blockIdx.y * C + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
-__global__ void rn_colred2_k(const float* __restrict__ tmp, int S, int C, float* __restrict__ out32,
+__global__ void rn_colred2_k(const float* __restrict__ tmp, int S, int C, long ld, float* __restrict__ out32,
                              __bf16* __restrict__ out16, int accum) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     float s = 0.f;
-    for (int i = 0; i < S; ++i) s += tmp[(long)i * C + c];
+    for (int i = 0; i < S; ++i) s += tmp[(long)i * ld + c];
     if (out32) out32[c] = s + (accum ? out32[c] : 0.f);
     if (out16) out16[c] = (__bf16)(s + (accum ? (float)out16[c] : 0.f));
+}
+
+// ---------------------------------------------------------------------------
+// Single-launch version: grid (ceil(C/64), S); every block writes its stage-1
+// row of tmp, bumps a per-column-chunk arrival counter (release/acquire at
+// agent scope), and the LAST arriving block of a chunk sums the S rows in fixed
+// order and writes the outputs, then re-arms the counter.  One launch instead
+// of two, still bitwise reproducible.  Outputs may be split into segments of
+// `seg` columns (e.g. [dw | db] of LayerNorm in one pass).
+// ---------------------------------------------------------------------------
+constexpr int RN_COLSUM_MAXCB = 4096;
+__device__ unsigned int rn_colsum_cnt[RN_COLSUM_MAXCB];  // zero at load, self-resetting
+
+struct RnColOut {
+    float* o32[3];
+    __bf16* o16[3];
+    int seg;
+    int accum[3];  // per segment: add into the outputs
+};
+
+__global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in, int R, int C,
+                                                   float* __restrict__ tmp, RnColOut out) {
+    __shared__ float red[4][64];
+    __shared__ int is_last;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    const int S = gridDim.y;
+    const int r0 = (int)((long)R * blockIdx.y / S), r1 = (int)((long)R * (blockIdx.y + 1) / S);
+    float s = 0.f;
+    if (c < C)
+        for (int r = r0 + w; r < r1; r += 4) s += in[(long)r * C + c];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0) {
+        if (c < C) tmp[(long)blockIdx.y * C + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            unsigned t = __hip_atomic_fetch_add(&rn_colsum_cnt[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            is_last = (t == (unsigned)S - 1);
+        }
+    }
+    __syncthreads();
+    if (!is_last || w != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (c < C) {
+        float acc = 0.f;
+        for (int i = 0; i < S; ++i) acc += __builtin_nontemporal_load(tmp + (long)i * C + c);
+        const int k = c / out.seg, o = c - k * out.seg;
+        if (out.o32[k]) out.o32[k][o] = acc + (out.accum[k] ? out.o32[k][o] : 0.f);
+        if (out.o16[k]) out.o16[k][o] = (__bf16)(acc + (out.accum[k] ? (float)out.o16[k][o] : 0.f));
+    }
+    if (lane == 0) rn_colsum_cnt[blockIdx.x] = 0u;
+}
+
+// Segmented column reduction: out.seg columns per output segment (≤ 3 segments).
+// tmp must hold RN_COLRED_S * C floats.
+static inline void rn_colreduce_seg(const float* in, int R, int C, float* tmp, const RnColOut& out,
+                                    hipStream_t st) {
+    int S = R < RN_COLRED_S ? (R > 0 ? R : 1) : RN_COLRED_S;
+    const int cb = (C + 63) / 64;
+    if (cb <= RN_COLSUM_MAXCB) {
+        rn_colsum_k<<<dim3(cb, S), 256, 0, st>>>(in, R, C, tmp, out);
+        return;
+    }
+    rn_colred1_k<<<dim3(cb, S), 256, 0, st>>>(in, R, C, tmp);
+    for (int k = 0; k * out.seg < C; ++k)
+        rn_colred2_k<<<(out.seg + 255) / 256, 256, 0, st>>>(
+            tmp + (long)k * out.seg, S, out.seg < C - k * out.seg ? out.seg : C - k * out.seg, C, out.o32[k],
+            out.o16[k], out.accum[k]);
 }
 
 // tmp must hold RN_COLRED_S * C floats.  accum: add into the outputs (gradient accumulation).
 static inline void rn_colreduce(const float* in, int R, int C, float* tmp, float* out32, __bf16* out16,
                                 hipStream_t st, int accum = 0) {
-    int S = R < RN_COLRED_S ? (R > 0 ? R : 1) : RN_COLRED_S;
-    dim3 g((C + 63) / 64, S);
-    rn_colred1_k<<<g, 256, 0, st>>>(in, R, C, tmp);
-    rn_colred2_k<<<(C + 255) / 256, 256, 0, st>>>(tmp, S, C, out32, out16, accum);
+    RnColOut o{{out32, nullptr, nullptr}, {out16, nullptr, nullptr}, C, {accum, 0, 0}};
+    rn_colreduce_seg(in, R, C, tmp, o, st);
 }
 
 }  // namespace

@@ -115,7 +115,7 @@ RN_DEV uint64_t drop_idx(const AttnArgs& p, int b, int h, int qi, int kj) {
 // ============================== forward, D = 64 ==============================
 // grid: (ceil(Tq/128), B*H); 4 waves x 32 query rows.
 template <bool CAUSAL, bool BIAS, bool DROP>
-__global__ void __launch_bounds__(256, 2) attn_fwd64_k(AttnArgs p) {
+__global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -125,6 +125,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd64_k(AttnArgs p) {
     const int q0 = qb * 128 + wave * 32;
     const int off = p.Tk - p.Tq;  // causal: key j visible to query i iff j <= i + off
     const float sl2 = p.scale * LOG2E;
+    const float xs = BIAS ? 1.f : sl2;  // units of the running max m: log2-scaled with bias, raw without
 
     const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
     const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
@@ -201,7 +202,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd64_k(AttnArgs p) {
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float x = sacc[qi][j][r] * sl2 + (BIAS ? bb[r] * LOG2E : 0.f);
+                    // no bias: keep raw scores (the scale folds into the exp's FMA below)
+                    float x = BIAS ? sacc[qi][j][r] * sl2 + bb[r] * LOG2E : sacc[qi][j][r];
                     if (need_mask) {
                         const int kvj = kvb + r;
                         if (kvj >= p.Tk || (CAUSAL && kvj > qg + off)) x = -INFINITY;
@@ -214,14 +216,15 @@ __global__ void __launch_bounds__(256, 2) attn_fwd64_k(AttnArgs p) {
             tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
             const float mn = fmaxf(m[qi], tmax);
             const float ms = (mn == -INFINITY) ? 0.f : mn;  // fully-masked rows stay at p = 0
-            const float alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[qi] - ms);
+            const float alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m[qi] - ms) * xs);
+            const float nms = -ms * xs;
             m[qi] = mn;
             float ls = 0.f;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float pv = __builtin_amdgcn_exp2f(sacc[qi][j][r] - ms);
+                    float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[qi][j][r], xs, nms));
                     ls += pv;
                     if constexpr (DROP) {
                         const int kvj = kv0 + j * 16 + 4 * g + r;
@@ -264,7 +267,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd64_k(AttnArgs p) {
                 *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
             }
             if (g == 0)
-                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] + log2f(lt)) * LN2 : INFINITY;
+                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * xs + log2f(lt)) * LN2 : INFINITY;
         }
     }
 }

@@ -37,6 +37,53 @@ __global__ void __launch_bounds__(256) emb_bwd_scatter_k(const int64_t* __restri
     for (int c = lane; c < E; c += 64) atomicAdd(dwte + id * E + c, bf2f(dx[(long)row * E + c]));
 }
 
+// ---- direct-accumulate variant (graph-safe, no full-table memset / convert) ----
+// d32 is a PERSISTENT fp32 V×E scratch kept all-zero between calls and owner a
+// persistent V-entry table kept at 0xFFFFFFFF.  Scatter: fp32 atomics into d32
+// plus atomicMin(owner[id], position).  Finish: the owning position of each
+// touched row adds the fp32 row into the bf16 gradient once, re-zeroes the
+// scratch row and re-arms owner — only touched rows are visited.
+__global__ void __launch_bounds__(256) emb_scatter_own_k(const int64_t* __restrict__ ids,
+                                                         const bf16* __restrict__ dx, float* __restrict__ d32,
+                                                         unsigned* __restrict__ owner, int rows, int E) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long id = ids[row];
+    if (lane == 0) atomicMin(owner + id, (unsigned)row);
+    for (int c = lane; c < E; c += 64) atomicAdd(d32 + id * E + c, bf2f(dx[(long)row * E + c]));
+}
+
+__global__ void __launch_bounds__(256) emb_finish_k(const int64_t* __restrict__ ids, float* __restrict__ d32,
+                                                    unsigned* __restrict__ owner, bf16* __restrict__ g, int rows,
+                                                    int E) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long id = ids[row];
+    if (owner[id] != (unsigned)row) return;
+    for (int c = lane * 4; c < E; c += 256) {
+        float4 v = *reinterpret_cast<float4*>(d32 + id * E + c);
+        *reinterpret_cast<float4*>(d32 + id * E + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+        bf16* q = g + id * E + c;
+        q[0] = (bf16)((float)q[0] + v.x);
+        q[1] = (bf16)((float)q[1] + v.y);
+        q[2] = (bf16)((float)q[2] + v.z);
+        q[3] = (bf16)((float)q[3] + v.w);
+    }
+    if (lane == 0) owner[id] = 0xFFFFFFFFu;
+}
+
+// dwpe[t] += sum_b dx[b, t]
+__global__ void emb_pos_acc_k(const bf16* __restrict__ dx, bf16* __restrict__ dwpe, int B, int T, int E) {
+    const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (i >= (long)T * E) return;
+    const int t = i / E, c = i % E;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += bf2f(dx[((long)b * T + t) * E + c]);
+    dwpe[i] = f2bf(bf2f(dwpe[i]) + s);
+}
+
 // dwpe[t] = sum_b dx[b, t]   (thread per column, loops over the batch)
 __global__ void emb_bwd_pos_k(const bf16* __restrict__ dx, bf16* __restrict__ dwpe, int B, int T, int Tp, int E) {
     const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -222,6 +269,15 @@ void rn_emb_bwd(const int64_t* ids, const void* dx, float* dwte32, void* dwte, v
     long n = (long)V * E;
     f32_to_bf16_k<<<grid_for(n / 4), 256, 0, st>>>(dwte32, (bf16*)dwte, n);
     if (dwpe) emb_bwd_pos_k<<<rn_cdiv((long)Tp * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)dwpe, B, T, Tp, E);
+}
+
+// E % 4 == 0.  gwte (bf16 V×E) and gwpe (bf16 ≥T×E, may be null) are accumulated into.
+void rn_emb_bwd_acc(const int64_t* ids, const void* dx, float* d32, unsigned* owner, void* gwte, void* gwpe, int B,
+                    int T, int E, hipStream_t st) {
+    const int rows = B * T;
+    emb_scatter_own_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (const bf16*)dx, d32, owner, rows, E);
+    emb_finish_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, d32, owner, (bf16*)gwte, rows, E);
+    if (gwpe) emb_pos_acc_k<<<rn_cdiv((long)T * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)gwpe, B, T, E);
 }
 
 int rn_norm_ws_floats() { return NORM_BLOCKS; }

@@ -65,22 +65,32 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const bf16* __restrict__ x, cons
     if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
 }
 
-template <int NV, bool GH>
+// One row per wave; each block folds its 4 waves' column partials in LDS and
+// writes ONE partial row [dw | db | Σdx] (Q = 2 or 3 segments of E floats), so
+// the column reduction reads 4× fewer partials and runs as a single launch.
+// Σdx (DXS) is the bias gradient of the linear layer whose output fed this
+// LayerNorm (x = x_prev + a·Wᵀ + b ⇒ db = Σ_rows dx): computed here for free
+// instead of a separate pass over dx.
+template <int NV, bool GH, bool DXS>
 __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ gh,
                                                 const bf16* __restrict__ h, const bf16* __restrict__ w,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                bf16* __restrict__ dx, float* __restrict__ pdw,
-                                                float* __restrict__ pdb, int M, int E) {
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                bf16* __restrict__ dx, float* __restrict__ part, int M, int E) {
+    constexpr int Q = DXS ? 3 : 2;
+    __shared__ float red[3][NV * 512];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wave = blockIdx.x * 4 + wv;
     const int nwaves = gridDim.x * 4;
     const int nvec = E / 8;
-    float adw[NV][8], adb[NV][8], wf[NV][8];
+    float acc[Q][NV][8], wf[NV][8];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         int c = lane + i * 64;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { adw[i][j] = 0.f; adb[i][j] = 0.f; }
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc[q][i][j] = 0.f;
+        }
         if (c < nvec) load8(w + c * 8, wf[i]);
     }
     for (int row = wave; row < M; row += nwaves) {
@@ -100,8 +110,8 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
                     g[i][j] = d[j] * wf[i][j];
                     s1 += g[i][j];
                     s2 += g[i][j] * xh[i][j];
-                    adw[i][j] += d[j] * xh[i][j];
-                    adb[i][j] += d[j];
+                    acc[0][i][j] += d[j] * xh[i][j];
+                    acc[1][i][j] += d[j];
                 }
             }
         }
@@ -121,19 +131,43 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
                     for (int j = 0; j < 8; ++j) o[j] += t[j];
                 }
                 store8(dx + (long)row * E + c * 8, o);
+                if constexpr (DXS) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[Q - 1][i][j] += (float)(bf16)o[j];  // Σ of the stored dx
+                }
             }
         }
     }
+    // fold the 4 waves: waves 1..3 park their partials in LDS, wave 0 adds (fixed order)
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int c = lane + i * 64;
-        if (c < nvec) {
+    for (int q = 0; q < Q; ++q) {
+        if (wv > 0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                pdw[(long)wave * E + c * 8 + j] = adw[i][j];
-                pdb[(long)wave * E + c * 8 + j] = adb[i][j];
+            for (int i = 0; i < NV; ++i) {
+                int c = lane + i * 64;
+                if (c < nvec) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) red[wv - 1][c * 8 + j] = acc[q][i][j];
+                }
             }
         }
+        __syncthreads();
+        if (wv == 0) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                int c = lane + i * 64;
+                if (c < nvec) {
+                    float o[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        o[j] = acc[q][i][j] + red[0][c * 8 + j] + red[1][c * 8 + j] + red[2][c * 8 + j];
+                    float* dst = part + (long)blockIdx.x * Q * E + (long)q * E + c * 8;
+                    *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+                    *reinterpret_cast<float4*>(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -158,31 +192,33 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
     return 0;
 }
 
-int rn_ln_bwd_waves(int M) { int W = M < 2048 ? M : 2048; return ((W + 3) / 4) * 4; }
+int rn_ln_bwd_blocks(int M) { int W = M < 2048 ? M : 2048; return (W + 3) / 4; }
+int rn_ln_bwd_waves(int M) { return 4 * rn_ln_bwd_blocks(M); }
 
-// pdw/pdb workspace: rn_ln_bwd_waves(M) * E floats each.
-long rn_ln_bwd_ws(int M, int E) { return 2L * rn_ln_bwd_waves(M) * E + 2L * RN_COLRED_S * E; }
+// workspace floats: partial rows [blocks][3E] + the reduction's [RN_COLRED_S][3E] scratch
+long rn_ln_bwd_ws(int M, int E) { return 3L * (rn_ln_bwd_blocks(M) + RN_COLRED_S) * E; }
 
 // ws: rn_ln_bwd_ws(M, E) floats.  dw/db (fp32) and dw16/db16 (bf16) outputs, any may be null.
+// dxs16 (optional, bf16, always accumulated into): Σ_rows dx — the bias gradient of the layer
+// that produced this LayerNorm's input.
 int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, const float* mean, const float* rstd,
-              void* dx, float* dw, float* db, void* dw16, void* db16, float* ws, int M, int E, int accum,
-              hipStream_t st) {
-    float* pdw = ws;
-    float* pdb = ws + (long)rn_ln_bwd_waves(M) * E;
+              void* dx, float* dw, float* db, void* dw16, void* db16, void* dxs16, float* ws, int M, int E,
+              int accum, hipStream_t st) {
     if (E % 8 != 0 || E > 8192) return -1;
-    int nv = rn_ln_nv(E);
-    int W = rn_ln_bwd_waves(M);
-    dim3 grid(W / 4);
-#define RN_LNB(NV, G) ln_bwd_k<NV, G><<<grid, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, pdw, pdb, M, E)
-#define RN_LNB2(NV) { if (gh) RN_LNB(NV, true); else RN_LNB(NV, false); }
+    const int nv = rn_ln_nv(E);
+    const int B = rn_ln_bwd_blocks(M);
+    const int Q = dxs16 ? 3 : 2;
+    float* part = ws;
+    float* tmp = ws + (long)B * Q * E;
+#define RN_LNB(NV, G, D) ln_bwd_k<NV, G, D><<<B, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, E)
+#define RN_LNB2(NV) { if (gh) { if (dxs16) RN_LNB(NV, true, true); else RN_LNB(NV, true, false); } \
+                      else { if (dxs16) RN_LNB(NV, false, true); else RN_LNB(NV, false, false); } }
     if (nv <= 1) RN_LNB2(1) else if (nv <= 2) RN_LNB2(2) else if (nv <= 4) RN_LNB2(4) else if (nv <= 8) RN_LNB2(8)
     else RN_LNB2(16)
 #undef RN_LNB2
 #undef RN_LNB
-    // pdw/pdb are followed by 2 * RN_COLRED_S * E floats of scratch (see rn_ln_bwd_ws)
-    float* tmp = pdb + (long)W * E;
-    rn_colreduce(pdw, W, E, tmp, dw, (bf16*)dw16, st, accum);
-    rn_colreduce(pdb, W, E, tmp + RN_COLRED_S * E, db, (bf16*)db16, st, accum);
+    RnColOut o{{dw, db, nullptr}, {(bf16*)dw16, (bf16*)db16, (bf16*)dxs16}, E, {accum, accum, 1}};
+    rn_colreduce_seg(part, B, Q * E, tmp, o, st);
     return 0;
 }
 

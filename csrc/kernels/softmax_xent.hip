@@ -128,6 +128,67 @@ __global__ void __launch_bounds__(TPB) xent_fwd_k(bf16* __restrict__ logits, con
     }
 }
 
+// Single-pass variant for V % 8 == 0, V <= 8 * 1024 * CH: the 1024-thread block
+// keeps its whole row in registers (CH 16-byte chunks per thread), so the row is
+// read from HBM once and (GRAD) written once — the two-pass kernel above re-reads
+// it.  Same outputs and the same fixed reduction order for every launch.
+template <int CH, bool GRAD>
+__global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                   float* __restrict__ loss, float* __restrict__ lse_out, int V,
+                                                   int nvalid, long ignore) {
+    __shared__ float sm[16];
+    bf16* row = logits + (long)blockIdx.x * V;
+    const int n8 = V / 8;
+    const long t = tgt[blockIdx.x];
+    const bool ign = (t == ignore || t < 0 || t >= nvalid);
+    const float xt = ign ? 0.f : bf2f(row[t]);
+    bf16x8 v[CH];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        if (i < n8) {
+            v[k] = *reinterpret_cast<const bf16x8*>(row + i * 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i * 8 + j < nvalid) m = fmaxf(m, (float)v[k][j]);
+        }
+    }
+    m = block_max(m, sm);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        if (i < n8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i * 8 + j < nvalid) s += __expf((float)v[k][j] - m);
+        }
+    }
+    s = block_sum(s, sm);
+    const float lse = m + __logf(s);
+    if (threadIdx.x == 0) {
+        lse_out[blockIdx.x] = lse;
+        loss[blockIdx.x] = ign ? 0.f : lse - xt;
+    }
+    if constexpr (GRAD) {
+        const float z = ign ? 0.f : 1.f;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int i = threadIdx.x + k * 1024;
+            if (i < n8) {
+                float f[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int c = i * 8 + j;
+                    f[j] = (c < nvalid ? __expf((float)v[k][j] - lse) - (c == t ? 1.f : 0.f) : 0.f) * z;
+                }
+                store8(row + i * 8, f);
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(TPB) xent_bwd_k(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                   const float* __restrict__ lse, const float* __restrict__ gscale,
                                                   bf16* __restrict__ grad, int V, int nvalid, long ignore) {
@@ -169,6 +230,15 @@ void rn_softmax_bwd(const void* dy, const void* y, void* dx, int M, int N, float
 }
 void rn_xent_fwd(void* logits, const int64_t* tgt, float* loss, float* lse, int M, int V, int nvalid, long ignore,
                  int write_grad, hipStream_t st) {
+    if (V % 8 == 0 && V <= 8 * 1024 * 8) {
+        const int ch = (V / 8 + 1023) / 1024;
+#define RN_XR(C) { if (write_grad) xent_row_k<C, true><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
+                   else xent_row_k<C, false><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); }
+        if (ch <= 1) RN_XR(1) else if (ch <= 2) RN_XR(2) else if (ch <= 4) RN_XR(4) else if (ch <= 7) RN_XR(7)
+        else RN_XR(8)
+#undef RN_XR
+        return;
+    }
     if (write_grad) xent_fwd_k<true><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
     else xent_fwd_k<false><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
 }

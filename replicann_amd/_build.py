@@ -68,7 +68,7 @@ def _compile(src: Path, hdr: str, torch_inc) -> Path:
     if is_binding:
         # host-only TU: torch headers, no device code
         flags = [f for f in flags if not f.startswith("--offload-arch")]
-        flags += ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-O2"]
+        flags += ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-O2", "--offload-host-only"]
         flags += [f"-I{p}" for p in torch_inc]
     key = hashlib.sha1((src.read_text() + hdr + " ".join(flags)).encode()).hexdigest()[:16]
     obj = BUILD / f"{src.stem}.{key}.o"

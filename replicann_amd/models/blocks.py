@@ -12,7 +12,10 @@ GPT-2/ViT formulation: fused c_attn with bias, scale 1/sqrt(head_dim), GELU
     u   = gelu(h·Wfcᵀ + b)                     GEMM (bias + GELU epilogue)
     x   = x + u·Wfc2ᵀ + b                      GEMM (bias + residual epilogue)
 
-Six kernel launches per block forward (plus dropout when enabled).
+Six kernel launches per block forward (plus dropout when enabled).  In the
+backward each LayerNorm kernel also adds the residual-branch gradient (x feeds
+both the LN and the residual) and reduces Σ_rows dx = the bias gradient of the
+c_proj that produced x, so neither needs a pass of its own.
 """
 
 from __future__ import annotations
@@ -51,8 +54,9 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(n))
         self.eps = eps
 
-    def forward(self, x):
-        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+    def forward(self, x, return_sum=False, producer_bias=None):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, return_sum=return_sum,
+                              producer_bias=producer_bias)
 
 
 class Attention(nn.Module):
@@ -62,6 +66,10 @@ class Attention(nn.Module):
         self.c_attn = Linear(n_embd, 3 * n_embd, fp8=fp8)
         self.c_proj = Linear(n_embd, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
         self.attn_dropout, self.resid_dropout = attn_dropout, resid_dropout
+
+    def out_bias(self):
+        """Bias whose gradient equals Σ_rows of the block output's gradient (None if dropout intervenes)."""
+        return self.c_proj.bias if not (self.resid_dropout > 0 and self.training) else None
 
     def forward(self, h, residual):
         B, T, E = h.shape
@@ -81,6 +89,9 @@ class MLP(nn.Module):
         self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
         self.dropout = dropout
 
+    def out_bias(self):
+        return self.c_proj.bias if not (self.dropout > 0 and self.training) else None
+
     def forward(self, h, residual):
         u = self.c_fc(h, act="gelu")
         if self.dropout > 0 and self.training:
@@ -96,7 +107,14 @@ class PreLNBlock(nn.Module):
         self.ln_2 = LayerNorm(n_embd, eps)
         self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer, fp8=fp8)
 
-    def forward(self, x):
-        x = self.attn(self.ln_1(x), residual=x)
-        x = self.mlp(self.ln_2(x), residual=x)
+    def out_bias(self):
+        return self.mlp.out_bias()
+
+    def forward(self, x, prev_bias=None):
+        """``prev_bias``: out_bias() of the block that produced x (its gradient is
+        then reduced inside ln_1's backward kernel)."""
+        h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias)
+        x = self.attn(h, residual=x)
+        h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias())
+        x = self.mlp(h, residual=x)
         return x

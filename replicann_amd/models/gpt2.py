@@ -64,7 +64,8 @@ class GPT2(nn.Module):
         nn.init.normal_(self.wpe, std=0.01)
         with torch.no_grad():
             self.wte[cfg.vocab_size:].zero_()
-        self.wte._rn_shared = True  # tied: embedding + LM head both contribute gradients
+        self.wte._rn_shared = True  # tied: embedding + LM head both contribute gradients ...
+        self.wte._rn_direct_uses = 2  # ... each accumulated in place into the flat .grad
         self.h = nn.ModuleList(
             PreLNBlock(cfg.n_embd, cfg.n_head, causal=True, dropout=cfg.dropout, n_layer=cfg.n_layer,
                        eps=cfg.ln_eps, fp8=cfg.fp8)
@@ -83,9 +84,11 @@ class GPT2(nn.Module):
         x = ops.embedding(idx, self.wte, self.wpe)
         if self.config.dropout > 0 and self.training:
             x = ops.dropout(x, self.config.dropout, True)
+        prev = None
         for blk in self.h:
-            x = blk(x)
-        return self.ln_f(x)
+            x = blk(x, prev)
+            prev = blk.out_bias()
+        return self.ln_f(x, producer_bias=prev)
 
     def forward(self, idx, targets=None):
         """idx (B, T) → logits (B, T, vocab_pad) [, mean CE loss when targets given].

@@ -68,8 +68,10 @@ class ViT(nn.Module):
         x = ops.conv2d_nhwc(images, self.patch_weight, self.patch_bias, stride=c.patch)
         x = x.reshape(B, -1, c.n_embd)
         x = torch.cat([self.cls_token.expand(B, -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype)
+        prev = None
         for blk in self.blocks:
-            x = blk(x)
+            x = blk(x, prev)
+            prev = blk.out_bias()
         x = self.norm(x[:, 0])
         logits = self.head(x)
         if targets is None:

@@ -5,6 +5,9 @@ vectors, one row per wave).  Backward scatter-adds the token gradient with
 fp32 ``global_atomic_add_f32`` shaped as whole 256-B wave-instructions (the
 MI355X guide's atomic-rate recipe) into an fp32 scratch, then rounds to the
 parameter dtype once; the position gradient is a column-sum over the batch.
+With flat-buffer parameters the scratch is persistent and kept zero, and only
+the touched rows are folded into the bf16 gradient (no full-table memset or
+conversion pass; tied LM-head + embedding contributions meet in place).
 """
 
 from __future__ import annotations
@@ -20,6 +23,7 @@ class _EmbFn(torch.autograd.Function):
     def forward(ctx, ids, wte, wpe):
         x = _ext.ops().embedding_fwd(ids, wte, wpe)
         ctx.save_for_backward(ids)
+        ctx.wte_ref, ctx.wpe_ref = wte, wpe
         ctx.V, ctx.has_pos = wte.shape[0], wpe is not None
         ctx.dt = wte.dtype
         ctx.Tp = wpe.shape[0] if wpe is not None else 0
@@ -27,7 +31,18 @@ class _EmbFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gx):
+        from .linear import _direct_grad, _notify
         (ids,) = ctx.saved_tensors
+        wte, wpe = ctx.wte_ref, ctx.wpe_ref
+        gw = _direct_grad(wte)
+        gp = _direct_grad(wpe) if wpe is not None else None
+        if gw is not None and (wpe is None or gp is not None):
+            # accumulate straight into the flat gradient views (touched rows only)
+            _ext.ops().embedding_bwd_acc(gx.contiguous(), ids, gw, gp)
+            _notify(wte)
+            if wpe is not None:
+                _notify(wpe)
+            return None, None, None
         dwte, dwpe = _ext.ops().embedding_bwd(gx.contiguous(), ids, ctx.V, ctx.Tp)
         return None, dwte.to(ctx.dt), (dwpe.to(ctx.dt) if ctx.has_pos else None)
 

@@ -62,13 +62,18 @@ class _LinearFp8Fn(torch.autograd.Function):
             y = y.to(x.dtype)
         ctx.save_for_backward(x2, weight, preact)
         ctx.act, ctx.has_bias, ctx.has_res, ctx.shp = act, bias is not None, residual is not None, shp
+        ctx.bias_ref = bias
         return y.reshape(*shp[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, gy):
         x2, weight, preact = ctx.saved_tensors
         gy2 = gy.reshape(-1, weight.shape[0]).contiguous()
-        dh, db = bias_act_grad(gy2, preact, ctx.act, ctx.has_bias)
+        want_b = ctx.has_bias
+        if want_b and getattr(ctx.bias_ref, "_rn_ln_done", False):  # see ops.norm._LayerNormFn
+            ctx.bias_ref._rn_ln_done = False
+            want_b = False
+        dh, db = bias_act_grad(gy2, preact, ctx.act, want_b)
         gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
         gw = gemm(dh, x2, ta=True, split_k=-1, out_dtype=weight.dtype) if ctx.needs_input_grad[1] else None
         gb = db.to(weight.dtype) if (db is not None and ctx.needs_input_grad[2]) else None

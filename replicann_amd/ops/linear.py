@@ -99,16 +99,28 @@ def bias_act_grad(dy2d, h2d, act, want_bias):
 def _direct_grad(p):
     """The flat-buffer ``.grad`` view of parameter ``p`` if its gradient may be
     accumulated directly by a backward kernel (GEMM epilogue / reduction with
-    ``accumulate``), bypassing autograd's AccumulateGrad add.  Only parameters
-    that are used once per forward qualify (tied weights are flagged shared)."""
+    ``accumulate``), bypassing autograd's AccumulateGrad add.  Parameters used
+    once per forward qualify; a shared (tied) parameter qualifies when it
+    declares how many direct contributions a backward makes (``_rn_direct_uses``,
+    e.g. 2 for GPT-2's token embedding + LM head)."""
     f = getattr(p, "_rn_flat", None)
-    if f is None or not f.direct or getattr(p, "_rn_shared", False) or p.grad is None:
+    if f is None or not f.direct or p.grad is None:
+        return None
+    if getattr(p, "_rn_shared", False) and getattr(p, "_rn_direct_uses", 0) < 2:
         return None
     return p.grad
 
 
 def _notify(p):
-    """Tell the flat buffer (and thus DDP's bucketing) that ``p``'s gradient is final."""
+    """Tell the flat buffer (and thus DDP's bucketing) that ``p``'s gradient is
+    final — for a multi-use parameter, after its last contribution."""
+    uses = getattr(p, "_rn_direct_uses", 1)
+    if uses > 1:
+        left = getattr(p, "_rn_pending", uses) - 1
+        if left > 0:
+            p._rn_pending = left
+            return
+        p._rn_pending = uses
     p._rn_flat.mark_ready(p)
 
 
@@ -156,12 +168,16 @@ class _LinearFn(torch.autograd.Function):
             gy2 = gy2.contiguous()
         native = _ext.use_native(gy2)
         gx = gw = gb = None
-        db_acc = _direct_grad(bias) if (native and ctx.has_bias and ctx.needs_input_grad[2]) else None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if want_b and getattr(bias, "_rn_ln_done", False):
+            # the downstream LayerNorm backward already accumulated Σ_rows gy into bias.grad
+            bias._rn_ln_done = False
+            want_b = False
+        db_acc = _direct_grad(bias) if (native and want_b) else None
         if native:
-            dh, db = _ext.ops().bias_act_grad(gy2, preact if ctx.act != ACT_NONE else None, ctx.act,
-                                              ctx.has_bias and ctx.needs_input_grad[2], db_acc)
+            dh, db = _ext.ops().bias_act_grad(gy2, preact if ctx.act != ACT_NONE else None, ctx.act, want_b, db_acc)
         else:
-            dh, db = bias_act_grad(gy2, preact, ctx.act, ctx.has_bias)
+            dh, db = bias_act_grad(gy2, preact, ctx.act, want_b)
         if ctx.needs_input_grad[0]:
             gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
@@ -171,7 +187,7 @@ class _LinearFn(torch.autograd.Function):
                 _notify(weight)
             else:
                 gw = gemm(dh, x2, ta=True, split_k=-1, out_dtype=weight.dtype)  # split-K chosen natively
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if want_b:
             if db_acc is not None:
                 _notify(bias)
             else:

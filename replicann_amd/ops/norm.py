@@ -20,22 +20,38 @@ from .. import _ext
 
 
 class _LayerNormFn(torch.autograd.Function):
-    """y = LN(x [+ residual]); with a residual the pre-norm sum h is a 2nd output."""
+    """y = LN(x [+ residual]).
+
+    Second output (``two_out``): the pre-norm sum h = x + residual, or — with no
+    residual — a pass-through alias of x.  Either way the gradient arriving on
+    it is added to dx inside the backward kernel (no separate add), which is
+    what a pre-LN block needs: x feeds both the LayerNorm and the residual
+    branch.
+
+    ``producer_bias``: bias of the linear layer whose output IS x (x = x_prev +
+    a·Wᵀ + b).  Its gradient Σ_rows dx is then produced by this backward kernel
+    for free and accumulated straight into the flat gradient buffer; the
+    linear's backward sees ``_rn_ln_done`` and skips its own bias pass.
+    """
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual):
+    def forward(ctx, x, weight, bias, eps, residual, two_out, producer_bias):
         shp = x.shape
         E = shp[-1]
         x2 = x.reshape(-1, E).contiguous()
         r2 = residual.reshape(-1, E).contiguous() if residual is not None else None
         y, h, mean, rstd = _ext.ops().layernorm_fwd(x2, r2, weight, bias, eps)
         ctx.save_for_backward(x2 if residual is None else h, weight, mean, rstd)
+        ctx.set_materialize_grads(False)  # an unused second output → gh None → no zero-tensor read
         ctx.bias_ref = bias
+        ctx.producer_bias = producer_bias if residual is None else None
         ctx.has_res = residual is not None
         ctx.has_bias = bias is not None
         ctx.shp = shp
         if residual is not None:
             return y.reshape(shp), h.reshape(shp)
+        if two_out:
+            return y.reshape(shp), x.view_as(x)
         return y.reshape(shp)
 
     @staticmethod
@@ -44,33 +60,41 @@ class _LayerNormFn(torch.autograd.Function):
         h, weight, mean, rstd = ctx.saved_tensors
         bias = ctx.bias_ref
         E = ctx.shp[-1]
+        if gy is None:
+            gy = torch.zeros(ctx.shp, dtype=h.dtype, device=h.device)
         gy2 = gy.reshape(-1, E).contiguous()
         gh2 = gh.reshape(-1, E).contiguous() if gh is not None else None
         dw_acc = _direct_grad(weight)
         db_acc = _direct_grad(bias) if bias is not None else None
         direct = dw_acc is not None and db_acc is not None
+        pb = ctx.producer_bias
+        pb_acc = _direct_grad(pb) if (pb is not None and direct) else None
         dx, dw, db = _ext.ops().layernorm_bwd(gy2, gh2, h, weight, mean, rstd, dw_acc if direct else None,
-                                              db_acc if direct else None)
+                                              db_acc if direct else None, pb_acc)
         dx = dx.reshape(ctx.shp)
+        if pb_acc is not None:
+            pb._rn_ln_done = True  # consumed (and reset) by the producer linear's backward
+            _notify(pb)
+        g_res = dx if ctx.has_res else None
         if direct:  # gradients already accumulated in the flat buffer
             _notify(weight)
             _notify(bias)
-            return dx, None, None, None, dx if ctx.has_res else None
-        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None,
-                dx if ctx.has_res else None)
+            return dx, None, None, None, g_res, None, None
+        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None, g_res, None, None)
 
 
-def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False):
+def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, producer_bias=None):
     """LayerNorm over the last dim.  With ``residual``: h = x + residual, y = LN(h).
 
-    Returns y, or (y, h) when ``return_sum``.
+    Returns y, or (y, h) when ``return_sum`` (h = x when there is no residual;
+    use that h as the block's residual so both gradients meet in one kernel).
+    ``producer_bias``: see :class:`_LayerNormFn`.
     """
     if _ext.use_native(x):
-        if residual is None:
-            y = _LayerNormFn.apply(x, weight, bias, eps, None)
-            return (y, x) if return_sum else y
-        y, h = _LayerNormFn.apply(x, weight, bias, eps, residual)
-        return (y, h) if return_sum else y
+        out = _LayerNormFn.apply(x, weight, bias, eps, residual, return_sum, producer_bias)
+        if residual is None and not return_sum:
+            return out
+        return out if return_sum else out[0]
     h = x + residual if residual is not None else x
     y = F.layer_norm(h, (h.shape[-1],), weight, bias, eps)
     return (y, h) if return_sum else y

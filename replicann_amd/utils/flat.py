@@ -69,6 +69,9 @@ class FlatParams:
 
     def zero_grad(self):
         self.grad.zero_()
+        for p in self.params:  # multi-use parameters restart their contribution count
+            if hasattr(p, "_rn_pending"):
+                del p._rn_pending
         # autograd may have replaced a .grad (e.g. set_to_none elsewhere): re-point
         for p, o in zip(self.params, self.offsets):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:o + 1].data_ptr():

@@ -119,6 +119,43 @@ def test_layernorm(cuda, E):
         assert rel_err(t.grad, tf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("M,E", [(37, 768), (5000, 96), (16384, 768), (300, 4096)])
+def test_layernorm_passthrough_producer_bias(cuda, M, E):
+    """Pre-LN block form: (y, x) = LN(x) with x also the residual; the kernel fuses the
+    residual-gradient add and reduces Σ_rows dx into the producer's bias grad."""
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(5)
+    mod = torch.nn.Module()
+    mod.w = torch.nn.Parameter(torch.randn(E, device="cuda").bfloat16())
+    mod.b = torch.nn.Parameter(torch.randn(E, device="cuda").bfloat16())
+    mod.pb = torch.nn.Parameter(torch.zeros(E, device="cuda").bfloat16())
+    flat = FlatParams(mod)
+    flat.zero_grad()
+    x = bf(M, E).requires_grad_()
+    gy, gr = bf(M, E), bf(M, E)
+    y, xp = ops.layer_norm(x, mod.w, mod.b, 1e-5, return_sum=True, producer_bias=mod.pb)
+    ((y.float() * gy.float()).sum() + (xp.float() * gr.float()).sum()).backward()
+    assert mod.pb._rn_ln_done
+    xf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, mod.w, mod.b)]
+    yf = F.layer_norm(xf, (E,), wf, bf_, 1e-5)
+    ((yf * gy.float()).sum() + (xf * gr.float()).sum()).backward()
+    assert rel_err(y, yf) < 1e-2
+    assert rel_err(x.grad, xf.grad) < 2e-2
+    assert rel_err(mod.w.grad, wf.grad) < 2e-2 and rel_err(mod.b.grad, bf_.grad) < 2e-2
+    assert rel_err(mod.pb.grad, x.grad.float().sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("C", [64, 200, 2304, 50304])
+def test_bias_grad_column_reduction(cuda, C):
+    """Single-launch deterministic column sums (last-block reduction) — also bitwise repeatable."""
+    torch.manual_seed(6)
+    dy = bf(3000, C)
+    _, db1 = torch.ops.replicann.bias_act_grad(dy, None, 0, True, None)
+    _, db2 = torch.ops.replicann.bias_act_grad(dy, None, 0, True, None)
+    assert rel_err(db1, dy.float().sum(0)) < 1e-2
+    assert torch.equal(db1, db2)
+
+
 # ----------------------------------------------------------------- cross entropy
 def test_cross_entropy_padded(cuda):
     torch.manual_seed(5)
