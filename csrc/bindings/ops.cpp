@@ -41,8 +41,8 @@ void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
 void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
 void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int, hipStream_t);
 void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
-void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, hipStream_t);
-void rn_emb_bwd_acc(const int64_t*, const void*, float*, unsigned*, void*, void*, int, int, int, hipStream_t);
+void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, int, hipStream_t);
+void rn_emb_bwd_acc(const int64_t*, const void*, float*, unsigned*, void*, void*, int, int, int, int, hipStream_t);
 void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
 int rn_norm_ws_floats();
 void rn_sumsq(const void*, long, int, float*, float*, hipStream_t);
@@ -162,6 +162,10 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         CHECK_BF16(*preact);
         TORCH_CHECK(preact->size(0) == M && preact->size(1) == N && preact->stride(0) == c.stride(0));
     }
+    const bool act_bwd = act == 3 || act == 4;  // fused activation backward: out = (A·B) ⊙ act'(preact)
+    if (act_bwd)
+        TORCH_CHECK(!ta && !tb && N % 8 == 0 && preact && preact->defined() && !accumulate && !(bias && bias->defined()),
+                    "activation-backward epilogue: dgrad layout (A·B, B [K][N]), N % 8 == 0, preact required");
     if (M == 0 || N == 0) return c;
     int split = split_k < 0 ? -1 : (int)std::max<int64_t>(1, split_k);
     Tensor ws;
@@ -214,7 +218,9 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                     const int sp = splits[si];
                     if (sp > 1 && Kp / sp < 256) break;
                     auto run = [&]() {
-                        return rn_gemm(A.data_ptr(), B.data_ptr(), scratch.data_ptr(), optr(bias), optr(residual), nullptr,
+                        // fwd activations: skip the pre-activation store while timing; bwd ones read it
+                        return rn_gemm(A.data_ptr(), B.data_ptr(), scratch.data_ptr(), optr(bias), optr(residual),
+                                       act_bwd ? preact->data_ptr() : nullptr,
                                        tws.data_ptr<float>(), alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr,
                                        (int)M, (int)N, (int)Kp, A.stride(0), B.stride(0), scratch.stride(0), ta, tb, (int)act,
                                        sp, out_fp32, 0, cfgs[ci], cur_stream());
@@ -386,7 +392,9 @@ Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const optional<Tensor
     auto shape = ids.sizes().vec();
     shape.push_back(E);
     Tensor x = at::empty(shape, wte.options());
-    if (rows) rn_emb_fwd(ids.data_ptr<int64_t>(), wte.data_ptr(), optr(wpe), x.data_ptr(), rows, T, E, cur_stream());
+    if (rows)
+        rn_emb_fwd(ids.data_ptr<int64_t>(), wte.data_ptr(), optr(wpe), x.data_ptr(), rows, T, E, (int)wte.size(0),
+                   cur_stream());
     return x;
 }
 std::tuple<Tensor, Tensor> embedding_bwd(const Tensor& dx, const Tensor& ids, int64_t V, int64_t Tp) {
@@ -437,7 +445,7 @@ void embedding_bwd_acc(const Tensor& dx, const Tensor& ids, const Tensor& gwte, 
     if (ids.numel())
         rn_emb_bwd_acc(ids.data_ptr<int64_t>(), dx.data_ptr(), buf.first.data_ptr<float>(),
                        reinterpret_cast<unsigned*>(buf.second.data_ptr<int>()), gwte.data_ptr(),
-                       (gwpe && gwpe->defined()) ? gwpe->data_ptr() : nullptr, B, T, (int)E, cur_stream());
+                       (gwpe && gwpe->defined()) ? gwpe->data_ptr() : nullptr, B, T, (int)E, (int)V, cur_stream());
 }
 
 // ------------------------------------------------------------------ optimizers

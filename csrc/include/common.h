@@ -19,6 +19,15 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 #define RN_WAVE 64
 #define RN_DEV __device__ __forceinline__
 
+// Debug build (REPLICANN_CHECK=1 python -m replicann_amd._build): device-side
+// bounds checks on data-dependent indices (token ids, targets) trap the wave
+// instead of reading/writing out of bounds.  Compiled out otherwise.
+#ifdef REPLICANN_CHECK
+#define RN_CHECK(c) do { if (!(c)) __builtin_trap(); } while (0)
+#else
+#define RN_CHECK(c) do { } while (0)
+#endif
+
 RN_DEV float bf2f(bf16 x) { return (float)x; }
 RN_DEV bf16 f2bf(float x) { return (bf16)x; }
 
@@ -94,7 +103,11 @@ RN_DEV float gelu_grad_f(float x) {
     return s + 2.f * x * s * (1.f - s) * c * (1.f + 0.134145f * x2);
 }
 
-enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU_BWD = 3, ACT_GELU_BWD = 4 };
+// *_BWD (GEMM epilogue only): out = acc · act'(aux) with aux = the saved pre-activation,
+// i.e. the activation backward fused into the dgrad GEMM that produces dY·W.
+constexpr bool act_fwd(int a) { return a == ACT_RELU || a == ACT_GELU; }
+constexpr bool act_bwd(int a) { return a == ACT_RELU_BWD || a == ACT_GELU_BWD; }
 
 template <int ACT>
 RN_DEV float act_f(float x) {
@@ -104,8 +117,8 @@ RN_DEV float act_f(float x) {
 }
 template <int ACT>
 RN_DEV float act_grad_f(float x) {
-    if constexpr (ACT == ACT_RELU) return x > 0.f ? 1.f : 0.f;
-    else if constexpr (ACT == ACT_GELU) return gelu_grad_f(x);
+    if constexpr (ACT == ACT_RELU || ACT == ACT_RELU_BWD) return x > 0.f ? 1.f : 0.f;
+    else if constexpr (ACT == ACT_GELU || ACT == ACT_GELU_BWD) return gelu_grad_f(x);
     else return 1.f;
 }
 

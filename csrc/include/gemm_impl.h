@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
             constexpr int STRIDE = BN * 2 + 16;
             constexpr int CPR = BN / 8;  // 16-B chunks per tile row
             const int mlim = min(BM, p.M - m0), nlim = min(BN, p.N - n0);
-            for (int pass = (ACT != ACT_NONE && p.pre) ? 0 : 1; pass < 2; ++pass) {
+            for (int pass = (act_fwd(ACT) && p.pre) ? 0 : 1; pass < 2; ++pass) {
                 __syncthreads();  // main-loop LDS reads (or the previous pass's reads) retired
 #pragma unroll
                 for (int i = 0; i < FM; ++i) {
@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
 #pragma unroll
                             for (int t = 0; t < 4; ++t) v[t] += (float)b[t];
                         }
-                        if constexpr (ACT != ACT_NONE) {
+                        if constexpr (act_fwd(ACT)) {
                             if (pass == 1) {
 #pragma unroll
                                 for (int t = 0; t < 4; ++t) v[t] = act_f<ACT>(v[t]);
@@ -337,10 +337,16 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                     if (r >= mlim || cc * 8 >= nlim) continue;
                     s16x8 v = *reinterpret_cast<const s16x8*>(smem + r * STRIDE + cc * 16);
                     const long goff = (long)(m0 + r) * p.ldc + n0 + cc * 8;
-                    if (addres || accum) {
+                    if (addres || accum || act_bwd(ACT)) {
                         float f[8];
 #pragma unroll
                         for (int t = 0; t < 8; ++t) f[t] = (float)__builtin_bit_cast(bf16, (short)v[t]);
+                        if constexpr (act_bwd(ACT)) {  // dH = (dY·W) ⊙ act'(pre), pre read row-coalesced
+                            float aux[8];
+                            load8(p.pre + goff, aux);
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) f[t] = (float)(bf16)f[t] * act_grad_f<ACT>(aux[t]);
+                        }
                         if (addres) {
                             float rr[8];
                             load8(p.res + goff, rr);
@@ -387,7 +393,13 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                         for (int t = 0; t < 4; ++t) v[t] += (float)b[t];
                     } else for (int t = 0; t < 4 && n + t < p.N; ++t) v[t] += (float)p.bias[n + t];
                 }
-                if constexpr (ACT != ACT_NONE) {
+                if constexpr (act_bwd(ACT)) {
+                    const bf16* pp = p.pre + (long)m * p.ldc + n;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (n + t < p.N) v[t] = (float)(bf16)v[t] * act_grad_f<ACT>((float)pp[t]);
+                }
+                if constexpr (act_fwd(ACT)) {
                     if (p.pre) {
                         bf16* pp = p.pre + (long)m * p.ldc + n;
                         if (full) {
@@ -450,10 +462,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
             const int m = e / p.N, n = e % p.N;
             float x = v[t];
             if (p.bias) x += (float)p.bias[n];
-            if constexpr (ACT != ACT_NONE) {
+            if constexpr (act_fwd(ACT)) {
                 if (p.pre) p.pre[(long)m * p.ldc + n] = (bf16)x;
                 x = act_f<ACT>(x);
             }
+            if constexpr (act_bwd(ACT)) x = (float)(bf16)x * act_grad_f<ACT>((float)p.pre[(long)m * p.ldc + n]);
             if (p.res) x += (float)p.res[(long)m * p.ldc + n];
             if (p.out_f32) {
                 float* cp = (float*)p.C + (long)m * p.ldc + n;
@@ -498,7 +511,11 @@ void launch_cfg(GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
     else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_RELU>(a, st);          \
     else launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_NONE>(a, st);
     if (ak && bk) { RN_L(true, true) }
-    else if (ak && !bk) { RN_L(true, false) }
+    else if (ak && !bk) {  // dgrad layout: also the fused activation-backward epilogues
+        if (act == ACT_GELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_GELU_BWD>(a, st);
+        else if (act == ACT_RELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_RELU_BWD>(a, st);
+        else { RN_L(true, false) }
+    }
     else if (!ak && bk) { RN_L(false, true) }
     else { RN_L(false, false) }
 #undef RN_L

@@ -7,11 +7,12 @@ namespace {
 template <bool POS>
 __global__ void __launch_bounds__(256) emb_fwd_k(const int64_t* __restrict__ ids, const bf16* __restrict__ wte,
                                                  const bf16* __restrict__ wpe, bf16* __restrict__ x, int rows,
-                                                 int T, int E) {
+                                                 int T, int E, int V) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
     const long id = ids[row];
+    RN_CHECK(id >= 0 && id < V);
     const int t = row % T;
     for (int c = lane; c < E / 8; c += 64) {
         float a[8];
@@ -45,11 +46,12 @@ __global__ void __launch_bounds__(256) emb_bwd_scatter_k(const int64_t* __restri
 // scratch row and re-arms owner — only touched rows are visited.
 __global__ void __launch_bounds__(256) emb_scatter_own_k(const int64_t* __restrict__ ids,
                                                          const bf16* __restrict__ dx, float* __restrict__ d32,
-                                                         unsigned* __restrict__ owner, int rows, int E) {
+                                                         unsigned* __restrict__ owner, int rows, int E, int V) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
     const long id = ids[row];
+    RN_CHECK(id >= 0 && id < V);
     if (lane == 0) atomicMin(owner + id, (unsigned)row);
     for (int c = lane; c < E; c += 64) atomicAdd(d32 + id * E + c, bf2f(dx[(long)row * E + c]));
 }
@@ -253,11 +255,11 @@ inline int grid_for(long work) {
 
 extern "C" {
 
-void rn_emb_fwd(const int64_t* ids, const void* wte, const void* wpe, void* x, int rows, int T, int E,
+void rn_emb_fwd(const int64_t* ids, const void* wte, const void* wpe, void* x, int rows, int T, int E, int V,
                 hipStream_t st) {
     dim3 g((rows + 3) / 4);
-    if (wpe) emb_fwd_k<true><<<g, 256, 0, st>>>(ids, (const bf16*)wte, (const bf16*)wpe, (bf16*)x, rows, T, E);
-    else emb_fwd_k<false><<<g, 256, 0, st>>>(ids, (const bf16*)wte, nullptr, (bf16*)x, rows, T, E);
+    if (wpe) emb_fwd_k<true><<<g, 256, 0, st>>>(ids, (const bf16*)wte, (const bf16*)wpe, (bf16*)x, rows, T, E, V);
+    else emb_fwd_k<false><<<g, 256, 0, st>>>(ids, (const bf16*)wte, nullptr, (bf16*)x, rows, T, E, V);
 }
 
 // dwte32: V*E fp32 scratch (zeroed here); dwte: bf16 out; dwpe: bf16 (Tp*E) or null
@@ -273,9 +275,9 @@ void rn_emb_bwd(const int64_t* ids, const void* dx, float* dwte32, void* dwte, v
 
 // E % 4 == 0.  gwte (bf16 V×E) and gwpe (bf16 ≥T×E, may be null) are accumulated into.
 void rn_emb_bwd_acc(const int64_t* ids, const void* dx, float* d32, unsigned* owner, void* gwte, void* gwpe, int B,
-                    int T, int E, hipStream_t st) {
+                    int T, int E, int V, hipStream_t st) {
     const int rows = B * T;
-    emb_scatter_own_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (const bf16*)dx, d32, owner, rows, E);
+    emb_scatter_own_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (const bf16*)dx, d32, owner, rows, E, V);
     emb_finish_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, d32, owner, (bf16*)gwte, rows, E);
     if (gwpe) emb_pos_acc_k<<<rn_cdiv((long)T * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)gwpe, B, T, E);
 }

@@ -106,6 +106,7 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
             int split, int out_f32, int accumulate, int cfg, hipStream_t st) {
     if (K % 8 != 0) return -1;
+    if (act_bwd(act) && (trans_a || trans_b || !pre)) return -1;  // fused act-backward: dgrad layout only
     if (trans_a && (M % 8 != 0 || lda % 8 != 0)) return -1;
     if (!trans_a && lda % 8 != 0) return -1;
     if (!trans_b && (N % 8 != 0 || ldb % 8 != 0)) return -1;

@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, co
     const int n8 = V / 8;
     const long t = tgt[blockIdx.x];
     const bool ign = (t == ignore || t < 0 || t >= nvalid);
+    RN_CHECK(t == ignore || (t >= 0 && t < nvalid));
     const float xt = ign ? 0.f : bf2f(row[t]);
     bf16x8 v[CH];
     float m = -INFINITY;

@@ -37,6 +37,8 @@ HIP_FLAGS = [
     "-munsafe-fp-atomics",
     "-Wno-unused-result",
 ]
+if os.environ.get("REPLICANN_CHECK", "0") == "1":  # debug build: device bounds checks (RN_CHECK)
+    HIP_FLAGS.append("-DREPLICANN_CHECK=1")
 
 
 def _torch_paths():

@@ -93,10 +93,14 @@ class MLP(nn.Module):
         return self.c_proj.bias if not (self.dropout > 0 and self.training) else None
 
     def forward(self, h, residual):
-        u = self.c_fc(h, act="gelu")
         if self.dropout > 0 and self.training:
+            u = self.c_fc(h, act="gelu")
             return residual + ops.dropout(self.c_proj(u), self.dropout, True)
-        return self.c_proj(u, residual=residual)
+        if self.c_fc.fp8 or self.c_proj.fp8:
+            return self.c_proj(self.c_fc(h, act="gelu"), residual=residual)
+        # one autograd node: GELU backward fused into the c_proj dgrad GEMM epilogue
+        return ops.mlp(h, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias, "gelu",
+                       residual=residual)
 
 
 class PreLNBlock(nn.Module):

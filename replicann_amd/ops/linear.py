@@ -202,3 +202,78 @@ def linear(x, weight, bias=None, act=None, residual=None):
     if not x.is_cuda and not torch.is_grad_enabled() and residual is None and a == ACT_NONE:
         return F.linear(x, weight, bias)
     return _LinearFn.apply(x, weight, bias, a, residual)
+
+
+# --------------------------------------------------------------------------
+# fused two-layer MLP: y = act(x·W1ᵀ + b1)·W2ᵀ + b2 (+ residual)
+# --------------------------------------------------------------------------
+ACT_BWD = {ACT_RELU: 3, ACT_GELU: 4}  # GEMM epilogue codes: out = (A·B) ⊙ act'(pre)
+
+
+def _bias_grad(g2, bias, native):
+    """Σ_rows g2 into ``bias``'s gradient: (returned grad or None, done_direct)."""
+    if bias is None or not bias.requires_grad:
+        return None
+    if getattr(bias, "_rn_ln_done", False):  # reduced by the downstream LayerNorm backward
+        bias._rn_ln_done = False
+        return None
+    acc = _direct_grad(bias) if native else None
+    if native:
+        _, db = _ext.ops().bias_act_grad(g2, None, ACT_NONE, True, acc)
+    else:
+        db = g2.float().sum(0)
+    if acc is not None:
+        _notify(bias)
+        return None
+    return db.to(bias.dtype)
+
+
+def _wgrad(g2, x2, weight, native):
+    acc = _direct_grad(weight) if native else None
+    if acc is not None:
+        gemm(g2, x2, ta=True, split_k=-1, out=acc, accumulate=True)
+        _notify(weight)
+        return None
+    return gemm(g2, x2, ta=True, split_k=-1, out_dtype=weight.dtype)
+
+
+class _MLPFn(torch.autograd.Function):
+    """One autograd node for the whole MLP so the activation backward runs in the
+    epilogue of the second layer's dgrad GEMM:  dH = (dY·W2) ⊙ act'(pre)  — the
+    separate activation-backward pass over dU (read dU + pre, write dH) is gone."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, act, residual):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).contiguous()
+        res2 = residual.reshape(-1, w2.shape[0]).contiguous() if residual is not None else None
+        ops = _ext.ops()
+        pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
+        u = ops.gemm(x2, w1, False, True, b1, None, act, pre, None, False, 0, False, None, -1)
+        y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)
+        ctx.save_for_backward(x2, w1, pre, u, w2)
+        ctx.b1, ctx.b2, ctx.act, ctx.shp, ctx.has_res = b1, b2, act, shp, residual is not None
+        return y.reshape(*shp[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w1, pre, u, w2 = ctx.saved_tensors
+        ops = _ext.ops()
+        gy2 = gy.reshape(-1, w2.shape[0]).contiguous()
+        nig = ctx.needs_input_grad
+        gw2 = _wgrad(gy2, u, w2, True) if nig[3] else None
+        gb2 = _bias_grad(gy2, ctx.b2, True) if nig[4] else None
+        dh = ops.gemm(gy2, w2, False, False, None, None, ACT_BWD[ctx.act], pre, None, False, 0, False, None, -1)
+        gb1 = _bias_grad(dh, ctx.b1, True) if nig[2] else None
+        gw1 = _wgrad(dh, x2, w1, True) if nig[1] else None
+        gx = ops.gemm(dh, w1, False, False, None, None, ACT_NONE, None, None, False, 0, False, None, -1)
+        return (gx.reshape(ctx.shp) if nig[0] else None, gw1, gb1, gw2, gb2, None,
+                gy if ctx.has_res else None)
+
+
+def mlp(x, w1, b1, w2, b2, act="gelu", residual=None):
+    """act(x·W1ᵀ + b1)·W2ᵀ + b2 [+ residual] — fused backward on GPU, plain linears on CPU."""
+    a = _ACTS[act] if not isinstance(act, int) else act
+    if _ext.use_native(x) and a in ACT_BWD:
+        return _MLPFn.apply(x, w1, b1, w2, b2, a, residual)
+    return linear(linear(x, w1, b1, act=a), w2, b2, residual=residual)

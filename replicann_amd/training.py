@@ -140,6 +140,19 @@ class Trainer:
     def samples_per_step(self):
         return self.cfg.batch_size * self.cfg.grad_accum * self.world
 
+    def _throughput(self, steps, dt):
+        """samples/s (+ tokens/s and model-FLOPs utilisation vs the bf16 dense peak for LMs)."""
+        from .utils.metrics import BF16_PEAK_FLOPS
+        sps = self.samples_per_step() * steps / max(dt, 1e-9)
+        out = {"samples_per_s": round(sps, 2)}
+        if self.kind == "lm":
+            tps = sps * self.cfg.seq_len
+            out["tokens_per_s"] = round(tps, 1)
+            fpt = getattr(self.model, "flops_per_token", None)
+            if fpt is not None:
+                out["mfu"] = round(tps * fpt(self.cfg.seq_len) / (BF16_PEAK_FLOPS * self.world), 4)
+        return out
+
     def _step_body(self, batches, lr=None):
         c = self.cfg
         self.opt.zero_grad()
@@ -240,7 +253,7 @@ class Trainer:
                 lv = float(loss)
                 dt = time.time() - t0
                 self.logger.log(step=i, loss=round(lv, 5), lr=round(float(self.opt._host_lr(None)), 8),
-                                samples_per_s=round(self.samples_per_step() * (i - start) / max(dt, 1e-9), 2))
+                                **self._throughput(i - start, dt))
                 last = lv
         if c.checkpoint:
             save_checkpoint(c.checkpoint, self.model, self.opt, c.steps, asdict(c))

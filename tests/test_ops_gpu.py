@@ -100,6 +100,41 @@ def test_linear_autograd(cuda):
         assert rel_err(t.grad, tf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("act", [3, 4])
+@pytest.mark.parametrize("cfg,split", [(0, 0), (1, 0), (6, 0), (2, 0), (0, 4), (-1, 0)])
+def test_gemm_act_backward_epilogue(cuda, act, cfg, split):
+    """dH = (dY·W) ⊙ act'(pre) fused into the dgrad GEMM epilogue (3 = ReLU', 4 = GELU')."""
+    torch.manual_seed(7)
+    M, N, K = 520, 776, 384
+    dy, w, pre = bf(M, K), bf(K, N, scale=0.1), bf(M, N)
+    out = torch.ops.replicann.gemm(dy, w, False, False, None, None, act, pre, None, False, split, False, None, cfg)
+    du = (dy.float() @ w.float()).bfloat16().float()
+    pf = pre.float().requires_grad_()
+    y = F.relu(pf) if act == 3 else F.gelu(pf, approximate="tanh")
+    (g,) = torch.autograd.grad(y, pf, du)
+    assert rel_err(out, g) < 1e-2
+
+
+def test_mlp_fused_matches_unfused(cuda):
+    torch.manual_seed(8)
+    E, H, M = 256, 1024, 300
+    x = bf(M, E).requires_grad_()
+    r = bf(M, E).requires_grad_()
+    w1, b1 = bf(H, E, scale=0.05).requires_grad_(), bf(H, scale=0.1).requires_grad_()
+    w2, b2 = bf(E, H, scale=0.05).requires_grad_(), bf(E, scale=0.1).requires_grad_()
+    g = bf(M, E)
+    y = ops.mlp(x, w1, b1, w2, b2, "gelu", residual=r)
+    y.backward(g)
+    got = [t.grad.clone() for t in (x, r, w1, b1, w2, b2)]
+    ts = [t.detach().float().requires_grad_() for t in (x, r, w1, b1, w2, b2)]
+    xf, rf, w1f, b1f, w2f, b2f = ts
+    yf = F.linear(F.gelu(F.linear(xf, w1f, b1f), approximate="tanh"), w2f, b2f) + rf
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2
+    for a, t in zip(got, ts):
+        assert rel_err(a, t.grad) < 2e-2
+
+
 # ----------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("E", [768, 1024, 96])
 def test_layernorm(cuda, E):
