@@ -99,9 +99,10 @@ const void* optr(const optional<Tensor>& t) { return (t && t->defined()) ? t->da
 // cache, or the native cost model.  REPLICANN_GEMM_AUTOTUNE=0 disables tuning.
 struct TuneKey {
     int64_t M, N, K;
-    int ta, tb, act, f32, autosplit;
+    int ta, tb, act, f32, autosplit, epi;  // epi: bias | residual<<1 | alpha<<2 | accumulate<<3
     bool operator<(const TuneKey& o) const {
-        return std::tie(M, N, K, ta, tb, act, f32, autosplit) < std::tie(o.M, o.N, o.K, o.ta, o.tb, o.act, o.f32, o.autosplit);
+        return std::tie(M, N, K, ta, tb, act, f32, autosplit, epi) <
+               std::tie(o.M, o.N, o.K, o.ta, o.tb, o.act, o.f32, o.autosplit, o.epi);
     }
 };
 static std::map<TuneKey, std::pair<int, int>> g_tune;
@@ -124,12 +125,22 @@ std::string gemm_tuning_table() {
     for (auto& kv : g_tune) {
         const TuneKey& k = kv.first;
         os << (first ? "" : ",") << "{\"M\":" << k.M << ",\"N\":" << k.N << ",\"K\":" << k.K << ",\"ta\":" << k.ta
-           << ",\"tb\":" << k.tb << ",\"act\":" << k.act << ",\"cfg\":" << kv.second.first << ",\"split\":"
+           << ",\"tb\":" << k.tb << ",\"act\":" << k.act << ",\"epi\":" << k.epi << ",\"cfg\":" << kv.second.first
+           << ",\"split\":"
            << kv.second.second << "}";
         first = false;
     }
     os << "]";
     return os.str();
+}
+
+// "cfg 7": the vendor library (hipBLASLt through at::mm) for PLAIN GEMMs only — no
+// epilogue (bias / activation / residual / accumulate / alpha), bf16 out.  It is one
+// more candidate the autotuner times per shape, never a fallback: fused GEMMs always
+// run on the MFMA kernels above.
+constexpr int kLibCfg = 7;
+static void lib_gemm(const Tensor& A, const Tensor& B, bool ta, bool tb, Tensor& c) {
+    at::mm_out(c, ta ? A.t() : A, tb ? B.t() : B);
 }
 
 Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<Tensor>& bias,
@@ -193,7 +204,9 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     if (c.stride(0) % 4 != 0 && (bias || residual)) { /* epilogue handles unaligned via scalar path */ }
     if (alpha && alpha->defined()) TORCH_CHECK(alpha->scalar_type() == at::kFloat && alpha->is_cuda());
     if (cfg < 0 && split_k <= 0) {
-        const TuneKey key{M, N, Kp, (int)ta, (int)tb, (int)act, (int)out_fp32, split_k < 0 ? 1 : 0};
+        const int epi = (bias && bias->defined() ? 1 : 0) | (residual && residual->defined() ? 2 : 0) |
+                        (alpha && alpha->defined() ? 4 : 0) | (accumulate ? 8 : 0);
+        const TuneKey key{M, N, Kp, (int)ta, (int)tb, (int)act, (int)out_fp32, split_k < 0 ? 1 : 0, epi};
         bool hit = false;
         {
             std::lock_guard<std::mutex> lk(g_tune_mu);
@@ -204,7 +217,10 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         (void)hipStreamIsCapturing(cur_stream(), &cap);
         if (!hit && autotune_enabled() && cap == hipStreamCaptureStatusNone) {
             Tensor scratch = at::empty({M, N}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
-            const int cfgs[4] = {0, 1, 6, 2};
+            const bool plain = !(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
+                               !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
+            const int ncfg = plain ? 5 : 4;
+            const int cfgs[5] = {0, 1, 6, 2, kLibCfg};
             const int splits[5] = {1, 2, 4, 8, 16};
             const int nsplit = split_k < 0 ? 5 : 1;
             Tensor tws = at::empty({rn_gemm_ws_floats(M, N, 16)}, a.options().dtype(at::kFloat));
@@ -213,11 +229,13 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             (void)hipEventCreate(&e1);
             float best_ms = 1e30f;
             int best_cfg = 0, best_split = 1;
-            for (int ci = 0; ci < 4; ++ci) {
+            for (int ci = 0; ci < ncfg; ++ci) {
                 for (int si = 0; si < nsplit; ++si) {
                     const int sp = splits[si];
                     if (sp > 1 && Kp / sp < 256) break;
+                    if (cfgs[ci] == kLibCfg && sp > 1) break;
                     auto run = [&]() {
+                        if (cfgs[ci] == kLibCfg) { lib_gemm(A, B, ta, tb, scratch); return 0; }
                         // fwd activations: skip the pre-activation store while timing; bwd ones read it
                         return rn_gemm(A.data_ptr(), B.data_ptr(), scratch.data_ptr(), optr(bias), optr(residual),
                                        act_bwd ? preact->data_ptr() : nullptr,
@@ -248,6 +266,13 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             split = best_split;
         }
         if (split > 1 && max_split < split) ws = at::empty({rn_gemm_ws_floats(M, N, split)}, a.options().dtype(at::kFloat));
+    }
+    if (cfg == kLibCfg) {
+        TORCH_CHECK(!(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
+                        !(alpha && alpha->defined()) && !out_fp32 && !accumulate,
+                    "gemm cfg 7 (library) is for plain GEMMs only");
+        lib_gemm(A, B, ta, tb, c);
+        return c;
     }
     const int ws_split = split > 1 ? split : max_split;
     if (ws_split > 1 && !ws.defined()) ws = at::empty({rn_gemm_ws_floats(M, N, ws_split)}, a.options().dtype(at::kFloat));

@@ -27,6 +27,8 @@
 // head sizes): straightforward per-query-row kernels with fp32 scores in LDS.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -114,6 +116,66 @@ RN_DEV uint64_t drop_idx(const AttnArgs& p, int b, int h, int qi, int kj) {
 
 // ============================== forward, D = 64 ==============================
 // grid: (ceil(Tq/128), B*H); 4 waves x 32 query rows.
+// LDS-DMA issued through inline asm: the compiler then does not know a DMA is in
+// flight, so it does not drain it (s_waitcnt vmcnt(0)) in front of every LDS read
+// of the OTHER buffer — hipcc (ROCm 7.2) cannot tell the two buffers apart.  The
+// hand-off is explicit instead: `s_waitcnt vmcnt(0)` + barrier at the top of each
+// tile.  M0 (the DMA's LDS base) is written here; nothing else in these kernels
+// uses it.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+RN_DEV u32x4 make_rsrc_sgpr(const void* base, uint32_t bytes = 0x7FFFFFF0u) {
+    const uint64_t bp = (uint64_t)base;
+    u32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    r[2] = __builtin_amdgcn_readfirstlane(bytes);  // range-checked: dwords past it read as 0
+    r[3] = 0x00020000u;
+    return r;
+}
+
+RN_DEV uint32_t lds_addr(const char* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)p);
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is "reserved": declaring the clobber is still right
+RN_DEV void dma16_async(const u32x4& rs, uint32_t voff, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// stage64 with compiler-invisible DMA (2 instructions per wave).
+RN_DEV void stage64_async(const u32x4& rs, long st, int r0, int rlim, const char* lds, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ins = wave * 2 + i;
+        const int r = ins * 8 + (lane >> 3);
+        const int cg = (lane & 7) ^ swz(r);
+        const bool ok = (r0 + r) < rlim;
+        const uint32_t voff = ok ? (uint32_t)((((long)(r0 + r)) * st + cg * 8) * 2) : 0xFFFFFFF0u;
+        dma16_async(rs, voff, lds_addr(lds + ins * 1024));
+    }
+}
+
+RN_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// max over lanes {l, l^16, l^32, l^48} (the 4 lane groups holding one softmax row)
+// with the gfx950 permlane swaps (VALU) instead of two ds_bpermute round trips.
+RN_DEV float max4groups(float x) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+RN_DEV float sum4groups(float x) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 template <bool CAUSAL, bool BIAS, bool DROP>
 __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -128,8 +190,18 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     const float xs = BIAS ? 1.f : sl2;  // units of the running max m: log2-scaled with bias, raw without
 
     const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
-    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
-    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
+    const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + h * p.k_sh);
+    const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
+
+    int kv_end = p.Tk;
+    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
+#define Kt(i) (smem + (i) * 16384)
+#define Vt(i) (smem + 8192 + (i) * 16384)
+    if (nkv > 0) {  // first tile in flight while Q is loaded
+        stage64_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+    }
 
     s16x8 qf[2][2];
 #pragma unroll
@@ -139,6 +211,10 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
             const int row = q0 + qi * 16 + c;
             qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
         }
+    // Re-define qf through an (empty) asm so the compiler's wait for these loads happens
+    // here, once: otherwise it re-waits vmcnt(0) inside the loop at their first use,
+    // which would also drain the in-flight K/V prefetch.
+    asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]));
     float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
     f32x4 oacc[2][4];
 #pragma unroll
@@ -146,22 +222,14 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
 #pragma unroll
         for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    int kv_end = p.Tk;
-    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
-    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
-#define Kt(i) (smem + (i) * 16384)
-#define Vt(i) (smem + 8192 + (i) * 16384)
-    if (nkv > 0) {
-        stage64(kbase, p.k_st, 0, p.Tk, Kt(0), wave, lane);
-        stage64(vbase, p.v_st, 0, p.Tk, Vt(0), wave, lane);
-    }
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     for (int t = 0; t < nkv; ++t) {
-        __syncthreads();
+        vm_wait_all();   // this wave's DMA of tile t landed ...
+        __syncthreads(); // ... and every wave's; every wave also finished tile t-1 (its buffer is free)
         const int cur = t & 1;
         if (t + 1 < nkv) {
-            stage64(kbase, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
-            stage64(vbase, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
+            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
+            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
         }
         const int kv0 = t * 64;
         // wave-uniform skip: this wave's queries all precede the tile
@@ -180,16 +248,14 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
                 sacc[qi][j] = MFMA(a1, qf[qi][1], z, 0, 0, 0);
             }
         }
-        const bool need_mask = (kv0 + 64 > p.Tk) || (CAUSAL && kv0 + 63 > q0 + off);
+        if constexpr (BIAS) {  // x = s·scale·log2e + bias·log2e
 #pragma unroll
-        for (int qi = 0; qi < 2; ++qi) {
-            const int qg = q0 + qi * 16 + c;
-            float tmax = -INFINITY;
+            for (int qi = 0; qi < 2; ++qi) {
+                const int qg = q0 + qi * 16 + c;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float bb[4] = {0.f, 0.f, 0.f, 0.f};
-                const int kvb = kv0 + j * 16 + 4 * g;
-                if constexpr (BIAS) {
+                for (int j = 0; j < 4; ++j) {
+                    const int kvb = kv0 + j * 16 + 4 * g;
+                    float bb[4] = {0.f, 0.f, 0.f, 0.f};
                     if (qg < p.Tq) {
                         const float* bp = p.bias + ((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvb;
                         if (kvb + 3 < p.Tk && (p.Tk & 3) == 0) {
@@ -199,21 +265,36 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
                             for (int r = 0; r < 4; ++r) bb[r] = (kvb + r < p.Tk) ? bp[r] : 0.f;
                         }
                     }
-                }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    // no bias: keep raw scores (the scale folds into the exp's FMA below)
-                    float x = BIAS ? sacc[qi][j][r] * sl2 + bb[r] * LOG2E : sacc[qi][j][r];
-                    if (need_mask) {
-                        const int kvj = kvb + r;
-                        if (kvj >= p.Tk || (CAUSAL && kvj > qg + off)) x = -INFINITY;
-                    }
-                    sacc[qi][j][r] = x;
-                    tmax = fmaxf(tmax, x);
+                    for (int r = 0; r < 4; ++r) sacc[qi][j][r] = sacc[qi][j][r] * sl2 + bb[r] * LOG2E;
                 }
             }
-            tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        }
+        // masking only on diagonal / ragged tiles: a real (wave-uniform) branch — the
+        // empty asm keeps hipcc from if-converting it into per-element selects on
+        // every tile
+        if ((kv0 + 64 > p.Tk) || (CAUSAL && kv0 + 63 > q0 + off)) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) {
+                const int qg = q0 + qi * 16 + c;
+                const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (kv0 + j * 16 + 4 * g + r > lim) sacc[qi][j][r] = -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) {
+            const int qg = q0 + qi * 16 + c;
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sacc[qi][j][r]);
+            tmax = max4groups(tmax);
             const float mn = fmaxf(m[qi], tmax);
             const float ms = (mn == -INFINITY) ? 0.f : mn;  // fully-masked rows stay at p = 0
             const float alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m[qi] - ms) * xs);
@@ -250,13 +331,13 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
             }
         }
     }
+#undef Kt
+#undef Vt
     // epilogue
     bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
-        float lt = l[qi];
-        lt += __shfl_xor(lt, 16, 64);
-        lt += __shfl_xor(lt, 32, 64);
+        const float lt = sum4groups(l[qi]);
         const int qg = q0 + qi * 16 + c;
         const float inv = lt > 0.f ? 1.f / lt : 0.f;
         if (qg < p.Tq) {
@@ -295,7 +376,7 @@ __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
 
 // dK, dV: grid (ceil(Tk/64), B*H); wave w owns keys kv0 + 16w + (lane&15)
 template <bool CAUSAL, bool BIAS, bool DROP>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
+__global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -306,12 +387,32 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
 
-    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
-    const bf16* dobase = p.dout + b * p.do_sb + h * p.do_sh;
+    const u32x4 qrs = make_rsrc_sgpr(p.q + b * p.q_sb + h * p.q_sh);
+    const u32x4 ors = make_rsrc_sgpr(p.dout + b * p.do_sb + h * p.do_sh);
+    // per-row softmax statistics ride along with each Q/dO tile (LDS-DMA, 64 floats each)
+    const u32x4 lrs = make_rsrc_sgpr(p.lse + ((long)b * p.H + h) * p.Tq, (uint32_t)p.Tq * 4);
+    const u32x4 drs = make_rsrc_sgpr(p.delta + ((long)b * p.H + h) * p.Tq, (uint32_t)p.Tq * 4);
     const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
     const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
-    const float* lsep = p.lse + ((long)b * p.H + h) * p.Tq;
-    const float* dlp = p.delta + ((long)b * p.H + h) * p.Tq;
+
+    int qt0 = 0;
+    if (CAUSAL) qt0 = max(0, (kb * 64 - off)) / 64;
+    const int nqt = (p.Tq + 63) / 64;
+    // buffer i: Q tile [0, 8K), dO tile [8K, 16K), lse [16K, 17K), delta [17K, 18K)
+#define Qt(i) (smem + (i) * 18432)
+#define Ot(i) (smem + 8192 + (i) * 18432)
+#define Lt(i) (smem + 16384 + (i) * 18432)
+#define Dt(i) (smem + 17408 + (i) * 18432)
+    auto stage = [&](int qt, int buf) {
+        stage64_async(qrs, p.q_st, qt * 64, p.Tq, Qt(buf), wave, lane);
+        stage64_async(ors, p.do_st, qt * 64, p.Tq, Ot(buf), wave, lane);
+        if (wave < 2) {  // lanes 0-15 carry 64 floats; the rest land as zeros past them
+            const int r = qt * 64 + lane * 4;
+            const uint32_t voff = (lane < 16 && r < p.Tq) ? (uint32_t)(r * 4) : 0xFFFFFFF0u;
+            dma16_async(wave == 0 ? lrs : drs, voff, lds_addr(wave == 0 ? Lt(buf) : Dt(buf)));
+        }
+    };
+    if (qt0 < nqt) stage(qt0, 0);
 
     s16x8 kf[2], vf[2];
 #pragma unroll
@@ -319,31 +420,25 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
         kf[s] = gload16(kbase + (long)kv * p.k_st + s * 32 + g * 8, kv < p.Tk);
         vf[s] = gload16(vbase + (long)kv * p.v_st + s * 32 + g * 8, kv < p.Tk);
     }
+    asm volatile("" : "+v"(kf[0]), "+v"(kf[1]), "+v"(vf[0]), "+v"(vf[1]));  // wait for them here, not in the loop
     f32x4 dvacc[4], dkacc[4];
 #pragma unroll
     for (int jd = 0; jd < 4; ++jd) { dvacc[jd] = (f32x4){0, 0, 0, 0}; dkacc[jd] = (f32x4){0, 0, 0, 0}; }
 
-    int qt0 = 0;
-    if (CAUSAL) qt0 = max(0, (kb * 64 - off)) / 64;
-    const int nqt = (p.Tq + 63) / 64;
-#define Qt(i) (smem + (i) * 16384)
-#define Ot(i) (smem + 8192 + (i) * 16384)
-    if (qt0 < nqt) {
-        stage64(qbase, p.q_st, qt0 * 64, p.Tq, Qt(0), wave, lane);
-        stage64(dobase, p.do_st, qt0 * 64, p.Tq, Ot(0), wave, lane);
-    }
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     for (int qt = qt0; qt < nqt; ++qt) {
+        vm_wait_all();
         __syncthreads();
         const int cur = (qt - qt0) & 1;
-        if (qt + 1 < nqt) {
-            stage64(qbase, p.q_st, (qt + 1) * 64, p.Tq, Qt(cur ^ 1), wave, lane);
-            stage64(dobase, p.do_st, (qt + 1) * 64, p.Tq, Ot(cur ^ 1), wave, lane);
-        }
+        if (qt + 1 < nqt) stage(qt + 1, cur ^ 1);
         const int q0 = qt * 64;
         if (CAUSAL && q0 + 63 + off < kvw) continue;  // wave-uniform: all queries precede this wave's keys
         const char* qt_ = Qt(cur);
         const char* ot_ = Ot(cur);
+        const float* lt_ = reinterpret_cast<const float*>(Lt(cur));
+        const float* dt_ = reinterpret_cast<const float*>(Dt(cur));
+        // masking only where a tile is ragged or crosses the causal diagonal (real branch)
+        const bool need_mask = (q0 + 64 > p.Tq) || (kvw + 16 > p.Tk) || (CAUSAL && kvw + 15 > q0 + off);
         f32x4 pq[4], dsq[4];
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
@@ -355,29 +450,19 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
             da = MFMA(o0, vf[0], da, 0, 0, 0);
             da = MFMA(o1, vf[1], da, 0, 0, 0);
             // lane holds S[q = q0 + 16qi + 4g + r][kv]
-            const int qb4 = q0 + qi * 16 + 4 * g;
-            float ls[4], dl[4];
-            if (qb4 + 3 < p.Tq) {
-                float4 a = *reinterpret_cast<const float4*>(lsep + qb4);
-                float4 d = *reinterpret_cast<const float4*>(dlp + qb4);
-                ls[0] = a.x; ls[1] = a.y; ls[2] = a.z; ls[3] = a.w;
-                dl[0] = d.x; dl[1] = d.y; dl[2] = d.z; dl[3] = d.w;
-            } else {
-                for (int r = 0; r < 4; ++r) {
-                    ls[r] = qb4 + r < p.Tq ? lsep[qb4 + r] : INFINITY;
-                    dl[r] = qb4 + r < p.Tq ? dlp[qb4 + r] : 0.f;
-                }
-            }
+            const int ql = qi * 16 + 4 * g;
+            const float4 l4 = *reinterpret_cast<const float4*>(lt_ + ql);
+            const float4 d4 = *reinterpret_cast<const float4*>(dt_ + ql);
+            const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int qg = qb4 + r;
+                const int qg = q0 + ql + r;
                 float x = sa[r] * sl2;
                 if constexpr (BIAS) {
                     if (qg < p.Tq && kv < p.Tk)
                         x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kv] * LOG2E;
                 }
                 float pv = __builtin_amdgcn_exp2f(x - ls[r] * LOG2E);
-                if (kv >= p.Tk || qg >= p.Tq || (CAUSAL && kv > qg + off) || ls[r] == INFINITY) pv = 0.f;
                 float dpv = da[r];
                 float pd = pv;
                 if constexpr (DROP) {
@@ -388,6 +473,16 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
                 pq[qi][r] = pd;
                 dsq[qi][r] = pv * (dpv - dl[r]);
             }
+        }
+        if (need_mask) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int qg = q0 + qi * 16 + 4 * g + r;
+                    if (kv >= p.Tk || qg >= p.Tq || (CAUSAL && kv > qg + off)) { pq[qi][r] = 0.f; dsq[qi][r] = 0.f; }
+                }
         }
         // dV^T[d][kv] += dO^T[d][q] Pd[q][kv];  dK^T[d][kv] += Q^T[d][q] dS[q][kv]
 #pragma unroll
@@ -403,6 +498,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv64_k(AttnArgs p) {
             }
         }
     }
+#undef Qt
+#undef Ot
+#undef Lt
+#undef Dt
     if (kv < p.Tk) {
         bf16* dkp = p.dk + b * p.dk_sb + (long)kv * p.dk_st + h * p.dk_sh;
         bf16* dvp = p.dv + b * p.dv_sb + (long)kv * p.dv_st + h * p.dv_sh;
@@ -433,8 +532,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
 
     const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
     const bf16* dobase = p.dout + b * p.do_sb + h * p.do_sh;
-    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
-    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
+    const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + h * p.k_sh);
+    const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
     s16x8 qf[2], df[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -456,11 +555,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
             for (int j = 0; j < 8; ++j)
                 part += (float)__builtin_bit_cast(bf16, (short)of[j]) * (float)__builtin_bit_cast(bf16, (short)df[s][j]);
         }
-        part += __shfl_xor(part, 16, 64);
-        part += __shfl_xor(part, 32, 64);
-        dl = part;
+        dl = sum4groups(part);
         if (qok && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qg] = dl;
     }
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(df[0]), "+v"(df[1]), "+v"(dl));  // loads retired here
     f32x4 dqacc[4];
 #pragma unroll
     for (int jd = 0; jd < 4; ++jd) dqacc[jd] = (f32x4){0, 0, 0, 0};
@@ -471,16 +569,17 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
 #define Kt(i) (smem + (i) * 16384)
 #define Vt(i) (smem + 8192 + (i) * 16384)
     if (nkv > 0) {
-        stage64(kbase, p.k_st, 0, p.Tk, Kt(0), wave, lane);
-        stage64(vbase, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+        stage64_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     for (int t = 0; t < nkv; ++t) {
+        vm_wait_all();
         __syncthreads();
         const int cur = t & 1;
         if (t + 1 < nkv) {
-            stage64(kbase, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
-            stage64(vbase, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
+            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
+            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
         }
         const int kv0 = t * 64;
         if (CAUSAL && kv0 > qw + 15 + off) continue;
@@ -503,7 +602,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
                         x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvj] * LOG2E;
                 }
                 float pv = __builtin_amdgcn_exp2f(x - lse2);
-                if (kvj >= p.Tk || !qok || (CAUSAL && kvj > qg + off)) pv = 0.f;
                 float dpv = da[r];
                 if constexpr (DROP) {
                     const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qg, kvj)) >= p.p_drop;
@@ -511,6 +609,16 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
                 }
                 dsv[j][r] = pv * (dpv - dl);
             }
+        }
+        if ((kv0 + 64 > p.Tk) || !qok || (CAUSAL && kv0 + 63 > qw + off)) {  // ragged / diagonal tiles only
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int kvj = kv0 + j * 16 + 4 * g + r;
+                    if (kvj >= p.Tk || !qok || (CAUSAL && kvj > qg + off)) dsv[j][r] = 0.f;
+                }
         }
         // dQ^T[d][q] += K^T[d][kv] dS^T[kv][q]
 #pragma unroll
@@ -712,7 +820,7 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         dim3 g2((Tq + 63) / 64, B * H);
         RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         dim3 g1((Tk + 63) / 64, B * H);
-        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 32768, st, a);
+        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
     } else {
         if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
         dim3 grid(Tq, B * H);

@@ -135,6 +135,22 @@ def test_mlp_fused_matches_unfused(cuda):
         assert rel_err(a, t.grad) < 2e-2
 
 
+def test_gemm_library_candidate_plain_only(cuda):
+    """cfg 7 (vendor library) serves plain GEMMs only; the autotuner cache is keyed by the epilogue,
+    so a shape tuned plain never sends a biased call to the library."""
+    torch.manual_seed(9)
+    a, w, bias = bf(640, 256), bf(384, 256), bf(384)
+    ref = a.float() @ w.float().t()
+    assert rel_err(torch.ops.replicann.gemm(a, w, False, True, None, None, 0, None, None, False, 0, False, None, 7),
+                   ref) < 1e-2
+    with pytest.raises(RuntimeError):
+        torch.ops.replicann.gemm(a, w, False, True, bias, None, 0, None, None, False, 0, False, None, 7)
+    plain = ops.gemm(a, w, tb=True)        # tunes the plain key (library is a candidate)
+    biased = ops.gemm(a, w, tb=True, bias=bias)
+    assert rel_err(plain, ref) < 1e-2
+    assert rel_err(biased, ref + bias.float()) < 1e-2
+
+
 # ----------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("E", [768, 1024, 96])
 def test_layernorm(cuda, E):
