@@ -219,8 +219,8 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             Tensor scratch = at::empty({M, N}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
             const bool plain = !(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
                                !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
-            const int ncfg = plain ? 5 : 4;
-            const int cfgs[5] = {0, 1, 6, 2, kLibCfg};
+            const int ncfg = plain ? 6 : 5;
+            const int cfgs[6] = {0, 1, 6, 2, 8, kLibCfg};
             const int splits[5] = {1, 2, 4, 8, 16};
             const int nsplit = split_k < 0 ? 5 : 1;
             Tensor tws = at::empty({rn_gemm_ws_floats(M, N, 16)}, a.options().dtype(at::kFloat));

@@ -130,7 +130,66 @@ RN_DEV i32x8 frag8(const char* lds, int mnbase, int lane) {
     return (i32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT, bool PIPE, bool FP8 = false>
+// ---- deep-pipeline support: compiler-invisible LDS-DMA + counted vmcnt waits ----
+// With more than one tile in flight the compiler's own waits would drain every DMA
+// (s_waitcnt vmcnt(0)) at each barrier and in front of LDS reads it cannot prove
+// disjoint from the DMA target; issuing the DMA from inline asm hides it, and the
+// kernel waits with counted vmcnt(N) itself (never 0 in steady state).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+RN_DEV u32x4 rsrc_sgpr(const void* base) {
+    const uint64_t bp = (uint64_t)base;
+    u32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    r[2] = 0x7FFFFFF0u;
+    r[3] = 0x00020000u;
+    return r;
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+RN_DEV void dma16(const u32x4& rs, uint32_t voff, const char* lds) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds);
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(l)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int N>
+RN_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// same tile/image as stage(), DMA through dma16
+template <bool KC, int ROWS, int NW>
+RN_DEV void stage_async(const bf16* base, long ld, int mn_lim, int k_lim, char* lds, int wave, int lane) {
+    const u32x4 rs = rsrc_sgpr(base);
+    constexpr int NINS = ROWS * 128 / 1024;
+    constexpr int PER = NINS / NW;
+    static_assert(NINS % NW == 0, "tile / wave mismatch");
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int ins = wave * PER + i;
+        uint32_t voff;
+        if constexpr (KC) {
+            const int r = ins * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz_kc(r);
+            const int k = cg * 8;
+            const bool ok = (r < mn_lim) && (k < k_lim);
+            voff = ok ? (uint32_t)(((long)r * ld + k) * 2) : 0xFFFFFFF0u;
+        } else {
+            const int sub = ins >> 3, within = ins & 7;
+            const int r = within * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz_mn(r);
+            const int mn = sub * 64 + cg * 8;
+            const bool ok = (r < k_lim) && (mn < mn_lim);
+            voff = ok ? (uint32_t)(((long)r * ld + mn) * 2) : 0xFFFFFFF0u;
+        }
+        dma16(rs, voff, lds + ins * 1024);
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT, bool PIPE, bool FP8 = false,
+          int NS = 2>
 __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     constexpr int NW = WM * WN;
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -163,7 +222,92 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (PIPE) {
+    if constexpr (PIPE && NS > 2) {
+        // NS-stage ring (NS-1 tiles in flight): the same 4-phase schedule as below, but
+        // the DMA of tile kt+NS is issued into tile kt's buffer right after the
+        // end-of-tile barrier, and that barrier only waits for tile kt+1 (counted vmcnt),
+        // so every tile has NS-1 tile-times to arrive from L2 / HBM.
+        constexpr int HM = FM / 2;
+        static_assert(FM % 2 == 0, "pipelined loop splits the wave's M fragments in two halves");
+        constexpr int OPS = (BM * 128 / 1024) / NW + (BN * 128 / 1024) / NW;  // DMA instr / wave / tile
+        static_assert((NS - 1) * OPS <= 63, "vmcnt range");
+        auto wait_tiles = [&](int younger) {  // wait until at most `younger` tiles' DMA remain in flight
+            if (younger <= 0) vm_wait<0>();
+            else if (younger == 1) vm_wait<OPS>();
+            else if (younger == 2) vm_wait<2 * OPS>();
+            else vm_wait<3 * OPS>();
+        };
+        auto sync = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        auto issue = [&](int t, int buf) {
+            const int k0 = kbeg + t * BK;
+            char* nb = smem + buf * STAGE;
+            stage_async<AK, BM, NW>(a_base(k0), p.lda, p.M - m0, kend - k0, nb, wave, lane);
+            stage_async<BK_, BN, NW>(b_base(k0), p.ldb, p.N - n0, kend - k0, nb + A_BYTES, wave, lane);
+        };
+        s16x8 A0[HM], A1[HM], B0[FN], B1[FN];
+#define RN_LDA(DST, LA, MH, S)                                                        \
+        _Pragma("unroll") for (int i_ = 0; i_ < HM; ++i_)                          \
+            DST[i_] = frag<AK>(LA, wm * (BM / WM) + ((MH) * HM + i_) * 16, S, lane);
+#define RN_LDB(DST, LB, S)                                                            \
+        _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                          \
+            DST[j_] = frag<BK_>(LB, wn * (BN / WN) + j_ * 16, S, lane);
+#define RN_MMA(A, B, MH)                                                              \
+        _Pragma("unroll") for (int i_ = 0; i_ < HM; ++i_)                          \
+        _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                          \
+            acc[(MH) * HM + i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B[j_], A[i_], acc[(MH) * HM + i_][j_], 0, 0, 0);
+        const int npro = min(NS, nk);
+        for (int t = 0; t < npro; ++t) issue(t, t);
+        wait_tiles(npro - 1);
+        sync();
+        if (nk > 0) {
+            RN_LDA(A0, smem, 0, 0)
+            RN_LDB(B0, smem + A_BYTES, 0)
+        }
+        int cur = 0;
+        for (int kt = 0; kt < nk; ++kt) {
+            const char* la = smem + cur * STAGE;
+            const char* lb = la + A_BYTES;
+            _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)
+                acc[0][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B0[j_], A0[0], acc[0][j_], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            RN_LDA(A1, la, 1, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            _Pragma("unroll") for (int i_ = 1; i_ < HM; ++i_)
+            _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)
+                acc[i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B0[j_], A0[i_], acc[i_][j_], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            RN_LDA(A0, la, 0, 1)
+            RN_LDB(B1, lb, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            RN_MMA(A1, B0, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            RN_LDA(A1, la, 1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            RN_MMA(A0, B1, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + 1 < nk) wait_tiles(min(NS - 2, nk - 2 - kt));  // tile kt+1 landed (this wave's DMA)
+            sync();  // ... every wave's; every read of buffer `cur` retired
+            if (kt + NS < nk) issue(kt + NS, cur);
+            const int nxt = cur + 1 == NS ? 0 : cur + 1;
+            if (kt + 1 < nk) {
+                const char* na = smem + nxt * STAGE;
+                RN_LDA(A0, na, 0, 0)
+                RN_LDB(B0, na + A_BYTES, 0)
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            RN_MMA(A1, B1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            cur = nxt;
+        }
+#undef RN_LDA
+#undef RN_LDB
+#undef RN_MMA
+        __syncthreads();  // epilogue reuses the LDS ring
+    } else if constexpr (PIPE) {
         // Software-pipelined main loop: 4 MFMA phases per K-tile (k-step s × M-half),
         // the fragments of phase i+1 are read from LDS while phase i's MFMAs run,
         // ONE barrier per K-tile (before the last phase) that (a) retires the
@@ -479,12 +623,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT>
+template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT, int NS = 2>
 void launch_t(GemmArgs& a, hipStream_t st) {
     constexpr int NT = WM * WN * 64;
-    const size_t lds = std::max<size_t>(2 * (BM + BN) * BK * 2, (size_t)BM * (BN * 2 + 16));
-    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE>;
-    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE>;
+    const size_t lds = std::max<size_t>((size_t)NS * (BM + BN) * BK * 2, (size_t)BM * (BN * 2 + 16));
+    static_assert((size_t)NS * (BM + BN) * BK * 2 <= 163840, "LDS ring exceeds 160 KiB");
+    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE, false, NS>;
+    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE, false, NS>;
     static bool attr = false;
     if (!attr) {  // >64 KiB of dynamic LDS must be opted into, once per instantiation
         attr = true;
@@ -502,18 +647,18 @@ void launch_t(GemmArgs& a, hipStream_t st) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool PIPE>
+template <int BM, int BN, int WM, int WN, bool PIPE, int NS = 2>
 void launch_cfg(GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
     a.tiles_m = (a.M + BM - 1) / BM;
     a.tiles_n = (a.N + BN - 1) / BN;
 #define RN_L(AKv, BKv)                                                                             \
-    if (act == ACT_GELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_GELU>(a, st);               \
-    else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_RELU>(a, st);          \
-    else launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_NONE>(a, st);
+    if (act == ACT_GELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_GELU, NS>(a, st);           \
+    else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_RELU, NS>(a, st);      \
+    else launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_NONE, NS>(a, st);
     if (ak && bk) { RN_L(true, true) }
     else if (ak && !bk) {  // dgrad layout: also the fused activation-backward epilogues
-        if (act == ACT_GELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_GELU_BWD>(a, st);
-        else if (act == ACT_RELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_RELU_BWD>(a, st);
+        if (act == ACT_GELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_GELU_BWD, NS>(a, st);
+        else if (act == ACT_RELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_RELU_BWD, NS>(a, st);
         else { RN_L(true, false) }
     }
     else if (!ak && bk) { RN_L(false, true) }

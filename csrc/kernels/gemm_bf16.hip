@@ -53,6 +53,7 @@ void rn_gemm_launch_cfg3(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg4(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg5(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg6(GemmArgs&, bool, bool, int, hipStream_t);
+void rn_gemm_launch_cfg8(GemmArgs&, bool, bool, int, hipStream_t);
 
 namespace {
 
@@ -100,7 +101,8 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 //   trans_a = 0: A stored [M][lda] (K contiguous);   1: A stored [K][lda] (M contiguous)
 //   trans_b = 0: B stored [K][ldb] (N contiguous);   1: B stored [N][ldb] (K contiguous)
 //   cfg: -1 auto, 0 = 128x128, 1 = 256x256 pipelined, 2 = 256x128 pipelined, 3 = 128x256,
-//        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined;  split: -1 auto, 0/1 none
+//        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined, 8 = 256x128 3-stage ring
+//        (7 is the vendor-library candidate handled in the bindings);  split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
@@ -133,6 +135,7 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
         case 4: rn_gemm_launch_cfg4(a, ak, bk, act, st); break;
         case 5: rn_gemm_launch_cfg5(a, ak, bk, act, st); break;
         case 6: rn_gemm_launch_cfg6(a, ak, bk, act, st); break;
+        case 8: rn_gemm_launch_cfg8(a, ak, bk, act, st); break;
         default: rn_gemm_launch_cfg0(a, ak, bk, act, st); break;
     }
     return 0;

@@ -74,7 +74,7 @@ def test_production_gemm_shapes_all_configs(cuda, M, N, K):
     dgrad = dy.float() @ w.float()
     g0 = (torch.randn(N, K, device="cuda") * 10).bfloat16()
     wgrad = g0.float() + dy.float().t() @ x.float()
-    for cfg in (0, 1, 2, 6):
+    for cfg in (0, 1, 2, 6, 8):
         assert rel_err(ops.gemm(x, w, tb=True, cfg=cfg), fwd) < 1e-2, cfg
         assert rel_err(ops.gemm(dy, w, cfg=cfg), dgrad) < 1e-2, cfg
         for split in (1, 2, 4, 8, 16):

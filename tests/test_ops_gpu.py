@@ -26,7 +26,7 @@ def test_native_loaded(cuda):
 
 
 # ----------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 96), (1000, 384, 520), (64, 24, 8), (520, 776, 1088)])
 def test_gemm_layouts(cuda, ta, tb, M, N, K, cfg):
