@@ -195,8 +195,10 @@ __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in,
     __syncthreads();
     if (w == 0) {
         if (c < C) tmp[(long)blockIdx.y * C + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores drained
         if (lane == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // hipcc may drop the fence's own wait
             unsigned t = __hip_atomic_fetch_add(&rn_colsum_cnt[blockIdx.x], 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
             is_last = (t == (unsigned)S - 1);
@@ -205,6 +207,7 @@ __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in,
     __syncthreads();
     if (!is_last || w != 0) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (c < C) {
         float acc = 0.f;
         for (int i = 0; i < S; ++i) acc += __builtin_nontemporal_load(tmp + (long)i * C + c);
