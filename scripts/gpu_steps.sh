@@ -32,6 +32,8 @@ for step in "$@"; do
     tprof) run tprof 600 python bench.py --steps 3 --warmup 2 --profile-steps 2 ;;
     microbench) run microbench 600 python scripts/microbench.py ;;
     mbgemm) run mbgemm 600 python scripts/microbench.py gemm ;;
+    mbattn) run mbattn 300 python scripts/microbench.py attn ln xent ;;
+    det) run det 300 python -m pytest tests/test_determinism_gpu.py -q ;;
     stock) run stock 600 python scripts/bench_stock_torch.py --steps 10 --warmup 3 ;;
     *) run custom 600 bash -c "$step" ;;
   esac

@@ -36,6 +36,7 @@ def main():
     torch.manual_seed(0)
     M = 16 * 1024
     res = []
+    want = set(sys.argv[1:]) or {"gemm", "fp8", "attn", "ln", "xent"}
     gemms = [  # name, M, N, K, layout
         ("qkv_fwd", M, 2304, 768, "nt"), ("proj_fwd", M, 768, 768, "nt"), ("fc_fwd", M, 3072, 768, "nt"),
         ("fc2_fwd", M, 768, 3072, "nt"), ("lmhead_fwd", M, 50304, 768, "nt"),
@@ -43,7 +44,7 @@ def main():
         ("fc_wgrad", 3072, 768, M, "tn"), ("qkv_wgrad", 2304, 768, M, "tn"), ("proj_wgrad", 768, 768, M, "tn"),
         ("lmhead_wgrad", 50304, 768, M, "tn"),
     ]
-    for name, m, n, k, lay in gemms:
+    for name, m, n, k, lay in (gemms if "gemm" in want else []):
         ta, tb = lay[0] == "t", lay[1] == "t"
         a = bf(k, m) if ta else bf(m, k)
         b = bf(n, k) if tb else bf(k, n)
@@ -55,8 +56,8 @@ def main():
         fl = 2 * m * n * k
         t_r = min(timeit(ref) for _ in range(3))
         cfg_t = {}
-        for cfg in (-1, 0, 1, 2, 5, 6):
-            for s_ in sorted({-1, 1, 2, 4}) if ta else [0]:
+        for cfg in (-1, 0, 1, 2, 5, 6, 8) + (() if ta else (7,)):
+            for s_ in (sorted({-1, 1, 2, 4}) if ta else [0]) if cfg != 7 else [0]:
                 ours = lambda: ops.gemm(a, b, ta=ta, tb=tb, split_k=s_, cfg=cfg)
                 err = ((ours().float() - ref().float()).norm() / ref().float().norm()).item()
                 cfg_t[f"c{cfg}s{s_}"] = (min(timeit(ours) for _ in range(2)), err)
@@ -68,11 +69,9 @@ def main():
                  all_tflops={kk: round(fl / v[0] / 1e9) for kk, v in cfg_t.items()})
         print(json.dumps(r), flush=True)
         res.append(r)
-    if len(sys.argv) > 1 and sys.argv[1] == "gemm":
-        return
     # fp8 (block-scaled MFMA) vs bf16 on GPT-2-medium forward shapes
-    for name, m, n, k in (("med_qkv", M, 3072, 1024), ("med_fc", M, 4096, 1024), ("med_fc2", M, 1024, 4096),
-                          ("med_proj", M, 1024, 1024)):
+    for name, m, n, k in ((("med_qkv", M, 3072, 1024), ("med_fc", M, 4096, 1024), ("med_fc2", M, 1024, 4096),
+                           ("med_proj", M, 1024, 1024)) if "fp8" in want else ()):
         a, b = bf(m, k), bf(n, k)
         qa, sa = ops.quantize_fp8(a)
         qb, sb = ops.quantize_fp8(b)
@@ -87,6 +86,7 @@ def main():
         res.append(r)
     # attention fwd / bwd (B=16, H=12, T=1024, D=64, causal)
     B, T, H, D = 16, 1024, 12, 64
+    attn_cases = ("attn_fwd", "attn_bwd") if "attn" in want else ()
     qkv = bf(B, T, 3, H, D).requires_grad_()
     q, k, v = [t.detach().transpose(1, 2).contiguous().requires_grad_() for t in qkv.unbind(2)]
     go = bf(B, T, H, D)
@@ -98,13 +98,16 @@ def main():
     gr = go.transpose(1, 2).contiguous()
     b_r = lambda: torch.autograd.grad(out_r, (q, k, v), gr, retain_graph=True)
     fl_f = 4 * B * H * T * T * D / 2
-    for nm, fo, fr, fl in (("attn_fwd", f_o, f_r, fl_f), ("attn_bwd", b_o, b_r, 2.5 * fl_f)):
+    for nm, fo, fr, fl in [c for c in (("attn_fwd", f_o, f_r, fl_f), ("attn_bwd", b_o, b_r, 2.5 * fl_f))
+                           if c[0] in attn_cases]:
         t_o = min(timeit(fo) for _ in range(3))
         t_r = min(timeit(fr) for _ in range(3))
         r = dict(op=nm, ours_ms=t_o, torch_ms=t_r, ours_tflops=fl / t_o / 1e9, torch_tflops=fl / t_r / 1e9)
         print(json.dumps(r), flush=True)
         res.append(r)
     # LayerNorm, cross-entropy
+    if "ln" not in want and "xent" not in want:
+        return _dump(res)
     x, w, bb = bf(M, 768), bf(768), bf(768)
     t_o = min(timeit(lambda: ops.layer_norm(x, w, bb)) for _ in range(3))
     t_r = min(timeit(lambda: F.layer_norm(x, (768,), w, bb)) for _ in range(3))
@@ -118,6 +121,10 @@ def main():
     r = dict(op="xent_fwd", ours_ms=t_o, torch_ms=t_r, gbps=logits.numel() * 2 / t_o / 1e6)
     print(json.dumps(r), flush=True)
     res.append(r)
+    _dump(res)
+
+
+def _dump(res):
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/microbench.json", "w") as f:
         json.dump(res, f, indent=1)
