@@ -58,7 +58,9 @@ int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const floa
                 int, int, float, int, float, uint64_t, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
                 void*, void*, void*, float*, float*, float*, const long*, int, int, int, int, int, float, int, float,
-                uint64_t, hipStream_t);
+                uint64_t, float*, hipStream_t);
+void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
+int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -534,7 +536,7 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 }
 void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                    const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
-                   const Tensor& dq, const Tensor& dk, const Tensor& dv) {
+                   const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad = {}) {
     GUARD(q);
     const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3), Tk = k.size(1);
     std::vector<long> s;
@@ -547,12 +549,28 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
     }
     int bias_b = bias && bias->defined() ? bias->size(0) : 1;
     if (B * H * Tq == 0) return;
+    // packed-QKV bias gradient: per-64-row-block column partials from the kernels, then one reduction
+    Tensor bsum;
+    const bool want_bg = qkv_bias_grad && qkv_bias_grad->defined();
+    const int nblk = (Tq + 63) / 64;
+    if (want_bg) {
+        CHECK_BF16(*qkv_bias_grad);
+        TORCH_CHECK(qkv_bias_grad->numel() == 3L * H * D && qkv_bias_grad->is_contiguous() && D == 64 && Tq == Tk,
+                    "qkv bias gradient: packed self-attention with head_dim 64 only");
+        bsum = at::empty({(int64_t)B * nblk, 3L * H * D}, q.options().dtype(at::kFloat));
+    }
     int rc = rn_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                          bias && bias->defined() ? bias->data_ptr<float>() : nullptr, bias_b, dq.data_ptr(), dk.data_ptr(),
                          dv.data_ptr(), delta.data_ptr<float>(), dk32.defined() ? dk32.data_ptr<float>() : nullptr,
                          dv32.defined() ? dv32.data_ptr<float>() : nullptr, s.data(), B, H, Tq, Tk, D, (float)scale,
-                         causal, (float)p, (uint64_t)seed, cur_stream());
+                         causal, (float)p, (uint64_t)seed, want_bg ? bsum.data_ptr<float>() : nullptr, cur_stream());
     TORCH_CHECK(rc == 0, "attention backward: unsupported shape D=", D);
+    if (want_bg) {
+        const int C = 3 * H * D;
+        Tensor tmp = at::empty({rn_colsum_ws(C)}, q.options().dtype(at::kFloat));
+        rn_colsum_f32(bsum.data_ptr<float>(), B * nblk, C, tmp.data_ptr<float>(), qkv_bias_grad->data_ptr(), 1,
+                      cur_stream());
+    }
 }
 std::tuple<Tensor, Tensor, Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
                                             const Tensor& o, const Tensor& lse, const optional<Tensor>& bias,
@@ -565,8 +583,8 @@ std::tuple<Tensor, Tensor, Tensor> attn_bwd(const Tensor& dout, const Tensor& q,
 }
 void attn_bwd_out(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                   const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
-                  const Tensor& dq, const Tensor& dk, const Tensor& dv) {
-    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv);
+                  const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad) {
+    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, qkv_bias_grad);
 }
 
 // ------------------------------------------------------------------ conv / pool / bn
@@ -716,7 +734,8 @@ TORCH_LIBRARY(replicann, m) {
     m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
           "bool causal, float p, int seed) -> (Tensor, Tensor, Tensor)");
     m.def("attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
-          "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+          "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, "
+          "Tensor(d!)? qkv_bias_grad=None) -> ()");
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> Tensor");

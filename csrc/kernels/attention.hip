@@ -47,7 +47,27 @@ struct AttnArgs {
     float scale, p_drop;
     uint64_t seed;
     float* dk32; float* dv32;  // generic bwd scratch
+    // optional [B * ceil(T/64)][3 * H * 64] fp32: per-64-row-block column sums of dQ | dK | dV
+    // (the packed-QKV projection's bias gradient, reduced later) — fast path, self-attention
+    float* bsum;
 };
+
+// Sum a wave-tile's [16 rows][64 cols] accumulator (lane holds row lane&15, cols 16jd+4g+r)
+// over the 64 rows of the 4 waves via LDS and write one partial row: out[col].
+RN_DEV void block_colsum64(const f32x4 (&acc)[4], float mul, float* lds, float* out, int wave, int lane) {
+    const int g = lane >> 4, c = lane & 15;
+    __syncthreads();  // LDS tiles no longer read by any wave
+#pragma unroll
+    for (int jd = 0; jd < 4; ++jd)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds[(wave * 16 + c) * 65 + jd * 16 + 4 * g + r] = acc[jd][r] * mul;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        float t = 0.f;
+        for (int row = 0; row < 64; ++row) t += lds[row * 65 + threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+}
 
 RN_DEV int swz(int r) { return ((r >> 1) & 3) << 1; }
 
@@ -502,6 +522,12 @@ __global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
 #undef Ot
 #undef Lt
 #undef Dt
+    if (p.bsum) {  // dK / dV column partials for the QKV bias gradient
+        const int E = p.H * 64;
+        float* row = p.bsum + ((long)b * gridDim.x + kb) * 3 * E + h * 64;
+        block_colsum64(dkacc, p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
+        block_colsum64(dvacc, 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
+    }
     if (kv < p.Tk) {
         bf16* dkp = p.dk + b * p.dk_sb + (long)kv * p.dk_st + h * p.dk_sh;
         bf16* dvp = p.dv + b * p.dv_sb + (long)kv * p.dv_st + h * p.dv_sh;
@@ -627,6 +653,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
 #pragma unroll
             for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfrag(kt, 32 * ks, 16 * jd, lane), sb, dqacc[jd], 0, 0, 0);
         }
+    }
+    if (p.bsum) {  // dQ column partials; row = (b, 64-query block)
+        const int E = p.H * 64;
+        float* row = p.bsum + ((long)b * gridDim.x + qb) * 3 * E + h * 64;
+        block_colsum64(dqacc, p.scale, reinterpret_cast<float*>(smem), row, wave, lane);
     }
     if (qok) {
         bf16* dqp = p.dq + b * p.dq_sb + (long)qg * p.dq_st + h * p.dq_sh;
@@ -802,7 +833,7 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
 int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                 const float* bias, int bias_b, void* dq, void* dk, void* dv, float* delta, float* dk32, float* dv32,
                 const long* s, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
-                uint64_t seed, hipStream_t st) {
+                uint64_t seed, float* bsum, hipStream_t st) {
     AttnArgs a = {};
     a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = (float*)lse;
     a.bias = bias; a.dout = (const bf16*)dout; a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.delta = delta;
@@ -811,10 +842,11 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     a.do_sb = s[12]; a.do_st = s[13]; a.do_sh = s[14]; a.dq_sb = s[15]; a.dq_st = s[16]; a.dq_sh = s[17];
     a.dk_sb = s[18]; a.dk_st = s[19]; a.dk_sh = s[20]; a.dv_sb = s[21]; a.dv_st = s[22]; a.dv_sh = s[23];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
-    a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.dk32 = dk32; a.dv32 = dv32;
+    a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.dk32 = dk32; a.dv32 = dv32; a.bsum = bsum;
     const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) &&
                       (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
                       (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
+    if (bsum && !(fast && Tq == Tk)) return -2;  // bias partials: fast self-attention path only
     if (fast) {
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2((Tq + 63) / 64, B * H);

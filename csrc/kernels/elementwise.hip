@@ -176,6 +176,12 @@ void rn_bias_act_grad(const void* dy, const void* h, void* dh, float* db, void* 
     if (want_bias) rn_colreduce(part, splits, N, part + (long)splits * N, db, (bf16*)db16, st, accum);
 }
 
+// out16[c] (+)= Σ_r in[r][c] for an fp32 [R][C] partial matrix (tmp: RN_COLRED_S * C floats).
+void rn_colsum_f32(const float* in, int R, int C, float* tmp, void* out16, int accum, hipStream_t st) {
+    rn_colreduce(in, R, C, tmp, nullptr, (bf16*)out16, st, accum);
+}
+int rn_colsum_ws(int C) { return RN_COLRED_S * C; }
+
 int rn_bias_act_grad_splits(int M, int N) {
     int cblocks = (N + 511) / 512;
     int splits = 1;

@@ -75,7 +75,8 @@ class Attention(nn.Module):
         B, T, E = h.shape
         qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
         a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
-                                 training=self.training)
+                                 training=self.training,
+                                 producer_bias=None if self.c_attn.fp8 else self.c_attn.bias)
         a = a.reshape(B, T, E)
         if self.resid_dropout > 0 and self.training:
             return residual + ops.dropout(self.c_proj(a), self.resid_dropout, True)

@@ -112,27 +112,40 @@ class _AttnPackedFn(torch.autograd.Function):
     """Attention on a packed (B, T, 3, H, D) QKV tensor; backward writes one packed dQKV."""
 
     @staticmethod
-    def forward(ctx, qkv, bias, scale, causal, dropout_p, seed):
+    def forward(ctx, qkv, bias, scale, causal, dropout_p, seed, producer_bias):
         q, k, v = qkv.unbind(2)
         o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, seed)
         ctx.save_for_backward(qkv, o, lse, bias)
         ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed = scale, causal, dropout_p, seed
+        ctx.producer_bias = producer_bias
         return o
 
     @staticmethod
     def backward(ctx, do):
+        from .linear import _direct_grad, _notify
         qkv, o, lse, bias = ctx.saved_tensors
         q, k, v = qkv.unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.unbind(2)
+        pb = ctx.producer_bias
+        B, T, _, H, D = qkv.shape
+        pb_acc = _direct_grad(pb) if (pb is not None and D == 64 and pb.numel() == 3 * H * D) else None
         _ext.ops().attn_bwd_out(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
-                                ctx.dropout_p, ctx.seed, dq, dk, dv)
-        return dqkv, None, None, None, None, None
+                                ctx.dropout_p, ctx.seed, dq, dk, dv, pb_acc)
+        if pb_acc is not None:  # Σ_rows dQKV reduced in the kernels: the c_attn bias gradient
+            pb._rn_bias_done = True
+            _notify(pb)
+        return dqkv, None, None, None, None, None, None
 
 
 def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dropout_p=0.0,
-                     training=False):
-    """Attention over a packed (B, T, 3, H, D) tensor → (B, T, H, D)."""
+                     training=False, producer_bias=None):
+    """Attention over a packed (B, T, 3, H, D) tensor → (B, T, H, D).
+
+    ``producer_bias``: bias of the projection that produced ``qkv`` (3·H·D); its gradient
+    Σ_rows dQKV is then reduced by the attention backward kernels (per-block column
+    partials) and accumulated into the flat gradient, and the projection skips its own
+    bias pass."""
     B, T, three, H, D = qkv.shape
     if scale is None:
         scale = D ** -0.5
@@ -142,6 +155,6 @@ def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dro
     if _ext.use_native(qkv):
         b3 = _bias_3d(bias, B, T, T)
         seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
-        return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed)
+        return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed, producer_bias)
     q, k, v = qkv.unbind(2)
     return attention_reference(q, k, v, scale, causal, bias, p, training)

@@ -70,8 +70,8 @@ class _LinearFp8Fn(torch.autograd.Function):
         x2, weight, preact = ctx.saved_tensors
         gy2 = gy.reshape(-1, weight.shape[0]).contiguous()
         want_b = ctx.has_bias
-        if want_b and getattr(ctx.bias_ref, "_rn_ln_done", False):  # see ops.norm._LayerNormFn
-            ctx.bias_ref._rn_ln_done = False
+        if want_b and getattr(ctx.bias_ref, "_rn_bias_done", False):  # see ops.norm._LayerNormFn
+            ctx.bias_ref._rn_bias_done = False
             want_b = False
         dh, db = bias_act_grad(gy2, preact, ctx.act, want_b)
         gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp) if ctx.needs_input_grad[0] else None

@@ -169,9 +169,9 @@ class _LinearFn(torch.autograd.Function):
         native = _ext.use_native(gy2)
         gx = gw = gb = None
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if want_b and getattr(bias, "_rn_ln_done", False):
+        if want_b and getattr(bias, "_rn_bias_done", False):
             # the downstream LayerNorm backward already accumulated Σ_rows gy into bias.grad
-            bias._rn_ln_done = False
+            bias._rn_bias_done = False
             want_b = False
         db_acc = _direct_grad(bias) if (native and want_b) else None
         if native:
@@ -214,8 +214,8 @@ def _bias_grad(g2, bias, native):
     """Σ_rows g2 into ``bias``'s gradient: (returned grad or None, done_direct)."""
     if bias is None or not bias.requires_grad:
         return None
-    if getattr(bias, "_rn_ln_done", False):  # reduced by the downstream LayerNorm backward
-        bias._rn_ln_done = False
+    if getattr(bias, "_rn_bias_done", False):  # reduced by the downstream LayerNorm backward
+        bias._rn_bias_done = False
         return None
     acc = _direct_grad(bias) if native else None
     if native:

@@ -31,7 +31,7 @@ class _LayerNormFn(torch.autograd.Function):
     ``producer_bias``: bias of the linear layer whose output IS x (x = x_prev +
     a·Wᵀ + b).  Its gradient Σ_rows dx is then produced by this backward kernel
     for free and accumulated straight into the flat gradient buffer; the
-    linear's backward sees ``_rn_ln_done`` and skips its own bias pass.
+    linear's backward sees ``_rn_bias_done`` and skips its own bias pass.
     """
 
     @staticmethod
@@ -73,7 +73,7 @@ class _LayerNormFn(torch.autograd.Function):
                                               db_acc if direct else None, pb_acc)
         dx = dx.reshape(ctx.shp)
         if pb_acc is not None:
-            pb._rn_ln_done = True  # consumed (and reset) by the producer linear's backward
+            pb._rn_bias_done = True  # consumed (and reset) by the producer linear's backward
             _notify(pb)
         g_res = dx if ctx.has_res else None
         if direct:  # gradients already accumulated in the flat buffer

@@ -186,7 +186,7 @@ def test_layernorm_passthrough_producer_bias(cuda, M, E):
     gy, gr = bf(M, E), bf(M, E)
     y, xp = ops.layer_norm(x, mod.w, mod.b, 1e-5, return_sum=True, producer_bias=mod.pb)
     ((y.float() * gy.float()).sum() + (xp.float() * gr.float()).sum()).backward()
-    assert mod.pb._rn_ln_done
+    assert mod.pb._rn_bias_done
     xf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, mod.w, mod.b)]
     yf = F.layer_norm(xf, (E,), wf, bf_, 1e-5)
     ((yf * gy.float()).sum() + (xf * gr.float()).sum()).backward()
@@ -279,6 +279,25 @@ def test_attention_packed_grad(cuda):
     of = ops.attention_reference(q, k, v, 0.125, True)
     of.backward(go.float())
     assert rel_err(o, of) < 2e-2 and rel_err(qkv.grad, qf.grad) < 4e-2
+
+
+@pytest.mark.parametrize("causal,T", [(True, 256), (False, 200)])
+def test_attention_packed_qkv_bias_grad(cuda, causal, T):
+    """Σ_rows dQKV (the c_attn bias gradient) reduced inside the attention backward kernels."""
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(11)
+    B, H, D = 3, 4, 64
+    mod = torch.nn.Module()
+    mod.pb = torch.nn.Parameter(torch.zeros(3 * H * D, device="cuda").bfloat16())
+    flat = FlatParams(mod)
+    flat.zero_grad()
+    qkv = bf(B, T, 3, H, D).requires_grad_()
+    g = bf(B, T, H, D)
+    o = ops.attention_packed(qkv, causal=causal, producer_bias=mod.pb)
+    o.backward(g)
+    assert mod.pb._rn_bias_done
+    ref = qkv.grad.float().reshape(B * T, 3 * H * D).sum(0)
+    assert rel_err(mod.pb.grad, ref) < 1e-2
 
 
 def test_attention_dropout_unbiased(cuda):
