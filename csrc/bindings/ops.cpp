@@ -53,7 +53,8 @@ void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, lon
             hipStream_t);
 long rn_gemm_ws_floats(int, int, int);
 int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, float*, const float*, int, int, int,
-            long, long, long, int, int, int, int, int, int, int, hipStream_t);
+            long, long, long, int, int, int, int, int, int, int, hipStream_t, float*);
+int rn_gemm_cfg_bm(int);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
                 int, int, float, int, float, uint64_t, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
@@ -147,7 +148,8 @@ static void lib_gemm(const Tensor& A, const Tensor& B, bool ta, bool tb, Tensor&
 
 Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<Tensor>& bias,
             const optional<Tensor>& residual, int64_t act, const optional<Tensor>& preact, const optional<Tensor>& out,
-            bool accumulate, int64_t split_k, bool out_fp32, const optional<Tensor>& alpha, int64_t cfg) {
+            bool accumulate, int64_t split_k, bool out_fp32, const optional<Tensor>& alpha, int64_t cfg,
+            const optional<Tensor>& bias_grad) {
     CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(b);
     GUARD(a);
     TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm expects 2-D operands");
@@ -176,6 +178,16 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         TORCH_CHECK(preact->size(0) == M && preact->size(1) == N && preact->stride(0) == c.stride(0));
     }
     const bool act_bwd = act == 3 || act == 4;  // fused activation backward: out = (A·B) ⊙ act'(preact)
+    // bias_grad (act-backward only): Σ_rows of the output accumulated into it — from per-M-tile
+    // column partials the epilogue writes (configs that support it), else one reduction pass
+    const bool want_bg = bias_grad && bias_grad->defined();
+    if (want_bg) {
+        TORCH_CHECK(act_bwd, "gemm bias_grad needs an activation-backward epilogue");
+        CHECK_BF16(*bias_grad);
+        TORCH_CHECK(bias_grad->numel() == N && bias_grad->is_contiguous());
+    }
+    Tensor colpart = want_bg ? at::empty({(M + 127) / 128, N}, a.options().dtype(at::kFloat)) : Tensor();
+    float* cp = want_bg ? colpart.data_ptr<float>() : nullptr;
     if (act_bwd)
         TORCH_CHECK(!ta && !tb && N % 8 == 0 && preact && preact->defined() && !accumulate && !(bias && bias->defined()),
                     "activation-backward epilogue: dgrad layout (A·B, B [K][N]), N % 8 == 0, preact required");
@@ -207,7 +219,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     if (alpha && alpha->defined()) TORCH_CHECK(alpha->scalar_type() == at::kFloat && alpha->is_cuda());
     if (cfg < 0 && split_k <= 0) {
         const int epi = (bias && bias->defined() ? 1 : 0) | (residual && residual->defined() ? 2 : 0) |
-                        (alpha && alpha->defined() ? 4 : 0) | (accumulate ? 8 : 0);
+                        (alpha && alpha->defined() ? 4 : 0) | (accumulate ? 8 : 0) | (want_bg ? 16 : 0);
         const TuneKey key{M, N, Kp, (int)ta, (int)tb, (int)act, (int)out_fp32, split_k < 0 ? 1 : 0, epi};
         bool hit = false;
         {
@@ -243,7 +255,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                                        act_bwd ? preact->data_ptr() : nullptr,
                                        tws.data_ptr<float>(), alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr,
                                        (int)M, (int)N, (int)Kp, A.stride(0), B.stride(0), scratch.stride(0), ta, tb, (int)act,
-                                       sp, out_fp32, 0, cfgs[ci], cur_stream());
+                                       sp, out_fp32, 0, cfgs[ci], cur_stream(), cp);
                     };
                     if (run() != 0) continue;
                     (void)hipEventRecord(e0, cur_stream());
@@ -278,11 +290,30 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     }
     const int ws_split = split > 1 ? split : max_split;
     if (ws_split > 1 && !ws.defined()) ws = at::empty({rn_gemm_ws_floats(M, N, ws_split)}, a.options().dtype(at::kFloat));
-    int rc = rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
-                     preact && preact->defined() ? preact->data_ptr() : nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr,
-                     alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr, (int)M, (int)N, (int)Kp, A.stride(0),
-                     B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32, accumulate, (int)cfg, cur_stream());
+    auto launch = [&](float* colp) {
+        return rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
+                       preact && preact->defined() ? preact->data_ptr() : nullptr,
+                       ws.defined() ? ws.data_ptr<float>() : nullptr,
+                       alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr, (int)M, (int)N, (int)Kp,
+                       A.stride(0), B.stride(0), c.stride(0), ta, tb, (int)act, split, out_fp32, accumulate, (int)cfg,
+                       cur_stream(), colp);
+    };
+    int rc = launch(cp);
+    if (rc == -3) {  // this config cannot emit column partials: plain GEMM + one reduction pass over C
+        rc = launch(nullptr);
+        TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
+        Tensor part = at::empty({(int64_t)(rn_bias_act_grad_splits((int)M, (int)N) + 32) * N}, a.options().dtype(at::kFloat));
+        rn_bias_act_grad(c.data_ptr(), nullptr, c.data_ptr(), nullptr, bias_grad->data_ptr(), part.data_ptr<float>(),
+                         (int)M, (int)N, 0, 1, 1, cur_stream());
+        return c;
+    }
     TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
+    if (want_bg) {
+        const int bm = rn_gemm_cfg_bm((int)cfg);
+        Tensor tmp = at::empty({rn_colsum_ws((int)N)}, a.options().dtype(at::kFloat));
+        rn_colsum_f32(colpart.data_ptr<float>(), (int)((M + bm - 1) / bm), (int)N, tmp.data_ptr<float>(),
+                      bias_grad->data_ptr(), 1, cur_stream());
+    }
     return c;
 }
 
@@ -707,7 +738,8 @@ int64_t native_version() { return 1; }
 
 TORCH_LIBRARY(replicann, m) {
     m.def("gemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, Tensor? residual, int act, Tensor? preact, "
-          "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1) -> Tensor");
+          "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1, "
+          "Tensor(a!)? bias_grad=None) -> Tensor");
     m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias, Tensor(a!)? db_accum=None) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");

@@ -24,7 +24,14 @@ struct GemmArgs {
     long lda, ldb, ldc;
     int tiles_m, tiles_n, split, k_per_split;
     int out_f32, accumulate;
+    // optional [tiles_m][N] fp32: per-M-tile column sums of the output (bias gradient of
+    // the layer the activation-backward epilogue feeds); only for act-backward epilogues
+    // on configs with (threads % (BN/8)) == 0, see colpart_ok()
+    float* colpart;
 };
+
+template <int BN, int NT>
+constexpr bool colpart_cfg_ok() { return (NT % (BN / 8)) == 0; }
 
 RN_DEV int swz_kc(int r) { return (r >> 1) & 7; }
 RN_DEV int swz_mn(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }
@@ -476,6 +483,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                 bf16* dst = pass == 0 ? p.pre : (bf16*)p.C;
                 const bool addres = pass == 1 && p.res;
                 const bool accum = pass == 1 && p.accumulate;
+                // column partial sums (act-backward only): with NT % CPR == 0 every thread
+                // always visits the same 8-column chunk, so it sums its rows in registers
+                constexpr bool CSUM_OK = act_bwd(ACT) && colpart_cfg_ok<BN, NW * 64>();
+                float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 for (int q = threadIdx.x; q < BM * CPR; q += NW * 64) {
                     const int r = q / CPR, cc = q % CPR;
                     if (r >= mlim || cc * 8 >= nlim) continue;
@@ -490,6 +501,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                             load8(p.pre + goff, aux);
 #pragma unroll
                             for (int t = 0; t < 8; ++t) f[t] = (float)(bf16)f[t] * act_grad_f<ACT>(aux[t]);
+                            if constexpr (CSUM_OK) {
+#pragma unroll
+                                for (int t = 0; t < 8; ++t) csum[t] += (float)(bf16)f[t];  // Σ of stored values
+                            }
                         }
                         if (addres) {
                             float rr[8];
@@ -506,6 +521,22 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                         store8(dst + goff, f);
                     } else {
                         *reinterpret_cast<s16x8*>(dst + goff) = v;
+                    }
+                }
+                if constexpr (CSUM_OK) {
+                    if (pass == 1 && p.colpart) {  // fold the NT/CPR row-groups of each chunk (fixed order)
+                        constexpr int RG = NW * 64 / CPR;
+                        float* red = reinterpret_cast<float*>(smem);  // [RG][BN]
+                        __syncthreads();  // staged tile fully read
+                        const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) red[rg * BN + cc * 8 + t] = csum[t];
+                        __syncthreads();
+                        for (int col = threadIdx.x; col < BN; col += NW * 64) {
+                            float tot = 0.f;
+                            for (int g2 = 0; g2 < RG; ++g2) tot += red[g2 * BN + col];
+                            if (n0 + col < p.N) p.colpart[(long)tm * p.N + n0 + col] = tot;
+                        }
                     }
                 }
             }

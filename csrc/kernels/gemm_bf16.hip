@@ -104,9 +104,14 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 //        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined, 8 = 256x128 3-stage ring
 //        (7 is the vendor-library candidate handled in the bindings);  split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
+// colpart (optional, act-backward only): [ceil(M / BM)][N] fp32 per-M-tile column sums of C
+// (BM of the config actually used: rn_gemm_cfg_bm).  Returns -3 if the requested config /
+// split cannot produce them (the caller then reduces C itself).
+int rn_gemm_cfg_bm(int cfg) { return (cfg == 0 || cfg == 3 || cfg == 5) ? 128 : 256; }
+
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
-            int split, int out_f32, int accumulate, int cfg, hipStream_t st) {
+            int split, int out_f32, int accumulate, int cfg, hipStream_t st, float* colpart) {
     if (K % 8 != 0) return -1;
     if (act_bwd(act) && (trans_a || trans_b || !pre)) return -1;  // fused act-backward: dgrad layout only
     if (trans_a && (M % 8 != 0 || lda % 8 != 0)) return -1;
@@ -127,6 +132,10 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     a.k_per_split = kps;
     a.split = (K + kps - 1) / kps;
     a.out_f32 = out_f32; a.accumulate = accumulate;
+    a.colpart = colpart;
+    if (colpart && (!act_bwd(act) || a.split > 1 || out_f32 || N % 8 != 0 || ldc % 8 != 0 || cfg == 6 || cfg == 4 ||
+                    cfg == 3))
+        return -3;  // 256x192 (CPR 24) and the simple 256-wide configs are not wired for it
     const bool ak = !trans_a, bk = trans_b;
     switch (cfg) {
         case 1: rn_gemm_launch_cfg1(a, ak, bk, act, st); break;

@@ -263,8 +263,19 @@ class _MLPFn(torch.autograd.Function):
         nig = ctx.needs_input_grad
         gw2 = _wgrad(gy2, u, w2, True) if nig[3] else None
         gb2 = _bias_grad(gy2, ctx.b2, True) if nig[4] else None
-        dh = ops.gemm(gy2, w2, False, False, None, None, ACT_BWD[ctx.act], pre, None, False, 0, False, None, -1)
-        gb1 = _bias_grad(dh, ctx.b1, True) if nig[2] else None
+        b1 = ctx.b1
+        b1_acc = None
+        if nig[2] and b1 is not None and not getattr(b1, "_rn_bias_done", False):
+            b1_acc = _direct_grad(b1)
+        # dH = (dY·W2) ⊙ act'(pre); with a flat-buffer b1 its gradient Σ_rows dH comes from the
+        # same GEMM's epilogue (per-tile column partials + one small reduction)
+        dh = ops.gemm(gy2, w2, False, False, None, None, ACT_BWD[ctx.act], pre, None, False, 0, False, None, -1,
+                      b1_acc)
+        if b1_acc is not None:
+            _notify(b1)
+            gb1 = None
+        else:
+            gb1 = _bias_grad(dh, b1, True) if nig[2] else None
         gw1 = _wgrad(dh, x2, w1, True) if nig[1] else None
         gx = ops.gemm(dh, w1, False, False, None, None, ACT_NONE, None, None, False, 0, False, None, -1)
         return (gx.reshape(ctx.shp) if nig[0] else None, gw1, gb1, gw2, gb2, None,

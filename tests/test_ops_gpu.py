@@ -107,12 +107,16 @@ def test_gemm_act_backward_epilogue(cuda, act, cfg, split):
     torch.manual_seed(7)
     M, N, K = 520, 776, 384
     dy, w, pre = bf(M, K), bf(K, N, scale=0.1), bf(M, N)
-    out = torch.ops.replicann.gemm(dy, w, False, False, None, None, act, pre, None, False, split, False, None, cfg)
+    bg = bf(N)
+    bg0 = bg.float().clone()
+    out = torch.ops.replicann.gemm(dy, w, False, False, None, None, act, pre, None, False, split, False, None, cfg, bg)
     du = (dy.float() @ w.float()).bfloat16().float()
     pf = pre.float().requires_grad_()
     y = F.relu(pf) if act == 3 else F.gelu(pf, approximate="tanh")
     (g,) = torch.autograd.grad(y, pf, du)
     assert rel_err(out, g) < 1e-2
+    # fused bias gradient (column partials in the epilogue, or the fallback pass) accumulates Σ_rows out
+    assert rel_err(bg.float() - bg0, out.float().sum(0)) < 2e-2
 
 
 def test_mlp_fused_matches_unfused(cuda):
