@@ -63,6 +63,8 @@ int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*,
 void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
 int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
+int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int, int, int, long, long, long, int, int,
+                 int, int, int, int, int, int, int, int, int, long, int, int, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_maxpool_fwd(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -618,6 +620,56 @@ void attn_bwd_out(const Tensor& dout, const Tensor& q, const Tensor& k, const Te
     attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, qkv_bias_grad);
 }
 
+// ------------------------------------------------------------------ implicit-GEMM conv
+// x / dy NHWC bf16 contiguous, w (OC, KH, KW, C) contiguous; the gathered tensor's channel count
+// must be a multiple of 64 (callers check conv_implicit_ok first).
+Tensor conv_fwd_implicit(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int64_t S, int64_t P) {
+    CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w); GUARD(x);
+    const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+    const int OC = w.size(0), KH = w.size(1), KW = w.size(2);
+    TORCH_CHECK(w.size(3) == C, "conv: channel mismatch");
+    const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
+    Tensor y = at::empty({N, OH, OW, OC}, x.options());
+    const int M = N * OH * OW, K = KH * KW * C;
+    if (M == 0) return y;
+    if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == OC); }
+    const int rc = rn_conv_gemm(1, x.data_ptr(), w.data_ptr(), y.data_ptr(), optr(bias), nullptr, M, OC, K, 0, K, OC, H,
+                                W, C, OH, OW, KH, KW, (int)S, (int)P, C, 0, 0, 1, 0, cur_stream());
+    TORCH_CHECK(rc == 0, "implicit conv fwd: unsupported geometry");
+    return y;
+}
+Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t P) {  // stride 1
+    CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w); GUARD(dy);
+    const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), OC = dy.size(3);
+    const int KH = w.size(1), KW = w.size(2), C = w.size(3);
+    TORCH_CHECK(w.size(0) == OC && OH == H + 2 * P - KH + 1 && OW == W + 2 * P - KW + 1, "conv dgrad geometry");
+    Tensor dx = at::empty({N, H, W, C}, dy.options());
+    const int M = N * (int)H * (int)W, K = KH * KW * OC;
+    if (M == 0) return dx;
+    const int rc = rn_conv_gemm(2, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, nullptr, M, C, K, 0, 0, C, OH,
+                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0, cur_stream());
+    TORCH_CHECK(rc == 0, "implicit conv dgrad: unsupported geometry");
+    return dx;
+}
+Tensor conv_wgrad_implicit(const Tensor& dy2, const Tensor& x, int64_t KH, int64_t KW, int64_t S, int64_t P) {
+    CHECK_BF16(dy2); CHECK_CONTIG(dy2); CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+    const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
+    const int OC = dy2.size(1), PIX = N * OH * OW, K = KH * KW * C;
+    TORCH_CHECK(dy2.size(0) == PIX, "conv wgrad: dy rows != output pixels");
+    Tensor dw = at::empty({OC, K}, x.options());
+    // split-K over the pixels so the (OC/128)×(K/128) tile grid fills the chip
+    const long tiles = (long)((OC + 127) / 128) * ((K + 127) / 128);
+    int split = 1;
+    while (tiles * split < 512 && PIX / (split * 2) >= 1024) split *= 2;
+    Tensor ws = split > 1 ? at::empty({(long)split * OC * K}, x.options().dtype(at::kFloat)) : Tensor();
+    const int rc = rn_conv_gemm(3, dy2.data_ptr(), x.data_ptr(), dw.data_ptr(), nullptr,
+                                ws.defined() ? ws.data_ptr<float>() : nullptr, OC, K, PIX, OC, 0, K, H, W, C, OH, OW,
+                                (int)KH, (int)KW, (int)S, (int)P, C, 0, 0, split, 0, cur_stream());
+    TORCH_CHECK(rc == 0, "implicit conv wgrad: unsupported geometry");
+    return dw;
+}
+
 // ------------------------------------------------------------------ conv / pool / bn
 Tensor im2col(const Tensor& x, int64_t KH, int64_t KW, int64_t S, int64_t P, int64_t Kp) {
     CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
@@ -769,6 +821,9 @@ TORCH_LIBRARY(replicann, m) {
           "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, "
           "Tensor(d!)? qkv_bias_grad=None) -> ()");
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
+    m.def("conv_fwd_implicit(Tensor x, Tensor w, Tensor? bias, int S, int P) -> Tensor");
+    m.def("conv_dgrad_implicit(Tensor dy, Tensor w, int H, int W, int P) -> Tensor");
+    m.def("conv_wgrad_implicit(Tensor dy2, Tensor x, int KH, int KW, int S, int P) -> Tensor");
     m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> Tensor");
     m.def("maxpool_bwd(Tensor gy, Tensor x, Tensor y, int K, int S, int P) -> Tensor");
@@ -809,6 +864,9 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("attn_bwd", &attn_bwd);
     m.impl("attn_bwd_out", &attn_bwd_out);
     m.impl("im2col", &im2col);
+    m.impl("conv_fwd_implicit", &conv_fwd_implicit);
+    m.impl("conv_dgrad_implicit", &conv_dgrad_implicit);
+    m.impl("conv_wgrad_implicit", &conv_wgrad_implicit);
     m.impl("col2im", &col2im);
     m.impl("maxpool_fwd", &maxpool_fwd);
     m.impl("maxpool_bwd", &maxpool_bwd);

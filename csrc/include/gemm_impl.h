@@ -11,6 +11,33 @@ constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// u32 division by a runtime constant: q = (umulhi(n, mul) + n) >> shr, exact for n, d < 2^31
+struct FastDiv {
+    uint32_t d, mul, shr;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+    return FastDiv{d, (uint32_t)m, l};
+}
+RN_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
+
+// Implicit-GEMM convolution geometry (NHWC bf16, C % 64 == 0 for the gathered operand):
+//   mode 1 (fwd):   A[m = (n,oh,ow)][k = (kh,kw,c)] = x[n][oh·S-P+kh][ow·S-P+kw][c]
+//   mode 2 (dgrad, S = 1): A[m = (n,ih,iw)][k = (kh,kw,co)] = dY[n][ih+P-kh][iw+P-kw][co],
+//                   B[k][c] = W[co][kh][kw][c]  (row stride bld = KH·KW·C)
+//   mode 3 (wgrad): B[k = (n,oh,ow)][j = (kh,kw,c)] = x[n][oh·S-P+kh][ow·S-P+kw][c]
+struct ConvGeom {
+    int H, W, C;     // gathered tensor (x, or dY for dgrad)
+    int RH, RW;      // decode of the pixel index: p = (n·RH + y)·RW + x
+    int KH, KW, S, P;
+    int KC;          // channels per tap in the K layout
+    int BC;          // dgrad: channels of W's last dim (= GEMM N)
+    long bld;        // dgrad: W row stride
+    FastDiv fd_hw, fd_w, fd_kc, fd_kw;
+};
+
 struct GemmArgs {
     const bf16* A;
     const bf16* B;
@@ -28,6 +55,7 @@ struct GemmArgs {
     // the layer the activation-backward epilogue feeds); only for act-backward epilogues
     // on configs with (threads % (BN/8)) == 0, see colpart_ok()
     float* colpart;
+    ConvGeom cv;
 };
 
 template <int BN, int NT>
@@ -195,8 +223,66 @@ RN_DEV void stage_async(const bf16* base, long ld, int mn_lim, int k_lim, char* 
     }
 }
 
+// ---- implicit-GEMM convolution operand loaders (LDS images identical to stage()) ----
+// A rows gathered from an NHWC tensor (modes 1, 2): K-contiguous image, one (kh, kw) tap and
+// 64 channels per K-tile (C % 64 == 0), zero-fill outside the image (padding) and past M.
+template <int ROWS, int NW, int MODE>
+RN_DEV void stage_conv_a(const GemmArgs& p, int m0, int k0, int kend, char* lds, int wave, int lane) {
+    const ConvGeom& g = p.cv;
+    const u32x4 rs = rsrc_sgpr(p.A);
+    constexpr int NINS = ROWS * 128 / 1024;
+    constexpr int PER = NINS / NW;
+    const int tap = (int)fdiv((uint32_t)k0, g.fd_kc);
+    const int c0 = k0 - tap * g.KC;
+    const int kh = (int)fdiv((uint32_t)tap, g.fd_kw), kw = tap - kh * g.KW;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int ins = wave * PER + i;
+        const int r = ins * 8 + (lane >> 3);
+        const int cg = (lane & 7) ^ swz_kc(r);
+        const int m = m0 + r;
+        const int n = (int)fdiv((uint32_t)m, g.fd_hw);
+        const int rem = m - n * g.RH * g.RW;
+        const int y = (int)fdiv((uint32_t)rem, g.fd_w), x = rem - y * g.RW;
+        const int ih = MODE == 1 ? y * g.S - g.P + kh : y + g.P - kh;
+        const int iw = MODE == 1 ? x * g.S - g.P + kw : x + g.P - kw;
+        const bool ok = m < p.M && k0 < kend && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const uint32_t voff = ok ? (uint32_t)(((((n * g.H + ih) * g.W + iw) * g.C) + c0 + cg * 8) * 2) : 0xFFFFFFF0u;
+        dma16(rs, voff, lds + ins * 1024);
+    }
+}
+
+// B gathered for the weight gradient (mode 3): N-contiguous image (64-column sub-images,
+// k-rows = output pixels), one tap per sub-image.
+template <int COLS, int NW>
+RN_DEV void stage_conv_b(const GemmArgs& p, int n0, int k0, int kend, char* lds, int wave, int lane) {
+    const ConvGeom& g = p.cv;
+    const u32x4 rs = rsrc_sgpr(p.B);
+    constexpr int NINS = COLS * 128 / 1024;
+    constexpr int PER = NINS / NW;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int ins = wave * PER + i;
+        const int sub = ins >> 3, within = ins & 7;
+        const int r = within * 8 + (lane >> 3);
+        const int cg = (lane & 7) ^ swz_mn(r);
+        const int nn = n0 + sub * 64;
+        const int tap = (int)fdiv((uint32_t)nn, g.fd_kc);
+        const int cb = nn - tap * g.KC;
+        const int kh = (int)fdiv((uint32_t)tap, g.fd_kw), kw = tap - kh * g.KW;
+        const int pix = k0 + r;
+        const int n = (int)fdiv((uint32_t)pix, g.fd_hw);
+        const int rem = pix - n * g.RH * g.RW;
+        const int y = (int)fdiv((uint32_t)rem, g.fd_w), x = rem - y * g.RW;
+        const int ih = y * g.S - g.P + kh, iw = x * g.S - g.P + kw;
+        const bool ok = pix < kend && nn + cg * 8 < p.N && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const uint32_t voff = ok ? (uint32_t)(((((n * g.H + ih) * g.W + iw) * g.C) + cb + cg * 8) * 2) : 0xFFFFFFF0u;
+        dma16(rs, voff, lds + ins * 1024);
+    }
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BK_, int ACT, bool SPLIT, bool PIPE, bool FP8 = false,
-          int NS = 2>
+          int NS = 2, int CONV = 0>
 __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     constexpr int NW = WM * WN;
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -252,8 +338,20 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
         auto issue = [&](int t, int buf) {
             const int k0 = kbeg + t * BK;
             char* nb = smem + buf * STAGE;
-            stage_async<AK, BM, NW>(a_base(k0), p.lda, p.M - m0, kend - k0, nb, wave, lane);
-            stage_async<BK_, BN, NW>(b_base(k0), p.ldb, p.N - n0, kend - k0, nb + A_BYTES, wave, lane);
+            if constexpr (CONV == 1 || CONV == 2) {
+                stage_conv_a<BM, NW, CONV>(p, m0, k0, kend, nb, wave, lane);
+            } else {
+                stage_async<AK, BM, NW>(a_base(k0), p.lda, p.M - m0, kend - k0, nb, wave, lane);
+            }
+            if constexpr (CONV == 3) {
+                stage_conv_b<BN, NW>(p, n0, k0, kend, nb + A_BYTES, wave, lane);
+            } else if constexpr (CONV == 2) {  // W[co][kh][kw][c] rows of one tap
+                const int tap = (int)fdiv((uint32_t)k0, p.cv.fd_kc), co0 = k0 - tap * p.cv.KC;
+                stage_async<false, BN, NW>(p.B + (long)co0 * p.cv.bld + (long)tap * p.cv.BC + n0, p.cv.bld,
+                                           p.N - n0, kend - k0, nb + A_BYTES, wave, lane);
+            } else {
+                stage_async<BK_, BN, NW>(b_base(k0), p.ldb, p.N - n0, kend - k0, nb + A_BYTES, wave, lane);
+            }
         };
         s16x8 A0[HM], A1[HM], B0[FN], B1[FN];
 #define RN_LDA(DST, LA, MH, S)                                                        \
@@ -654,13 +752,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT, int NS = 2>
+template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT, int NS = 2, int CONV = 0>
 void launch_t(GemmArgs& a, hipStream_t st) {
     constexpr int NT = WM * WN * 64;
     const size_t lds = std::max<size_t>((size_t)NS * (BM + BN) * BK * 2, (size_t)BM * (BN * 2 + 16));
     static_assert((size_t)NS * (BM + BN) * BK * 2 <= 163840, "LDS ring exceeds 160 KiB");
-    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE, false, NS>;
-    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE, false, NS>;
+    static_assert(CONV == 0 || (PIPE && NS > 2), "implicit-GEMM conv loaders live in the NS-stage path");
+    auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE, false, NS, CONV>;
+    auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE, false, NS, CONV>;
     static bool attr = false;
     if (!attr) {  // >64 KiB of dynamic LDS must be opted into, once per instantiation
         attr = true;

@@ -1,0 +1,67 @@
+// Implicit-GEMM convolution (NHWC bf16): the im2col matrix is never materialised — the
+// GEMM's LDS-DMA loaders gather each K-tile (one filter tap × 64 channels) straight from
+// the activation tensor, zero-filling the padding through the buffer range check.
+//   mode 1  fwd    y[pix][oc]    = Σ_k x̂[pix][k] · w[oc][k]          (A gathered)
+//   mode 2  dgrad  dx[pix][c]    = Σ_k dŷ[pix][k] · w[co][kh][kw][c]  (A gathered, stride 1)
+//   mode 3  wgrad  dw[oc][k]     = Σ_pix dy[pix][oc] · x̂[pix][k]      (B gathered, split-K over pixels)
+// All on the NS = 3 stage ring of gemm_impl.h.
+#include "gemm_impl.h"
+
+using namespace rn_gemm_detail;
+
+namespace {
+
+template <int BM, int BN, int WM, int WN, int MODE, bool AK, bool BK_>
+void conv_launch(GemmArgs& a, hipStream_t st) {
+    a.tiles_m = (a.M + BM - 1) / BM;
+    a.tiles_n = (a.N + BN - 1) / BN;
+    launch_t<BM, BN, WM, WN, true, AK, BK_, ACT_NONE, 3, MODE>(a, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns 0, or -1 if the geometry is outside the implicit path (caller falls back to im2col).
+int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bias, float* ws, int M, int N, int K,
+                 long lda, long ldb, long ldc, int H, int W, int Cg, int RH, int RW, int KH, int KW, int S, int P,
+                 int KC, int BC, long bld, int split, int out_f32, hipStream_t st) {
+    if (KC % 64 != 0 || K % 64 != 0) return -1;
+    const long pixels = mode == 3 ? K : M;  // the gathered tensor holds pixels / (RH·RW) images
+    if ((long)H * W * Cg * (pixels / ((long)RH * RW) + 1) * 2 >= (1L << 31)) return -1;  // 32-bit offsets
+    GemmArgs a = {};
+    a.A = (const bf16*)A; a.B = (const bf16*)B; a.C = C; a.bias = (const bf16*)bias; a.ws = ws;
+    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.out_f32 = out_f32;
+    ConvGeom& g = a.cv;
+    g.H = H; g.W = W; g.C = Cg; g.RH = RH; g.RW = RW; g.KH = KH; g.KW = KW; g.S = S; g.P = P;
+    g.KC = KC; g.BC = BC; g.bld = bld;
+    g.fd_hw = make_fastdiv((uint32_t)(RH * RW));
+    g.fd_w = make_fastdiv((uint32_t)RW);
+    g.fd_kc = make_fastdiv((uint32_t)KC);
+    g.fd_kw = make_fastdiv((uint32_t)KW);
+    a.split = split < 1 ? 1 : split;
+    int kps = (K + a.split - 1) / a.split;
+    kps = (kps + BK - 1) / BK * BK;
+    a.k_per_split = kps;
+    a.split = (K + kps - 1) / kps;
+    if (mode == 1) {
+        if (N % 64 != 0) return -1;
+        if (N == 64) conv_launch<256, 64, 8, 1, 1, true, true>(a, st);
+        else conv_launch<256, 128, 4, 2, 1, true, true>(a, st);
+        return 0;
+    }
+    if (mode == 2) {
+        if (N % 64 != 0 || S != 1) return -1;
+        if (N == 64) conv_launch<256, 64, 8, 1, 2, true, false>(a, st);
+        else conv_launch<256, 128, 4, 2, 2, true, false>(a, st);
+        return 0;
+    }
+    if (mode == 3) {
+        if (N % 64 != 0 || M % 8 != 0 || lda % 8 != 0) return -1;
+        conv_launch<128, 128, 2, 2, 3, false, false>(a, st);
+        return 0;
+    }
+    return -1;
+}
+
+}  // extern "C"

@@ -13,6 +13,12 @@ columns that read it — deterministic, no atomics).
 1×1 stride-1 convolutions skip im2col entirely (cols = x).  The ViT patch
 embedding (16×16 stride-16) is the non-overlapping case: im2col is a pure
 reshape/permute, done by the same kernel.
+
+Convolutions whose input and output channels are multiples of 64 (all of
+ResNet-18 after the 7×7 stem) take the implicit-GEMM path instead
+(``_ConvImplicitFn``, csrc/kernels/gemm_conv.hip): the GEMM's LDS-DMA loaders
+gather each K-tile (one filter tap × 64 channels) straight from the NHWC
+tensor, so the 9×-sized im2col matrix is never written, read or saved.
 """
 
 from __future__ import annotations
@@ -26,6 +32,49 @@ from .linear import gemm
 
 def _out_hw(H, W, kh, kw, stride, pad):
     return (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+
+
+def implicit_ok(C, OC, KH, KW, stride, pad):
+    """Implicit-GEMM path (no im2col matrix): channels in multiples of 64 (ResNet-18 past the stem)."""
+    return C % 64 == 0 and OC % 64 == 0 and not (KH == 1 and KW == 1 and stride == 1 and pad == 0)
+
+
+class _ConvImplicitFn(torch.autograd.Function):
+    """conv2d whose GEMM loaders gather the filter taps straight from the NHWC activation:
+    fwd (A gathered), wgrad (B gathered, split-K over pixels), dgrad (stride 1: the
+    transposed conv, A = dY gathered; stride 2: dcols GEMM + col2im gather)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad):
+        ops = _ext.ops()
+        x = x.contiguous()
+        w = weight.contiguous()
+        y = ops.conv_fwd_implicit(x, w, bias, stride, pad)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        ops = _ext.ops()
+        N, H, W, C = x.shape
+        OC, KH, KW, _ = w.shape
+        gy = gy.contiguous()
+        gy2 = gy.reshape(-1, OC)
+        gx = gw = gb = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            _, gb = ops.bias_act_grad(gy2, None, 0, True)
+        if ctx.needs_input_grad[1]:
+            gw = ops.conv_wgrad_implicit(gy2, x, KH, KW, ctx.stride, ctx.pad).reshape(OC, KH, KW, C)
+        if ctx.needs_input_grad[0]:
+            if ctx.stride == 1:
+                gx = ops.conv_dgrad_implicit(gy, w, H, W, ctx.pad)
+            else:
+                K = KH * KW * C
+                dcols = gemm(gy2, w.reshape(OC, K), out_dtype=x.dtype)
+                gx = ops.col2im(dcols, N, H, W, C, KH, KW, ctx.stride, ctx.pad, K)
+        return gx, gw, gb, None, None
 
 
 class _ConvFn(torch.autograd.Function):
@@ -73,6 +122,9 @@ class _ConvFn(torch.autograd.Function):
 def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0):
     """x (N,H,W,C), weight (OC,KH,KW,C) → (N,OH,OW,OC)."""
     if _ext.use_native(x):
+        OC, KH, KW, C = weight.shape
+        if implicit_ok(C, OC, KH, KW, int(stride), int(padding)):
+            return _ConvImplicitFn.apply(x, weight, bias, int(stride), int(padding))
         return _ConvFn.apply(x, weight, bias, int(stride), int(padding))
     y = F.conv2d(x.permute(0, 3, 1, 2), weight.permute(0, 3, 1, 2), bias, stride, padding)
     return y.permute(0, 2, 3, 1)

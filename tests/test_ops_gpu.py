@@ -398,6 +398,27 @@ def test_conv2d(cuda, cfg):
         assert rel_err(t.grad, tf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("C,OC,Kk,S,P,HW", [(64, 64, 3, 1, 1, 14), (64, 128, 3, 2, 1, 15), (128, 64, 3, 1, 1, 9),
+                                           (64, 128, 1, 2, 0, 16), (128, 128, 3, 1, 1, 7), (64, 64, 3, 1, 0, 10)])
+def test_conv2d_implicit_gemm(cuda, C, OC, Kk, S, P, HW):
+    """Implicit-GEMM path (channels % 64 == 0): fwd, dgrad (stride 1 implicit / stride 2 col2im), wgrad."""
+    from replicann_amd.ops.conv import implicit_ok
+    assert implicit_ok(C, OC, Kk, Kk, S, P)
+    torch.manual_seed(17)
+    x = bf(3, HW, HW, C).requires_grad_()
+    w = bf(OC, Kk, Kk, C, scale=0.05).requires_grad_()
+    y = ops.conv2d_nhwc(x, w, None, S, P)
+    g = bf(*y.shape)
+    y.backward(g)
+    xf, wf = [t.detach().float().requires_grad_() for t in (x, w)]
+    yf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), None, S, P).permute(0, 2, 3, 1)
+    yf.backward(g.float())
+    assert y.shape == yf.shape
+    assert rel_err(y, yf) < 1e-2
+    assert rel_err(x.grad, xf.grad) < 2e-2
+    assert rel_err(w.grad, wf.grad) < 2e-2
+
+
 @pytest.mark.parametrize("relu", [False, True])
 def test_batchnorm(cuda, relu):
     torch.manual_seed(16)
