@@ -237,8 +237,10 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                                !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
             const int ncfg = plain ? 6 : 5;
             const int cfgs[6] = {0, 1, 6, 2, 8, kLibCfg};
-            const int splits[5] = {1, 2, 4, 8, 16};
-            const int nsplit = split_k < 0 ? 5 : 1;
+            // non-powers of two too: the split that makes tiles × split just fill the 256 CUs
+            // (e.g. 48 tiles × 5 = 240) beats the next power of two by up to 25 %
+            const int splits[9] = {1, 2, 3, 4, 5, 6, 8, 12, 16};
+            const int nsplit = split_k < 0 ? 9 : 1;
             Tensor tws = at::empty({rn_gemm_ws_floats(M, N, 16)}, a.options().dtype(at::kFloat));
             hipEvent_t e0, e1;
             (void)hipEventCreate(&e0);

@@ -164,11 +164,14 @@ __global__ void rn_colred2_k(const float* __restrict__ tmp, int S, int C, long l
 
 // ---------------------------------------------------------------------------
 // Single-launch version: grid (ceil(C/64), S); every block writes its stage-1
-// row of tmp, bumps a per-column-chunk arrival counter (release/acquire at
-// agent scope), and the LAST arriving block of a chunk sums the S rows in fixed
-// order and writes the outputs, then re-arms the counter.  One launch instead
-// of two, still bitwise reproducible.  Outputs may be split into segments of
-// `seg` columns (e.g. [dw | db] of LayerNorm in one pass).
+// row of tmp, bumps a per-column-chunk arrival counter, and the LAST arriving
+// block of a chunk sums the S rows in fixed order and writes the outputs, then
+// re-arms the counter.  One launch instead of two, still bitwise reproducible.
+// Hand-off without fences (MI355X guide §6 G16, R1): the slab values are stored
+// write-through (sc1, agent-scope atomic stores) and drained before the ticket,
+// and the last arriver reads them with sc1 loads — an agent-scope release fence
+// per block (buffer_wbl2, ≈1.7 µs each) made this kernel ~4× slower.  Outputs may
+// be split into segments of `seg` columns (e.g. [dw | db] of LayerNorm in one pass).
 // ---------------------------------------------------------------------------
 constexpr int RN_COLSUM_MAXCB = 4096;
 __device__ unsigned int rn_colsum_cnt[RN_COLSUM_MAXCB];  // zero at load, self-resetting
@@ -181,24 +184,36 @@ struct RnColOut {
 };
 
 __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in, int R, int C,
-                                                   float* __restrict__ tmp, RnColOut out) {
+                                                   float* tmp, RnColOut out) {
     __shared__ float red[4][64];
     __shared__ int is_last;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
     const int S = gridDim.y;
     const int r0 = (int)((long)R * blockIdx.y / S), r1 = (int)((long)R * (blockIdx.y + 1) / S);
+    // Batches of 8 independent loads per lane (one L2/HBM round trip per batch instead of one
+    // per row); the adds stay in row order, so the result does not depend on the batching.
     float s = 0.f;
-    if (c < C)
-        for (int r = r0 + w; r < r1; r += 4) s += in[(long)r * C + c];
+    if (c < C) {
+        for (int rb = r0 + w; rb < r1; rb += 32) {
+            float t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {  // clamped row, no per-load branch (each would wait vmcnt(0))
+                const int r = min(rb + 4 * u, r1 - 1);
+                t[u] = in[(long)r * C + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (rb + 4 * u < r1) ? t[u] : 0.f;
+        }
+    }
     red[w][lane] = s;
     __syncthreads();
     if (w == 0) {
-        if (c < C) tmp[(long)blockIdx.y * C + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        if (c < C)
+            __hip_atomic_store(tmp + (long)blockIdx.y * C + c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 write-through
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores drained
         if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // hipcc may drop the fence's own wait
             unsigned t = __hip_atomic_fetch_add(&rn_colsum_cnt[blockIdx.x], 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
             is_last = (t == (unsigned)S - 1);
@@ -206,23 +221,30 @@ __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in,
     }
     __syncthreads();
     if (!is_last || w != 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
     if (c < C) {
+        // all S (≤ RN_COLRED_S) slab values in flight at once (sc1 loads), summed in fixed order
+        float t[RN_COLRED_S];
+#pragma unroll
+        for (int i = 0; i < RN_COLRED_S; ++i)
+            t[i] = __hip_atomic_load(tmp + (long)min(i, S - 1) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         float acc = 0.f;
-        for (int i = 0; i < S; ++i) acc += __builtin_nontemporal_load(tmp + (long)i * C + c);
+#pragma unroll
+        for (int i = 0; i < RN_COLRED_S; ++i) acc += i < S ? t[i] : 0.f;
         const int k = c / out.seg, o = c - k * out.seg;
         if (out.o32[k]) out.o32[k][o] = acc + (out.accum[k] ? out.o32[k][o] : 0.f);
         if (out.o16[k]) out.o16[k][o] = (__bf16)(acc + (out.accum[k] ? (float)out.o16[k][o] : 0.f));
     }
-    if (lane == 0) rn_colsum_cnt[blockIdx.x] = 0u;
+    if (lane == 0) __hip_atomic_store(&rn_colsum_cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Segmented column reduction: out.seg columns per output segment (≤ 3 segments).
 // tmp must hold RN_COLRED_S * C floats.
 static inline void rn_colreduce_seg(const float* in, int R, int C, float* tmp, const RnColOut& out,
                                     hipStream_t st) {
-    int S = R < RN_COLRED_S ? (R > 0 ? R : 1) : RN_COLRED_S;
+    // >= 32 rows per block (8-deep load batches for each of its 4 waves), at most RN_COLRED_S blocks
+    int S = (R + 31) / 32;
+    S = S < 1 ? 1 : (S > RN_COLRED_S ? RN_COLRED_S : S);
     const int cb = (C + 63) / 64;
     if (cb <= RN_COLSUM_MAXCB) {
         rn_colsum_k<<<dim3(cb, S), 256, 0, st>>>(in, R, C, tmp, out);

@@ -26,7 +26,9 @@ extern "C" {
 int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bias, float* ws, int M, int N, int K,
                  long lda, long ldb, long ldc, int H, int W, int Cg, int RH, int RW, int KH, int KW, int S, int P,
                  int KC, int BC, long bld, int split, int out_f32, hipStream_t st) {
-    if (KC % 64 != 0 || K % 64 != 0) return -1;
+    // the gathered operand's dimension must be whole 64-channel taps: GEMM K for fwd/dgrad,
+    // GEMM N for wgrad (whose K = output pixels has an arbitrary tail, zero-filled by the loaders)
+    if (KC % 64 != 0 || (mode != 3 && K % 64 != 0)) return -1;
     const long pixels = mode == 3 ? K : M;  // the gathered tensor holds pixels / (RH·RW) images
     if ((long)H * W * Cg * (pixels / ((long)RH * RW) + 1) * 2 >= (1L << 31)) return -1;  // 32-bit offsets
     GemmArgs a = {};
