@@ -27,6 +27,7 @@
 // head sizes): straightforward per-query-row kernels with fp32 scores in LDS.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -373,6 +374,181 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     }
 }
 
+// ------------------------- forward v2 (no bias / dropout) -------------------------
+// Same data layout and fragment algebra as attn_fwd64_k; the loop is restructured:
+//   * two loops — tiles every wave of the block sees in full (no mask, no per-wave skip)
+//     and the diagonal / ragged tail (masked).  The single loop's per-wave `continue`
+//     made hipcc carry the accumulators through a phi and copy 34 VGPRs per tile.
+//   * the 16 transposed V reads of a tile are issued right after its QKᵀ MFMAs, so they
+//     land under the softmax VALU work instead of being waited for between PV MFMAs;
+//   * QKᵀ issues the k-step-0 MFMAs of all 8 output tiles before the k-step-1 ones (no
+//     back-to-back dependent MFMAs).
+template <bool CAUSAL, int OCC>
+__global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nqb = gridDim.x;
+    const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heaviest first
+    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const int q0 = qb * 128 + wave * 32;
+    const int off = p.Tk - p.Tq;
+    const float sl2 = p.scale * LOG2E;
+
+    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
+    const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + h * p.k_sh);
+    const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
+
+    int kv_end = p.Tk;
+    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
+    // tiles [0, nfull): every key visible to every query of the block (and Tk-complete)
+    int nfull = p.Tk / 64;
+    if (CAUSAL) nfull = min(nfull, max(0, (qb * 128 + off + 1) / 64));
+    nfull = min(nfull, nkv);
+#define Kt(i) (smem + (i) * 16384)
+#define Vt(i) (smem + 8192 + (i) * 16384)
+    if (nkv > 0) {
+        stage64_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+    }
+    s16x8 qf[2][2];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int row = q0 + qi * 16 + c;
+            qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
+        }
+    asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]));
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    f32x4 oacc[2][4];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    auto tile = [&](const int t, auto masked_c) {
+        constexpr bool MASKED = decltype(masked_c)::value;
+        const int cur = t & 1;
+        const char* kt = Kt(cur);
+        const char* vt = Vt(cur);
+        const int kv0 = t * 64;
+        f32x4 sacc[2][4];
+        s16x8 ka[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ka[j][0] = rowfrag(kt, j * 16 + c, 0, lane);
+            ka[j][1] = rowfrag(kt, j * 16 + c, 1, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
+        // V^T fragments for the PV product, in flight during the softmax
+        s16x8 va[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) va[s][jd] = colfrag(vt, 32 * s, 16 * jd, lane);
+        if constexpr (MASKED) {
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) {
+                const int qg = q0 + qi * 16 + c;
+                const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (kv0 + j * 16 + 4 * g + r > lim) sacc[qi][j][r] = -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) {
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sacc[qi][j][r]);
+            tmax = max4groups(tmax);
+            const float mn = fmaxf(m[qi], tmax);
+            float alpha, nms;
+            if constexpr (MASKED) {
+                const float ms = (mn == -INFINITY) ? 0.f : mn;  // fully-masked rows stay at p = 0
+                alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m[qi] - ms) * sl2);
+                nms = -ms * sl2;
+            } else {  // an unmasked tile has a finite max in every row
+                alpha = __builtin_amdgcn_exp2f((m[qi] - mn) * sl2);  // exp2(-inf) = 0 on the first tile
+                nms = -mn * sl2;
+            }
+            m[qi] = mn;
+            float ls = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[qi][j][r], sl2, nms));
+                    ls += pv;
+                    sacc[qi][j][r] = pv;
+                }
+            l[qi] = l[qi] * alpha + ls;
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alpha;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            s16x8 pb[2];
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd)
+#pragma unroll
+                for (int qi = 0; qi < 2; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
+        }
+    };
+    auto sync_prefetch = [&](int t) {
+        vm_wait_all();   // this wave's DMA of tile t landed ...
+        __syncthreads(); // ... and every wave's; tile t-1's buffer is free
+        if (t + 1 < nkv) {
+            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt((t & 1) ^ 1), wave, lane);
+            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
+        }
+    };
+    int t = 0;
+    for (; t < nfull; ++t) {
+        sync_prefetch(t);
+        tile(t, std::false_type{});
+    }
+    for (; t < nkv; ++t) {
+        sync_prefetch(t);
+        if (CAUSAL && t * 64 > q0 + 31 + off) continue;  // wave-uniform: every query of this wave precedes the tile
+        tile(t, std::true_type{});
+    }
+#undef Kt
+#undef Vt
+    bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+        const float lt = sum4groups(l[qi]);
+        const int qg = q0 + qi * 16 + c;
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        if (qg < p.Tq) {
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                bf16x4 o4 = {(bf16)(oacc[qi][jd][0] * inv), (bf16)(oacc[qi][jd][1] * inv),
+                             (bf16)(oacc[qi][jd][2] * inv), (bf16)(oacc[qi][jd][3] * inv)};
+                *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
+            }
+            if (g == 0)
+                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * sl2 + log2f(lt)) * LN2 : INFINITY;
+        }
+    }
+}
+
 // ============================== backward, D = 64 ==============================
 // delta[b,h,q] = sum_d dO * O  — one thread per (b, q, h) row of D = 64 (8 x 16-B loads each)
 __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
@@ -395,8 +571,8 @@ __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
 }
 
 // dK, dV: grid (ceil(Tk/64), B*H); wave w owns keys kv0 + 16w + (lane&15)
-template <bool CAUSAL, bool BIAS, bool DROP>
-__global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
+template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 3>
+__global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -446,19 +622,25 @@ __global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
     for (int jd = 0; jd < 4; ++jd) { dvacc[jd] = (f32x4){0, 0, 0, 0}; dkacc[jd] = (f32x4){0, 0, 0, 0}; }
 
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
-    for (int qt = qt0; qt < nqt; ++qt) {
+    // Tiles split into masked (causal diagonal of this block's keys, ragged Tq / Tk) and unmasked
+    // ones, each class in its own loop: a per-wave `continue` or a runtime mask branch inside one
+    // loop makes hipcc carry the accumulators through a phi (a VGPR copy block every tile).
+    auto masked_tile = [&](int qt) {
+        return (qt * 64 + 64 > p.Tq) || (kb * 64 + 64 > p.Tk) || (CAUSAL && kb * 64 + 63 > qt * 64 + off);
+    };
+    auto sync_stage = [&](int qt) {
         vm_wait_all();
         __syncthreads();
+        if (qt + 1 < nqt) stage(qt + 1, ((qt - qt0) & 1) ^ 1);
+    };
+    auto body = [&](int qt, auto masked_c) {
+        constexpr bool MASKED = decltype(masked_c)::value;
         const int cur = (qt - qt0) & 1;
-        if (qt + 1 < nqt) stage(qt + 1, cur ^ 1);
         const int q0 = qt * 64;
-        if (CAUSAL && q0 + 63 + off < kvw) continue;  // wave-uniform: all queries precede this wave's keys
         const char* qt_ = Qt(cur);
         const char* ot_ = Ot(cur);
         const float* lt_ = reinterpret_cast<const float*>(Lt(cur));
         const float* dt_ = reinterpret_cast<const float*>(Dt(cur));
-        // masking only where a tile is ragged or crosses the causal diagonal (real branch)
-        const bool need_mask = (q0 + 64 > p.Tq) || (kvw + 16 > p.Tk) || (CAUSAL && kvw + 15 > q0 + off);
         f32x4 pq[4], dsq[4];
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
@@ -494,8 +676,7 @@ __global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
                 dsq[qi][r] = pv * (dpv - dl[r]);
             }
         }
-        if (need_mask) {
-            asm volatile("" ::: "memory");
+        if constexpr (MASKED) {
 #pragma unroll
             for (int qi = 0; qi < 4; ++qi)
 #pragma unroll
@@ -517,6 +698,19 @@ __global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
                 dkacc[jd] = MFMA(aq, sb, dkacc[jd], 0, 0, 0);
             }
         }
+    };
+    int qt = qt0;
+    for (; qt < nqt && masked_tile(qt); ++qt) {  // diagonal head
+        sync_stage(qt);
+        if (!(CAUSAL && qt * 64 + 63 + off < kvw)) body(qt, std::true_type{});  // wave-uniform skip
+    }
+    for (; qt < nqt && !masked_tile(qt); ++qt) {
+        sync_stage(qt);
+        body(qt, std::false_type{});
+    }
+    for (; qt < nqt; ++qt) {  // ragged tail
+        sync_stage(qt);
+        if (!(CAUSAL && qt * 64 + 63 + off < kvw)) body(qt, std::true_type{});
     }
 #undef Qt
 #undef Ot
@@ -543,8 +737,8 @@ __global__ void __launch_bounds__(256, 3) attn_bwd_dkdv64_k(AttnArgs p) {
 }
 
 // dQ: grid (ceil(Tq/64), B*H); wave w owns queries q0 + 16w + (lane&15)
-template <bool CAUSAL, bool BIAS, bool DROP>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
+template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 2>
+__global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -599,16 +793,22 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
         stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
-    for (int t = 0; t < nkv; ++t) {
+    // masked (diagonal / ragged) and unmasked tiles in separate loops, see the dK/dV kernel
+    auto masked_tile = [&](int t) {
+        return (t * 64 + 64 > p.Tk) || (qb * 64 + 64 > p.Tq) || (CAUSAL && t * 64 + 63 > qb * 64 + off);
+    };
+    auto sync_stage = [&](int t) {
         vm_wait_all();
         __syncthreads();
-        const int cur = t & 1;
         if (t + 1 < nkv) {
-            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
-            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
+            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt((t & 1) ^ 1), wave, lane);
+            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
         }
+    };
+    auto body = [&](int t, auto masked_c) {
+        constexpr bool MASKED = decltype(masked_c)::value;
+        const int cur = t & 1;
         const int kv0 = t * 64;
-        if (CAUSAL && kv0 > qw + 15 + off) continue;
         const char* kt = Kt(cur);
         const char* vt = Vt(cur);
         f32x4 dsv[4];
@@ -636,8 +836,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
                 dsv[j][r] = pv * (dpv - dl);
             }
         }
-        if ((kv0 + 64 > p.Tk) || !qok || (CAUSAL && kv0 + 63 > qw + off)) {  // ragged / diagonal tiles only
-            asm volatile("" ::: "memory");
+        if constexpr (MASKED) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -653,6 +852,15 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq64_k(AttnArgs p) {
 #pragma unroll
             for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfrag(kt, 32 * ks, 16 * jd, lane), sb, dqacc[jd], 0, 0, 0);
         }
+    };
+    int t = 0;
+    for (; t < nkv && !masked_tile(t); ++t) {
+        sync_stage(t);
+        body(t, std::false_type{});
+    }
+    for (; t < nkv; ++t) {  // diagonal / ragged tail
+        sync_stage(t);
+        if (!(CAUSAL && t * 64 > qw + 15 + off)) body(t, std::true_type{});  // wave-uniform skip
     }
     if (p.bsum) {  // dQ column partials; row = (b, 64-query block)
         const int E = p.H * 64;
@@ -819,7 +1027,21 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast) {
         dim3 grid((Tq + 127) / 128, B * H);
-        RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
+        // REPLICANN_ATTN_FWD: 1 = original single-loop kernel, 2 (default) = split-loop v2 at 3 blocks/CU,
+        // 3 = v2 at 2 blocks/CU (read per call so one process can A/B them)
+        const char* ev = std::getenv("REPLICANN_ATTN_FWD");
+        const int var = ev ? std::atoi(ev) : 2;
+        if (!bias && p_drop == 0.f && var >= 2) {
+            if (var == 3) {
+                if (causal) attn_fwd64v2_k<true, 2><<<grid, 256, 32768, st>>>(a);
+                else attn_fwd64v2_k<false, 2><<<grid, 256, 32768, st>>>(a);
+            } else {
+                if (causal) attn_fwd64v2_k<true, 3><<<grid, 256, 32768, st>>>(a);
+                else attn_fwd64v2_k<false, 3><<<grid, 256, 32768, st>>>(a);
+            }
+        } else {
+            RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
+        }
     } else {
         if (D > 256 || Tk > 12000) return -1;
         dim3 grid(Tq, B * H);
@@ -850,9 +1072,22 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     if (fast) {
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2((Tq + 63) / 64, B * H);
-        RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         dim3 g1((Tk + 63) / 64, B * H);
-        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
+        // REPLICANN_ATTN_BWD=2: 4 waves per SIMD for both kernels (both fit 128 VGPRs)
+        const char* ev = std::getenv("REPLICANN_ATTN_BWD");
+        const int var = ev ? std::atoi(ev) : 1;
+        if (var == 2 && !bias && p_drop == 0.f) {
+            if (causal) {
+                attn_bwd_dq64_k<true, false, false, 4><<<g2, 256, 32768, st>>>(a);
+                attn_bwd_dkdv64_k<true, false, false, 4><<<g1, 256, 36864, st>>>(a);
+            } else {
+                attn_bwd_dq64_k<false, false, false, 4><<<g2, 256, 32768, st>>>(a);
+                attn_bwd_dkdv64_k<false, false, false, 4><<<g1, 256, 36864, st>>>(a);
+            }
+        } else {
+            RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
+            RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
+        }
     } else {
         if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
         dim3 grid(Tq, B * H);

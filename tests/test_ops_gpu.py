@@ -258,6 +258,18 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
+@pytest.mark.parametrize("fwd,bwd", [("1", "1"), ("2", "1"), ("3", "2")])
+def test_attention_kernel_variants(cuda, monkeypatch, fwd, bwd):
+    """Every D=64 kernel variant (REPLICANN_ATTN_FWD / _BWD) against the fp32 reference, incl. Tq != Tk
+    (causal offset, ragged key blocks) so the masked / unmasked tile loops both run."""
+    monkeypatch.setenv("REPLICANN_ATTN_FWD", fwd)
+    monkeypatch.setenv("REPLICANN_ATTN_BWD", bwd)
+    torch.manual_seed(70)
+    _attn_check(2, 320, 3, 64, True)
+    _attn_check(1, 100, 2, 64, True, Tk=260)
+    _attn_check(1, 130, 2, 64, False, Tk=70)
+
+
 def test_attention_bias_additive(cuda):
     torch.manual_seed(8)
     T = 96
