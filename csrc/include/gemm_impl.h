@@ -544,97 +544,126 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     // The accumulator layout gives each lane 4 consecutive columns of ONE row, so
     // direct stores write 16 rows × 32 B per wave-instruction.  Instead the tile is
     // staged through LDS (row stride BN*2+16 B: 2-way at worst on the b64 writes)
-    // and written back as whole rows, 16 B per lane, with residual / accumulate
-    // read the same coalesced way.  For short-K GEMMs (K = 768) the store tail is
-    // otherwise as long as the main loop.
+    // and written back as whole rows, 16 B per lane.  For short-K GEMMs (K = 768) the
+    // store tail is otherwise as long as the main loop.
+    //   * the one operand the store loop reads (pre-activation for an activation
+    //     backward, else the residual, else the accumulate target) is fetched for ALL
+    //     of a thread's chunks before the staging barrier: its HBM latency overlaps the
+    //     LDS pass instead of being paid once per chunk (a dependent load per 16-B chunk
+    //     serialised ITERS round trips per tile);
+    //   * an activation forward that also saves the pre-activation stages the
+    //     pre-activation once and writes both outputs from it (act of the bf16-rounded
+    //     value, the same value the backward differentiates at): one LDS pass, not two.
     if constexpr (!SPLIT) {
         if (!p.out_f32 && (p.N % 8) == 0 && (p.ldc % 8) == 0) {
             constexpr int STRIDE = BN * 2 + 16;
             constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+            constexpr int NTH = NW * 64;
+            static_assert((BM * CPR) % NTH == 0, "epilogue chunks must divide evenly over the threads");
+            constexpr int ITERS = BM * CPR / NTH;
             const int mlim = min(BM, p.M - m0), nlim = min(BN, p.N - n0);
-            for (int pass = (act_fwd(ACT) && p.pre) ? 0 : 1; pass < 2; ++pass) {
-                __syncthreads();  // main-loop LDS reads (or the previous pass's reads) retired
+            const bool two_out = act_fwd(ACT) && p.pre != nullptr;
+            const bf16* auxp = act_bwd(ACT) ? p.pre
+                               : (p.res ? p.res : (p.accumulate ? (const bf16*)p.C : (const bf16*)nullptr));
+            s16x8 aux[ITERS];
+            if (auxp) {
 #pragma unroll
-                for (int i = 0; i < FM; ++i) {
-                    const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+                for (int it = 0; it < ITERS; ++it) {  // clamped addresses: no per-load branch
+                    const int q = threadIdx.x + it * NTH;
+                    const int r = min(q / CPR, mlim - 1), cc = min(q % CPR, nlim / 8 - 1);
+                    aux[it] = *reinterpret_cast<const s16x8*>(auxp + (long)(m0 + r) * p.ldc + n0 + cc * 8);
+                }
+            }
+            __syncthreads();  // main-loop LDS reads retired
 #pragma unroll
-                    for (int j = 0; j < FN; ++j) {
-                        const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
-                        float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha,
-                                      acc[i][j][3] * alpha};
-                        if (p.bias && n0 + nl < p.N) {
-                            bf16x4 b = *reinterpret_cast<const bf16x4*>(p.bias + n0 + nl);
+            for (int i = 0; i < FM; ++i) {
+                const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) v[t] += (float)b[t];
+                for (int j = 0; j < FN; ++j) {
+                    const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+                    float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha,
+                                  acc[i][j][3] * alpha};
+                    if (p.bias && n0 + nl < p.N) {
+                        bf16x4 b = *reinterpret_cast<const bf16x4*>(p.bias + n0 + nl);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) v[t] += (float)b[t];
+                    }
+                    if constexpr (act_fwd(ACT)) {
+                        if (!two_out) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) v[t] = act_f<ACT>(v[t]);
                         }
-                        if constexpr (act_fwd(ACT)) {
-                            if (pass == 1) {
+                    }
+                    bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+                    *reinterpret_cast<bf16x4*>(smem + ml * STRIDE + nl * 2) = o;
+                }
+            }
+            __syncthreads();
+            bf16* dst = (bf16*)p.C;
+            // column partial sums (act-backward only): with NT % CPR == 0 every thread
+            // always visits the same 8-column chunk, so it sums its rows in registers
+            constexpr bool CSUM_OK = act_bwd(ACT) && colpart_cfg_ok<BN, NTH>();
+            float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                                for (int t = 0; t < 4; ++t) v[t] = act_f<ACT>(v[t]);
-                            }
-                        }
-                        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-                        *reinterpret_cast<bf16x4*>(smem + ml * STRIDE + nl * 2) = o;
+            for (int it = 0; it < ITERS; ++it) {
+                const int q = threadIdx.x + it * NTH;
+                const int r = q / CPR, cc = q % CPR;
+                if (r >= mlim || cc * 8 >= nlim) continue;
+                s16x8 v = *reinterpret_cast<const s16x8*>(smem + r * STRIDE + cc * 16);
+                const long goff = (long)(m0 + r) * p.ldc + n0 + cc * 8;
+                float f[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) f[t] = (float)__builtin_bit_cast(bf16, (short)v[t]);
+                bool changed = false;
+                if constexpr (act_fwd(ACT)) {
+                    if (two_out) {
+                        *reinterpret_cast<s16x8*>(p.pre + goff) = v;
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) f[t] = act_f<ACT>(f[t]);
+                        changed = true;
                     }
                 }
-                __syncthreads();
-                bf16* dst = pass == 0 ? p.pre : (bf16*)p.C;
-                const bool addres = pass == 1 && p.res;
-                const bool accum = pass == 1 && p.accumulate;
-                // column partial sums (act-backward only): with NT % CPR == 0 every thread
-                // always visits the same 8-column chunk, so it sums its rows in registers
-                constexpr bool CSUM_OK = act_bwd(ACT) && colpart_cfg_ok<BN, NW * 64>();
-                float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-                for (int q = threadIdx.x; q < BM * CPR; q += NW * 64) {
-                    const int r = q / CPR, cc = q % CPR;
-                    if (r >= mlim || cc * 8 >= nlim) continue;
-                    s16x8 v = *reinterpret_cast<const s16x8*>(smem + r * STRIDE + cc * 16);
-                    const long goff = (long)(m0 + r) * p.ldc + n0 + cc * 8;
-                    if (addres || accum || act_bwd(ACT)) {
-                        float f[8];
+                if (!auxp) {  // no residual / accumulate / activation-backward operand
+                    if (changed) store8(dst + goff, f);
+                    else *reinterpret_cast<s16x8*>(dst + goff) = v;
+                    continue;
+                }
+                float ax[8];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) f[t] = (float)__builtin_bit_cast(bf16, (short)v[t]);
-                        if constexpr (act_bwd(ACT)) {  // dH = (dY·W) ⊙ act'(pre), pre read row-coalesced
-                            float aux[8];
-                            load8(p.pre + goff, aux);
+                for (int t = 0; t < 8; ++t) ax[t] = (float)__builtin_bit_cast(bf16, (short)aux[it][t]);
+                if constexpr (act_bwd(ACT)) {  // dH = (dY·W) ⊙ act'(pre)
 #pragma unroll
-                            for (int t = 0; t < 8; ++t) f[t] = (float)(bf16)f[t] * act_grad_f<ACT>(aux[t]);
-                            if constexpr (CSUM_OK) {
+                    for (int t = 0; t < 8; ++t) f[t] = (float)(bf16)f[t] * act_grad_f<ACT>(ax[t]);
+                    if constexpr (CSUM_OK) {
 #pragma unroll
-                                for (int t = 0; t < 8; ++t) csum[t] += (float)(bf16)f[t];  // Σ of stored values
-                            }
-                        }
-                        if (addres) {
-                            float rr[8];
-                            load8(p.res + goff, rr);
+                        for (int t = 0; t < 8; ++t) csum[t] += (float)(bf16)f[t];  // Σ of stored values
+                    }
+                } else {
+                    // ax holds the residual if there is one, else the accumulate target
 #pragma unroll
-                            for (int t = 0; t < 8; ++t) f[t] += rr[t];
-                        }
-                        if (accum) {
-                            float cc8[8];
-                            load8(dst + goff, cc8);
+                    for (int t = 0; t < 8; ++t) f[t] += ax[t];
+                    if (p.res && p.accumulate) {
+                        float cc8[8];
+                        load8(dst + goff, cc8);
 #pragma unroll
-                            for (int t = 0; t < 8; ++t) f[t] += cc8[t];
-                        }
-                        store8(dst + goff, f);
-                    } else {
-                        *reinterpret_cast<s16x8*>(dst + goff) = v;
+                        for (int t = 0; t < 8; ++t) f[t] += cc8[t];
                     }
                 }
-                if constexpr (CSUM_OK) {
-                    if (pass == 1 && p.colpart) {  // fold the NT/CPR row-groups of each chunk (fixed order)
-                        constexpr int RG = NW * 64 / CPR;
-                        float* red = reinterpret_cast<float*>(smem);  // [RG][BN]
-                        __syncthreads();  // staged tile fully read
-                        const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
+                store8(dst + goff, f);
+            }
+            if constexpr (CSUM_OK) {
+                if (p.colpart) {  // fold the NT/CPR row-groups of each chunk (fixed order)
+                    constexpr int RG = NTH / CPR;
+                    float* red = reinterpret_cast<float*>(smem);  // [RG][BN]
+                    __syncthreads();  // staged tile fully read
+                    const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) red[rg * BN + cc * 8 + t] = csum[t];
-                        __syncthreads();
-                        for (int col = threadIdx.x; col < BN; col += NW * 64) {
-                            float tot = 0.f;
-                            for (int g2 = 0; g2 < RG; ++g2) tot += red[g2 * BN + col];
-                            if (n0 + col < p.N) p.colpart[(long)tm * p.N + n0 + col] = tot;
-                        }
+                    for (int t = 0; t < 8; ++t) red[rg * BN + cc * 8 + t] = csum[t];
+                    __syncthreads();
+                    for (int col = threadIdx.x; col < BN; col += NTH) {
+                        float tot = 0.f;
+                        for (int g2 = 0; g2 < RG; ++g2) tot += red[g2 * BN + col];
+                        if (n0 + col < p.N) p.colpart[(long)tm * p.N + n0 + col] = tot;
                     }
                 }
             }

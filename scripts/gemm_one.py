@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--split", type=int, default=0)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--torch", action="store_true", help="time torch.matmul (hipBLASLt) instead")
+    ap.add_argument("--act", type=int, default=0,
+                    help="epilogue: 0 none, 2 GELU + pre-activation store (fc fwd), 4 GELU backward reading it")
+    ap.add_argument("--bias", action="store_true")
     a = ap.parse_args()
     ta, tb = a.layout[0] == "t", a.layout[1] == "t"
     torch.manual_seed(0)
@@ -36,7 +39,10 @@ def main():
         Am, Bm = (A.t() if ta else A), (B.t() if tb else B)
         fn = lambda: Am @ Bm  # noqa: E731
     else:
-        fn = lambda: ops.gemm(A, B, ta=ta, tb=tb, cfg=a.cfg, split_k=a.split)  # noqa: E731
+        bias = torch.randn(a.N, device="cuda").bfloat16() if a.bias else None
+        pre = torch.randn(a.M, a.N, device="cuda").bfloat16() if a.act else None
+        fn = lambda: ops.gemm(A, B, ta=ta, tb=tb, cfg=a.cfg, split_k=a.split, bias=bias, act=a.act,  # noqa: E731
+                              preact=pre)
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
@@ -48,7 +54,7 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     print(json.dumps({"M": a.M, "N": a.N, "K": a.K, "layout": a.layout, "cfg": a.cfg, "split": a.split,
-                      "torch": a.torch, "ms": round(ms, 4),
+                      "torch": a.torch, "act": a.act, "ms": round(ms, 4),
                       "tflops": round(2 * a.M * a.N * a.K / ms / 1e9, 1)}), flush=True)
 
 
