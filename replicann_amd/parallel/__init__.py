@@ -24,12 +24,19 @@ def init_distributed(backend=None, timeout_s=600):
     LOCAL_RANK.  CPU → "gloo".  Returns (rank, local_rank, world, device).
     """
     rank, local_rank, world = dist_env()
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
-    if use_gpu:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+    # Rehearsal knobs for a 1-GPU box (never needed on a real node):
+    #   REPLICANN_DIST_BACKEND=gloo  collectives over gloo (GPU tensors staged through the host)
+    #   REPLICANN_SHARE_DEVICE=1     every rank on cuda:0
+    backend = backend or os.environ.get("REPLICANN_DIST_BACKEND") or None
+    gpu = torch.cuda.is_available() and backend != "gloo"
+    share = os.environ.get("REPLICANN_SHARE_DEVICE") == "1"
+    if torch.cuda.is_available() and (gpu or share):
+        dev_idx = 0 if share else local_rank
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
+    use_gpu = gpu
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")

@@ -76,6 +76,7 @@ class DistributedDataParallel(nn.Module):
         self._launched = [False] * len(self.buckets)
         self._next = 0
         self._seen = set()
+        self.launched_in_backward = 0  # buckets whose all-reduce was issued from a gradient hook (last step)
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p, _, _ in segs]
         flat.ready_hooks.append(self._hook)  # parameters whose grads are accumulated directly by kernels
 
@@ -92,9 +93,11 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         self._works = []
         self._seen = set()
+        self.launched_in_backward = 0
 
-    def _launch_ready(self):
+    def _launch_ready(self, from_hook=False):
         while self._next < len(self.buckets) and self._ready[self._next]:
+            self.launched_in_backward += int(from_hook)
             lo, hi, _ = self.buckets[self._next]
             w = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
             self._works.append(w)
@@ -111,7 +114,7 @@ class DistributedDataParallel(nn.Module):
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._ready[bi] = True
-            self._launch_ready()
+            self._launch_ready(from_hook=True)
 
     # ------------------------------------------------------------------
     def forward(self, *args, **kwargs):
