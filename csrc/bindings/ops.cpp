@@ -74,6 +74,7 @@ void rn_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
 void rn_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
 void rn_fp8_quantize(const void*, long, void*, float*, hipStream_t);
 void rn_fp8_dequantize(const void*, long, const float*, void*, hipStream_t);
+void rn_fp8_quantize_delayed(const void*, long, void*, float*, hipStream_t);
 int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
                 int, int, int, long, long, long, int, hipStream_t);
 long rn_bn_ws_floats(int, int);
@@ -763,6 +764,15 @@ std::tuple<Tensor, Tensor> fp8_quantize(const Tensor& x) {
     rn_fp8_quantize(x.data_ptr(), x.numel(), q.data_ptr(), state.data_ptr<float>(), cur_stream());
     return {q, state};
 }
+// delayed scaling: `state` (fp32 [4], persistent per tensor) carries the amax of the previous
+// quantisation; one pass over x (the two-pass fp8_quantize initialises it)
+Tensor fp8_quantize_delayed(const Tensor& x, const Tensor& state) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda());
+    Tensor q = at::empty(x.sizes(), x.options().dtype(at::kByte));
+    rn_fp8_quantize_delayed(x.data_ptr(), x.numel(), q.data_ptr(), state.data_ptr<float>(), cur_stream());
+    return q;
+}
 Tensor fp8_dequantize(const Tensor& q, const Tensor& state) {
     GUARD(q);
     Tensor y = at::empty(q.sizes(), q.options().dtype(at::kBFloat16));
@@ -837,6 +847,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu) -> (Tensor, Tensor, Tensor)");
     m.def("fp8_quantize(Tensor x) -> (Tensor, Tensor)");
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
+    m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("native_version() -> int");
     m.def("gemm_tuning_table() -> str");
@@ -879,6 +890,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("batchnorm_bwd", &batchnorm_bwd);
     m.impl("fp8_quantize", &fp8_quantize);
     m.impl("fp8_dequantize", &fp8_dequantize);
+    m.impl("fp8_quantize_delayed", &fp8_quantize_delayed);
     m.impl("gemm_fp8", &gemm_fp8);
 }
 

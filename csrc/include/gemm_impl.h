@@ -136,12 +136,16 @@ RN_DEV s16x8 frag(const char* lds, int mnbase, int s, int lane) {
     }
 }
 
-RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, int& tn) {
-    // XCD remap (bijective for any nblocks): blocks sharing bid%8 get a contiguous id range
+// XCD remap (bijective for any nblocks): the dispatcher deals block ids round-robin over the
+// 8 XCDs, so blocks sharing bid%8 share an L2; give each such group a contiguous id range.
+RN_DEV int xcd_remap(int bid, int nblocks) {
     const int xcd = bid & 7, loc = bid >> 3;
     const int q = nblocks >> 3, r = nblocks & 7;
-    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-    // grouped ordering: GROUP_M tile-rows share B panels
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// grouped ordering of a linear tile id: GROUP_M tile-rows share B panels
+RN_DEV void group_tile(int id, int tiles_m, int tiles_n, int& tm, int& tn) {
     const int per_group = GROUP_M * tiles_n;
     const int gid = id / per_group;
     const int first_m = gid * GROUP_M;
@@ -149,6 +153,10 @@ RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, in
     const int in = id % per_group;
     tm = first_m + in % gsz;
     tn = in / gsz;
+}
+
+RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, int& tn) {
+    group_tile(xcd_remap(bid, nblocks), tiles_m, tiles_n, tm, tn);
 }
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -293,10 +301,17 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     const int wm = wave / WN, wn = wave % WN;
 
     const int tiles = p.tiles_m * p.tiles_n;
-    const int split_id = SPLIT ? blockIdx.x / tiles : 0;
-    const int tb = SPLIT ? blockIdx.x % tiles : blockIdx.x;
-    int tm, tn;
-    map_tile(tb, tiles, p.tiles_m, p.tiles_n, tm, tn);
+    int split_id = 0, tm, tn;
+    if constexpr (SPLIT) {
+        // remap over the WHOLE grid first, then split = id / tiles: an XCD then holds a contiguous
+        // run of tiles of the same K-slice, which share A and B panels in its L2 (decomposing
+        // blockIdx first scattered a tile group over all XCDs whenever tiles % 8 != 0)
+        const int id = xcd_remap(blockIdx.x, tiles * p.split);
+        split_id = id / tiles;
+        group_tile(id % tiles, p.tiles_m, p.tiles_n, tm, tn);
+    } else {
+        map_tile(blockIdx.x, tiles, p.tiles_m, p.tiles_n, tm, tn);
+    }
     const int m0 = tm * BM, n0 = tn * BN;
     const int kbeg = split_id * p.k_per_split;
     const int kend = min(p.K, kbeg + p.k_per_split);

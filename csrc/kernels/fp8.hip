@@ -54,6 +54,46 @@ __global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long 
     }
 }
 
+// Delayed scaling (one pass over x): the scale comes from the amax recorded by the PREVIOUS
+// quantisation of this tensor (x2 headroom), and this pass records the current amax for the
+// next one.  state: [0] scale used, [1] amax of the last pass, [2] amax the scale came from.
+__global__ void fp8_roll_k(float* __restrict__ state) {
+    const float a = state[1];
+    state[2] = a;
+    state[0] = a > 0.f ? 2.f * a / E4M3_MAX : 1.f;
+    state[1] = 0.f;
+}
+
+__global__ void __launch_bounds__(256) quant_delayed_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
+                                                       float* __restrict__ state) {
+    __shared__ float sm[16];
+    const float inv = 1.f / state[0];
+    float m = 0.f;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(x + i * 8, f);
+        int w0 = 0, w1 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            m = fmaxf(m, fabsf(f[j]));
+            f[j] = fminf(fmaxf(f[j] * inv, -E4M3_MAX), E4M3_MAX);
+        }
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+        *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    }
+    for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float v = bf2f(x[i]);
+        m = fmaxf(m, fabsf(v));
+        const float f = fminf(fmaxf(v * inv, -E4M3_MAX), E4M3_MAX);
+        q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(f, 0.f, 0, false) & 0xFF);
+    }
+    m = block_max(m, sm);
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
+}
+
 __global__ void dequant_k(const uint8_t* __restrict__ q, long n, const float* __restrict__ state,
                           bf16* __restrict__ y) {
     const float scale = state[0];
@@ -80,6 +120,12 @@ void rn_fp8_quantize(const void* x, long n, void* q, float* state, hipStream_t s
     (void)hipMemsetAsync(state, 0, 2 * sizeof(float), st);
     amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
     quant_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
+}
+
+// One-pass delayed-scaling quantisation (state as fp8_roll_k / quant_delayed_k); graph-capturable.
+void rn_fp8_quantize_delayed(const void* x, long n, void* q, float* state, hipStream_t st) {
+    fp8_roll_k<<<1, 1, 0, st>>>(state);
+    quant_delayed_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
 
 void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {

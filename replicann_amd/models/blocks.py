@@ -31,7 +31,8 @@ from .. import ops
 class Linear(nn.Module):
     """nn.Linear-compatible parameters (weight (out, in), bias (out,)) on the MFMA GEMM.
 
-    ``fp8=True`` runs the forward GEMM in fp8 e4m3 (ops.linear_fp8)."""
+    ``fp8=True`` runs the forward GEMM in fp8 e4m3 with delayed scaling (ops.fp8.Fp8State);
+    the backward is the bf16 one either way."""
 
     def __init__(self, in_features, out_features, bias=True, std=0.02, fp8=False):
         super().__init__()
@@ -39,12 +40,11 @@ class Linear(nn.Module):
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
         self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
         self.fp8 = fp8
+        self.fp8_state = ops.Fp8State() if fp8 else None
         nn.init.normal_(self.weight, std=std)
 
     def forward(self, x, act=None, residual=None):
-        if self.fp8:
-            return ops.linear_fp8(x, self.weight, self.bias, act=act, residual=residual)
-        return ops.linear(x, self.weight, self.bias, act=act, residual=residual)
+        return ops.linear(x, self.weight, self.bias, act=act, residual=residual, fp8=self.fp8_state)
 
 
 class LayerNorm(nn.Module):
@@ -76,7 +76,7 @@ class Attention(nn.Module):
         qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
         a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
                                  training=self.training,
-                                 producer_bias=None if self.c_attn.fp8 else self.c_attn.bias)
+                                 producer_bias=self.c_attn.bias)
         a = a.reshape(B, T, E)
         if self.resid_dropout > 0 and self.training:
             return residual + ops.dropout(self.c_proj(a), self.resid_dropout, True)
@@ -97,11 +97,10 @@ class MLP(nn.Module):
         if self.dropout > 0 and self.training:
             u = self.c_fc(h, act="gelu")
             return residual + ops.dropout(self.c_proj(u), self.dropout, True)
-        if self.c_fc.fp8 or self.c_proj.fp8:
-            return self.c_proj(self.c_fc(h, act="gelu"), residual=residual)
         # one autograd node: GELU backward fused into the c_proj dgrad GEMM epilogue
+        fp8 = (self.c_fc.fp8_state, self.c_proj.fp8_state) if self.c_fc.fp8 else None
         return ops.mlp(h, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias, "gelu",
-                       residual=residual)
+                       residual=residual, fp8=fp8)
 
 
 class PreLNBlock(nn.Module):

@@ -1,12 +1,12 @@
 """FP8 (OCP e4m3fn) linear layers on the CDNA4 block-scaled MFMA (csrc/kernels/fp8.hip) — N3.
 
-``linear_fp8`` runs the FORWARD GEMM in fp8: activations and weights are
-quantised per tensor with current scaling (amax → scale = amax/448, computed
-on device), multiplied by ``v_mfma_scale_f32_16x16x128_f8f6f4`` at twice the
-bf16 MFMA rate, and the two tensor scales are folded into the epilogue alpha
-together with bias / GELU / residual.  The backward keeps the bf16 master
-weight and bf16 gradients (dgrad/wgrad on the bf16 MFMA GEMM), the recipe
-used for "fp8 weights" training in BASELINE.json's GPT-2-medium config.
+``linear_fp8`` (and ``linear`` / ``mlp`` with an ``fp8=`` state) runs the FORWARD
+GEMM in fp8: activations and weights are quantised per tensor (delayed scaling,
+see :class:`Fp8State`), multiplied by ``v_mfma_scale_f32_16x16x128_f8f6f4`` at
+twice the bf16 MFMA rate, and the two tensor scales are folded into the epilogue
+alpha together with bias / GELU / residual.  The backward is the bf16 one (bf16
+master weight, bf16 gradients, fused activation-backward / bias reductions), the
+recipe used for "fp8 weights" training in BASELINE.json's GPT-2-medium config.
 
 CPU tensors emulate the numerics (quantise → dequantise → fp32 matmul).
 """
@@ -16,7 +16,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
-from .linear import ACT_NONE, _ACTS, _act_ref, bias_act_grad, gemm
+from .linear import _act_ref
 
 E4M3_MAX = 448.0
 
@@ -37,50 +37,53 @@ def dequantize_fp8(q, state):
     return (q.view(torch.float8_e4m3fn).float() * state[0]).to(torch.bfloat16)
 
 
-class _LinearFp8Fn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, bias, act, residual):
-        shp = x.shape
-        x2 = x.reshape(-1, shp[-1]).contiguous()
-        res2 = residual.reshape(-1, weight.shape[0]).contiguous() if residual is not None else None
-        xq, xs = quantize_fp8(x2)
-        wq, ws = quantize_fp8(weight)
-        preact = None
-        if act != ACT_NONE:
-            preact = torch.empty(x2.shape[0], weight.shape[0], device=x.device, dtype=x.dtype)
-        if _ext.use_native(x2):
-            y = _ext.ops().gemm_fp8(xq, wq, xs, ws, bias, res2, act, preact)
-        else:
-            h = dequantize_fp8(xq, xs).float() @ dequantize_fp8(wq, ws).float().t()
-            if bias is not None:
-                h = h + bias.float()
-            if preact is not None:
-                preact.copy_(h)
-            y = _act_ref(h, act)
-            if res2 is not None:
-                y = y + res2.float()
-            y = y.to(x.dtype)
-        ctx.save_for_backward(x2, weight, preact)
-        ctx.act, ctx.has_bias, ctx.has_res, ctx.shp = act, bias is not None, residual is not None, shp
-        ctx.bias_ref = bias
-        return y.reshape(*shp[:-1], weight.shape[0])
+class Fp8State:
+    """Scaling state of one fp8 GEMM's two forward operands (activation, weight).
 
-    @staticmethod
-    def backward(ctx, gy):
-        x2, weight, preact = ctx.saved_tensors
-        gy2 = gy.reshape(-1, weight.shape[0]).contiguous()
-        want_b = ctx.has_bias
-        if want_b and getattr(ctx.bias_ref, "_rn_bias_done", False):  # see ops.norm._LayerNormFn
-            ctx.bias_ref._rn_bias_done = False
-            want_b = False
-        dh, db = bias_act_grad(gy2, preact, ctx.act, want_b)
-        gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
-        gw = gemm(dh, x2, ta=True, split_k=-1, out_dtype=weight.dtype) if ctx.needs_input_grad[1] else None
-        gb = db.to(weight.dtype) if (db is not None and ctx.needs_input_grad[2]) else None
-        return gx, gw, gb, None, (gy if ctx.has_res else None)
+    The first quantisation of each operand uses current scaling (amax pass + quantise
+    pass) and records the amax in a persistent device tensor; every later one is a
+    single pass with delayed scaling: the scale comes from the previous quantisation's
+    amax (x2 headroom, saturating beyond it) and the pass records the new amax
+    (``fp8_quantize_delayed``) — the Transformer-Engine recipe with a history of one.
+    Everything is on device, so a captured step graph replays it unchanged."""
+
+    def __init__(self):
+        self.t = None
+        self.ready = [False, False]
+
+    def quant(self, x, i):
+        if self.t is None or self.t.device != x.device:
+            self.t = torch.zeros(2, 4, device=x.device, dtype=torch.float32)
+            self.ready = [False, False]
+        st = self.t[i]
+        if not self.ready[i] or not _ext.use_native(x):
+            q, s = quantize_fp8(x)
+            st.copy_(s)
+            self.ready[i] = True
+            return q, st
+        return _ext.ops().fp8_quantize_delayed(x, st), st
 
 
-def linear_fp8(x, weight, bias=None, act=None, residual=None):
-    """Linear with an fp8 e4m3 forward GEMM (per-tensor current scaling)."""
-    a = _ACTS[act] if not isinstance(act, int) else act
-    return _LinearFp8Fn.apply(x, weight, bias, a, residual)
+def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State):
+    """act(x2·weightᵀ + bias) + res2 with both operands in e4m3 (GPU: block-scaled MFMA;
+    CPU: the same quantise → dequantise numerics in fp32)."""
+    xq, xs = state.quant(x2, 0)
+    wq, ws = state.quant(weight.contiguous(), 1)
+    if _ext.use_native(x2):
+        return _ext.ops().gemm_fp8(xq, wq, xs, ws, bias, res2, act, preact)
+    h = dequantize_fp8(xq, xs).float() @ dequantize_fp8(wq, ws).float().t()
+    if bias is not None:
+        h = h + bias.float()
+    if preact is not None:
+        preact.copy_(h)
+    y = _act_ref(h, act)
+    if res2 is not None:
+        y = y + res2.float()
+    return y.to(x2.dtype)
+
+
+def linear_fp8(x, weight, bias=None, act=None, residual=None, state: Fp8State | None = None):
+    """Linear with an fp8 e4m3 forward GEMM; the backward is the bf16 linear's
+    (ops.linear: direct flat-buffer gradient accumulation, fused bias reduction)."""
+    from .linear import linear
+    return linear(x, weight, bias, act=act, residual=residual, fp8=state if state is not None else Fp8State())

@@ -136,7 +136,7 @@ def _pick_split_k(m_out: int, n_out: int, k: int) -> int:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, act, residual):
+    def forward(ctx, x, weight, bias, act, residual, fp8=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if not x2.is_contiguous():
@@ -146,7 +146,12 @@ class _LinearFn(torch.autograd.Function):
         preact = None
         if act != ACT_NONE:
             preact = torch.empty(x2.shape[0], weight.shape[0], device=x.device, dtype=x.dtype)
-        if native:
+        if fp8 is not None:
+            from .fp8 import fp8_forward
+            if res2 is not None and not res2.is_contiguous():
+                res2 = res2.contiguous()
+            y = fp8_forward(x2, weight, bias, res2, act, preact, fp8)
+        elif native:
             y = _ext.ops().gemm(x2, weight, False, True, bias, res2, act, preact, None, False, 0, False, None, -1)
         else:
             y = gemm(x2, weight, tb=True, bias=bias, residual=res2, act=act, preact=preact,
@@ -193,15 +198,16 @@ class _LinearFn(torch.autograd.Function):
             else:
                 gb = db.to(weight.dtype)
         gres = gy if ctx.has_res else None
-        return gx, gw, gb, None, gres
+        return gx, gw, gb, None, gres, None
 
 
-def linear(x, weight, bias=None, act=None, residual=None):
-    """y = act(x @ weightᵀ + bias) [+ residual].  ``act`` ∈ {None,'relu','gelu'}."""
+def linear(x, weight, bias=None, act=None, residual=None, fp8=None):
+    """y = act(x @ weightᵀ + bias) [+ residual].  ``act`` ∈ {None,'relu','gelu'}.
+    ``fp8``: an :class:`~replicann_amd.ops.fp8.Fp8State` → the forward GEMM runs in e4m3."""
     a = _ACTS[act] if not isinstance(act, int) else act
-    if not x.is_cuda and not torch.is_grad_enabled() and residual is None and a == ACT_NONE:
+    if fp8 is None and not x.is_cuda and not torch.is_grad_enabled() and residual is None and a == ACT_NONE:
         return F.linear(x, weight, bias)
-    return _LinearFn.apply(x, weight, bias, a, residual)
+    return _LinearFn.apply(x, weight, bias, a, residual, fp8)
 
 
 # --------------------------------------------------------------------------
@@ -243,14 +249,19 @@ class _MLPFn(torch.autograd.Function):
     separate activation-backward pass over dU (read dU + pre, write dH) is gone."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, act, residual):
+    def forward(ctx, x, w1, b1, w2, b2, act, residual, fp8=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).contiguous()
         res2 = residual.reshape(-1, w2.shape[0]).contiguous() if residual is not None else None
         ops = _ext.ops()
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
-        u = ops.gemm(x2, w1, False, True, b1, None, act, pre, None, False, 0, False, None, -1)
-        y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)
+        if fp8 is not None:  # (state of layer 1, state of layer 2): e4m3 forward GEMMs
+            from .fp8 import fp8_forward
+            u = fp8_forward(x2, w1, b1, None, act, pre, fp8[0])
+            y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
+        else:
+            u = ops.gemm(x2, w1, False, True, b1, None, act, pre, None, False, 0, False, None, -1)
+            y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)
         ctx.save_for_backward(x2, w1, pre, u, w2)
         ctx.b1, ctx.b2, ctx.act, ctx.shp, ctx.has_res = b1, b2, act, shp, residual is not None
         return y.reshape(*shp[:-1], w2.shape[0])
@@ -279,12 +290,14 @@ class _MLPFn(torch.autograd.Function):
         gw1 = _wgrad(dh, x2, w1, True) if nig[1] else None
         gx = ops.gemm(dh, w1, False, False, None, None, ACT_NONE, None, None, False, 0, False, None, -1)
         return (gx.reshape(ctx.shp) if nig[0] else None, gw1, gb1, gw2, gb2, None,
-                gy if ctx.has_res else None)
+                gy if ctx.has_res else None, None)
 
 
-def mlp(x, w1, b1, w2, b2, act="gelu", residual=None):
-    """act(x·W1ᵀ + b1)·W2ᵀ + b2 [+ residual] — fused backward on GPU, plain linears on CPU."""
+def mlp(x, w1, b1, w2, b2, act="gelu", residual=None, fp8=None):
+    """act(x·W1ᵀ + b1)·W2ᵀ + b2 [+ residual] — fused backward on GPU, plain linears on CPU.
+    ``fp8``: (Fp8State, Fp8State) of the two layers → e4m3 forward GEMMs."""
     a = _ACTS[act] if not isinstance(act, int) else act
     if _ext.use_native(x) and a in ACT_BWD:
-        return _MLPFn.apply(x, w1, b1, w2, b2, a, residual)
-    return linear(linear(x, w1, b1, act=a), w2, b2, residual=residual)
+        return _MLPFn.apply(x, w1, b1, w2, b2, a, residual, fp8)
+    f1, f2 = fp8 if fp8 is not None else (None, None)
+    return linear(linear(x, w1, b1, act=a, fp8=f1), w2, b2, residual=residual, fp8=f2)

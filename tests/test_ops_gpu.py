@@ -505,3 +505,41 @@ def test_linear_fp8_autograd(cuda):
     assert rel_err(y, yref) < 0.05
     y.float().pow(2).mean().backward()
     assert all(torch.isfinite(t.grad.float()).all() for t in (x, w, b))
+
+
+def test_fp8_delayed_scaling(cuda):
+    """One-pass delayed scaling: scale = 2·amax(previous quantisation)/448, the pass records the new
+    amax; values beyond the headroom saturate at ±448·scale."""
+    torch.manual_seed(23)
+    st = ops.Fp8State()
+    x0 = bf(256, 512, scale=2.0)
+    q0, s0 = st.quant(x0, 0)  # first call: current scaling
+    amax0 = x0.float().abs().max().item()
+    assert abs(s0[1].item() - amax0) < 1e-3 * amax0
+    x1 = bf(256, 512, scale=2.5)
+    q1, s1 = st.quant(x1, 0)  # delayed: scale from amax0
+    assert abs(s1[0].item() - 2 * amax0 / 448) < 1e-6 * amax0
+    assert abs(s1[1].item() - x1.float().abs().max().item()) < 1e-3 * amax0  # new amax recorded
+    y1 = ops.dequantize_fp8(q1, s1)
+    assert rel_err(y1, x1) < 0.06
+    x2 = bf(256, 512, scale=40.0)  # far beyond the headroom: saturates, stays finite
+    q2, s2 = st.quant(x2, 0)
+    y2 = ops.dequantize_fp8(q2, s2)
+    assert torch.isfinite(y2.float()).all() and y2.float().abs().max().item() <= 448 * s2[0].item() * 1.001
+
+
+def test_mlp_fp8_matches_bf16(cuda):
+    """Fused MLP node with e4m3 forward GEMMs (delayed scaling after the first call) vs bf16."""
+    torch.manual_seed(24)
+    x = bf(2, 128, 256)
+    w1, b1 = bf(1024, 256, scale=0.05), bf(1024, scale=0.1)
+    w2, b2 = bf(256, 1024, scale=0.05), bf(256, scale=0.1)
+    r = bf(2, 128, 256)
+    states = (ops.Fp8State(), ops.Fp8State())
+    ref = ops.mlp(x, w1, b1, w2, b2, "gelu", residual=r)
+    for _ in range(3):  # first call current scaling, then delayed
+        xs = x.clone().requires_grad_()
+        y = ops.mlp(xs, w1, b1, w2, b2, "gelu", residual=r, fp8=states)
+        assert rel_err(y, ref) < 0.05
+    y.float().pow(2).mean().backward()
+    assert torch.isfinite(xs.grad.float()).all()
