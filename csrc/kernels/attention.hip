@@ -202,9 +202,11 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nqb = gridDim.x;
-    const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heaviest first
-    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    // grid (B*H, blocks): the block index varies SLOWEST, so under causal masking every head's
+    // heaviest query block is dispatched before any lighter one (longest-first over the grid)
+    const int nqb = gridDim.y;
+    const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
+    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
     const int q0 = qb * 128 + wave * 32;
     const int off = p.Tk - p.Tq;  // causal: key j visible to query i iff j <= i + off
     const float sl2 = p.scale * LOG2E;
@@ -388,9 +390,11 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nqb = gridDim.x;
-    const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heaviest first
-    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    // grid (B*H, blocks): the block index varies SLOWEST, so under causal masking every head's
+    // heaviest query block is dispatched before any lighter one (longest-first over the grid)
+    const int nqb = gridDim.y;
+    const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
+    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
     const int q0 = qb * 128 + wave * 32;
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
@@ -576,8 +580,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int kb = blockIdx.x;  // low key blocks see the most queries under causal: they launch first
-    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    // grid (B*H, key blocks): low key blocks see the most queries under causal and, with the block
+    // index varying slowest, launch first across ALL heads (longest-first)
+    const int kb = blockIdx.y;
+    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
     const int kvw = kb * 64 + wave * 16;  // this wave's first key
     const int kv = kvw + c;
     const int off = p.Tk - p.Tq;
@@ -718,7 +724,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
 #undef Dt
     if (p.bsum) {  // dK / dV column partials for the QKV bias gradient
         const int E = p.H * 64;
-        float* row = p.bsum + ((long)b * gridDim.x + kb) * 3 * E + h * 64;
+        float* row = p.bsum + ((long)b * gridDim.y + kb) * 3 * E + h * 64;
         block_colsum64(dkacc, p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
         block_colsum64(dvacc, 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
     }
@@ -742,9 +748,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nqb = gridDim.x;
-    const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
-    const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const int nqb = gridDim.y;  // grid (B*H, query blocks): heaviest blocks of every head first
+    const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
+    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
     const int qw = qb * 64 + wave * 16;
     const int qg = qw + c;
     const int off = p.Tk - p.Tq;
@@ -864,7 +870,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     }
     if (p.bsum) {  // dQ column partials; row = (b, 64-query block)
         const int E = p.H * 64;
-        float* row = p.bsum + ((long)b * gridDim.x + qb) * 3 * E + h * 64;
+        float* row = p.bsum + ((long)b * gridDim.y + qb) * 3 * E + h * 64;
         block_colsum64(dqacc, p.scale, reinterpret_cast<float*>(smem), row, wave, lane);
     }
     if (qok) {
@@ -1026,7 +1032,7 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     a.scale = scale; a.p_drop = p_drop; a.seed = seed;
     const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast) {
-        dim3 grid((Tq + 127) / 128, B * H);
+        dim3 grid(B * H, (Tq + 127) / 128);
         // REPLICANN_ATTN_FWD: 1 = original single-loop kernel, 2 (default) = split-loop v2 at 3 blocks/CU,
         // 3 = v2 at 2 blocks/CU (read per call so one process can A/B them)
         const char* ev = std::getenv("REPLICANN_ATTN_FWD");
@@ -1071,8 +1077,8 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     if (bsum && !(fast && Tq == Tk)) return -2;  // bias partials: fast self-attention path only
     if (fast) {
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
-        dim3 g2((Tq + 63) / 64, B * H);
-        dim3 g1((Tk + 63) / 64, B * H);
+        dim3 g2(B * H, (Tq + 63) / 64);
+        dim3 g1(B * H, (Tk + 63) / 64);
         // REPLICANN_ATTN_BWD=2: 4 waves per SIMD for both kernels (both fit 128 VGPRs)
         const char* ev = std::getenv("REPLICANN_ATTN_BWD");
         const int var = ev ? std::atoi(ev) : 1;
