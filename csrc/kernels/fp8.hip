@@ -138,7 +138,7 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
                 int act, hipStream_t st) {
     if (K % 16 || lda % 16 || ldb % 16) return -1;
     scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
-    rn_gemm_detail::GemmArgs a;
+    rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
     a.pre = (bf16*)pre; a.ws = nullptr; a.alpha = alpha_ws;
     a.M = M; a.N = N; a.K = K / 2; a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;

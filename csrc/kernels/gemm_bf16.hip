@@ -39,6 +39,8 @@
 // Block→tile mapping is XCD-aware: the round-robin dispatcher puts blocks b
 // and b+8 on one XCD, so block ids are remapped (bijectively) to give each
 // XCD a contiguous run of tiles, walked in GROUP_M-row groups for L2 reuse.
+#include <cstdlib>
+
 #include "common.h"
 
 #include "gemm_impl.h"
@@ -118,7 +120,7 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     if (!trans_a && lda % 8 != 0) return -1;
     if (!trans_b && (N % 8 != 0 || ldb % 8 != 0)) return -1;
     if (trans_b && ldb % 8 != 0) return -1;
-    GemmArgs a;
+    GemmArgs a = {};
     a.A = (const bf16*)A; a.B = (const bf16*)B; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
     a.pre = (bf16*)pre; a.ws = ws; a.alpha = alpha; a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
     if (cfg < 0 || split < 0) {
@@ -133,6 +135,7 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     a.split = (K + kps - 1) / kps;
     a.out_f32 = out_f32; a.accumulate = accumulate;
     a.colpart = colpart;
+
     if (colpart && (!act_bwd(act) || a.split > 1 || out_f32 || N % 8 != 0 || ldc % 8 != 0 || cfg == 6 || cfg == 4 ||
                     cfg == 3))
         return -3;  // 256x192 (CPR 24) and the simple 256-wide configs are not wired for it
