@@ -6,6 +6,8 @@
 //   fwd:  h = x (+ r);  y = (h - mu) * rstd * w + b;  saves mu, rstd (fp32)
 //   bwd:  dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) (+ gh),  g = dy * w
 //         dw, db: per-wave fp32 partial rows, reduced in fixed order (deterministic).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -192,7 +194,18 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
     return 0;
 }
 
-int rn_ln_bwd_blocks(int M) { int W = M < 2048 ? M : 2048; return (W + 3) / 4; }
+// waves of the backward grid (each loops over rows): enough to keep HBM busy on a latency-bound
+// row loop; REPLICANN_LN_BWD_WAVES overrides (A/B)
+int rn_ln_bwd_blocks(int M) {
+    static int cap = -1;
+    if (cap < 0) {
+        const char* e = std::getenv("REPLICANN_LN_BWD_WAVES");
+        cap = e ? std::atoi(e) : 8192;
+        if (cap < 4) cap = 4;
+    }
+    int W = M < cap ? M : cap;
+    return (W + 3) / 4;
+}
 int rn_ln_bwd_waves(int M) { return 4 * rn_ln_bwd_blocks(M); }
 
 // workspace floats: partial rows [blocks][3E] + the reduction's [RN_COLRED_S][3E] scratch
