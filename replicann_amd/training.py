@@ -261,7 +261,10 @@ class Trainer:
 
 
 def train(config: TrainConfig | None = None, model=None, **kw):
-    """Train a replicated model; returns a summary dict."""
+    """Train a replicated model; returns a summary dict.  ``model`` is an nn.Module to train, or a
+    model name (same as ``TrainConfig.model``, e.g. ``train(model="gpt2-small", steps=100)``)."""
+    if isinstance(model, str):
+        kw["model"], model = model, None
     cfg = config or TrainConfig(**kw)
     return Trainer(cfg, model=model).run()
 
@@ -284,6 +287,27 @@ def evaluate(model, data, steps=10):
         n += 1
     model.train(was)
     return {"loss": tot / n, "accuracy": acc / n}
+
+
+def eval_main(argv=None):
+    """``python -m replicann.eval``: mean loss (+ accuracy) of a model — random init, or a
+    checkpoint written by ``train(checkpoint=...)`` — over synthetic batches."""
+    ap = argparse.ArgumentParser(description="replicann evaluation entrypoint")
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--batch-size", type=int, default=8)
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--model-kwargs", type=json.loads, default={})
+    a = ap.parse_args(argv)
+    cfg = TrainConfig(model=a.model, batch_size=a.batch_size, seq_len=a.seq_len, steps=1, device=a.device,
+                      resume=a.checkpoint, model_kwargs=a.model_kwargs, graph="off")
+    tr = Trainer(cfg)
+    out = evaluate(tr.model, tr.data, steps=a.steps)
+    if is_rank0():
+        print(json.dumps({"model": a.model, **out}))
+    return out
 
 
 def main(argv=None):
