@@ -248,6 +248,9 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             (void)hipEventCreate(&e1);
             float best_ms = 1e30f;
             int best_cfg = 0, best_split = 1;
+            // two interleaved rounds over all candidates, best-of per candidate: one round's
+            // clock / cache transients otherwise flip close calls (e.g. library vs MFMA kernel)
+            for (int round = 0; round < 2; ++round)
             for (int ci = 0; ci < ncfg; ++ci) {
                 for (int si = 0; si < nsplit; ++si) {
                     const int sp = splits[si];
