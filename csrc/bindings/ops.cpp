@@ -67,9 +67,8 @@ int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int,
                  int, int, int, int, int, int, int, int, int, long, int, int, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
-void rn_maxpool_fwd(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
-void rn_maxpool_bwd(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int,
-                    hipStream_t);
+void rn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+void rn_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
 void rn_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
 void rn_fp8_quantize(const void*, long, void*, float*, hipStream_t);
@@ -78,12 +77,13 @@ void rn_fp8_quantize_delayed(const void*, long, void*, float*, hipStream_t);
 int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
                 int, int, int, long, long, long, int, hipStream_t);
 long rn_bn_ws_floats(int, int);
+int rn_bn_supported(int);
 void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, float*, float*, float*, int, int, float,
-               float, int, hipStream_t);
+               float, int, const void*, hipStream_t);
 void rn_bn_eval(const void*, const void*, const void*, const float*, const float*, void*, int, int, float, int,
-                hipStream_t);
-void rn_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
-               float*, int, int, int, hipStream_t);
+                const void*, hipStream_t);
+void rn_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
+               float*, int, int, int, void*, hipStream_t);
 }
 
 namespace {
@@ -196,10 +196,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                     "activation-backward epilogue: dgrad layout (A·B, B [K][N]), N % 8 == 0, preact required");
     if (M == 0 || N == 0) return c;
     int split = split_k < 0 ? -1 : (int)std::max<int64_t>(1, split_k);
-    Tensor ws;
-    // auto split (-1) may pick up to 32 slabs: size the workspace for the worst case only when K allows it
-    const int max_split = split < 0 ? (int)std::min<int64_t>(32, std::max<int64_t>(1, K / 512)) : split;
-    if (max_split > 1) ws = at::empty({rn_gemm_ws_floats(M, N, max_split)}, a.options().dtype(at::kFloat));
+    Tensor ws;  // split-K slabs: allocated once the split is known (tuned / cached / explicit)
     // K must be a multiple of 8 (16-B rows); pad both operands with zeros otherwise
     Tensor A = a, B = b;
     int64_t Kp = K;
@@ -240,9 +237,12 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             const int cfgs[6] = {0, 1, 6, 2, 8, kLibCfg};
             // non-powers of two too: the split that makes tiles × split just fill the 256 CUs
             // (e.g. 48 tiles × 5 = 240) beats the next power of two by up to 25 %
-            const int splits[9] = {1, 2, 3, 4, 5, 6, 8, 12, 16};
-            const int nsplit = split_k < 0 ? 9 : 1;
-            Tensor tws = at::empty({rn_gemm_ws_floats(M, N, 16)}, a.options().dtype(at::kFloat));
+            // up to 128 slabs for tiny outputs over a huge K (e.g. a conv-stem weight gradient: 64×147
+            // outputs, 3 M pixels), where even 16 splits leave most CUs idle
+            const int splits[12] = {1, 2, 3, 4, 5, 6, 8, 12, 16, 32, 64, 128};
+            const long out_tiles = ((M + 255) / 256) * ((N + 255) / 256);
+            const int nsplit = split_k < 0 ? (out_tiles * 16 < 256 ? 12 : 9) : 1;
+            Tensor tws = at::empty({rn_gemm_ws_floats(M, N, splits[nsplit - 1])}, a.options().dtype(at::kFloat));
             hipEvent_t e0, e1;
             (void)hipEventCreate(&e0);
             (void)hipEventCreate(&e1);
@@ -287,7 +287,6 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             cfg = best_cfg;
             split = best_split;
         }
-        if (split > 1 && max_split < split) ws = at::empty({rn_gemm_ws_floats(M, N, split)}, a.options().dtype(at::kFloat));
     }
     if (cfg == kLibCfg) {
         TORCH_CHECK(!(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
@@ -296,8 +295,9 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         lib_gemm(A, B, ta, tb, c);
         return c;
     }
-    const int ws_split = split > 1 ? split : max_split;
-    if (ws_split > 1 && !ws.defined()) ws = at::empty({rn_gemm_ws_floats(M, N, ws_split)}, a.options().dtype(at::kFloat));
+    // split < 0: the native cost model picks (at most 32 slabs, K/split >= 512): size for its worst case
+    const int ws_split = split > 1 ? split : (split < 0 ? (int)std::min<int64_t>(32, std::max<int64_t>(1, Kp / 512)) : 1);
+    if (ws_split > 1) ws = at::empty({rn_gemm_ws_floats(M, N, ws_split)}, a.options().dtype(at::kFloat));
     auto launch = [&](float* colp) {
         return rn_gemm(A.data_ptr(), B.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
                        preact && preact->defined() ? preact->data_ptr() : nullptr,
@@ -693,20 +693,23 @@ Tensor col2im(const Tensor& dcols, int64_t N, int64_t H, int64_t W, int64_t C, i
     rn_col2im(dcols.data_ptr(), dx.data_ptr(), N, H, W, C, KH, KW, S, P, OH, OW, Kp, cur_stream());
     return dx;
 }
-Tensor maxpool_fwd(const Tensor& x, int64_t K, int64_t S, int64_t P) {
+std::tuple<Tensor, Tensor> maxpool_fwd(const Tensor& x, int64_t K, int64_t S, int64_t P) {
     CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    TORCH_CHECK(K * K <= 256, "maxpool: window too large for byte indices");
     const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
     const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
     Tensor y = at::empty({N, OH, OW, C}, x.options());
-    rn_maxpool_fwd(x.data_ptr(), y.data_ptr(), N, H, W, C, K, S, P, OH, OW, cur_stream());
-    return y;
+    Tensor idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+    rn_maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, K, S, P, OH, OW, cur_stream());
+    return {y, idx};
 }
-Tensor maxpool_bwd(const Tensor& gy, const Tensor& x, const Tensor& y, int64_t K, int64_t S, int64_t P) {
-    GUARD(x);
-    const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-    Tensor dx = at::empty_like(x);
-    rn_maxpool_bwd(gy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), N, H, W, C, K, S, P, y.size(1), y.size(2),
-                   cur_stream());
+// gy (N, OH, OW, C) + the forward's window indices → dx (N, H, W, C)
+Tensor maxpool_bwd(const Tensor& gy, const Tensor& idx, int64_t H, int64_t W, int64_t K, int64_t S, int64_t P) {
+    CHECK_BF16(gy); CHECK_CONTIG(gy); GUARD(gy);
+    TORCH_CHECK(idx.scalar_type() == at::kByte && idx.sizes() == gy.sizes() && idx.is_contiguous());
+    const int N = gy.size(0), OH = gy.size(1), OW = gy.size(2), C = gy.size(3);
+    Tensor dx = at::empty({N, H, W, C}, gy.options());
+    rn_maxpool_bwd(gy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, (int)H, (int)W, C, K, S, P, OH, OW, cur_stream());
     return dx;
 }
 Tensor avgpool_fwd(const Tensor& x) {
@@ -723,10 +726,19 @@ Tensor avgpool_bwd(const Tensor& gy, int64_t H, int64_t W) {
     rn_avgpool_bwd(gy.contiguous().data_ptr(), dx.data_ptr(), N, H * W, C, cur_stream());
     return dx;
 }
+// NHWC BatchNorm over [M][C] rows (C % 8 == 0, C <= 2048); res (optional, same shape): y = relu(BN(x) + res)
+static void check_bn(const Tensor& x, const optional<Tensor>& res) {
+    CHECK_BF16(x); CHECK_CONTIG(x);
+    TORCH_CHECK(rn_bn_supported((int)x.size(1)), "batchnorm: channels must be a multiple of 8 and <= 2048");
+    if (res && res->defined()) {
+        CHECK_BF16(*res); CHECK_CONTIG(*res);
+        TORCH_CHECK(res->sizes() == x.sizes(), "batchnorm residual shape");
+    }
+}
 std::tuple<Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
                                                  const Tensor& rmean, const Tensor& rvar, double mom, double eps,
-                                                 bool relu) {
-    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+                                                 bool relu, const optional<Tensor>& res) {
+    check_bn(x, res); GUARD(x);
     TORCH_CHECK(rmean.scalar_type() == at::kFloat && rvar.scalar_type() == at::kFloat, "BN running stats must be fp32");
     const int M = x.size(0), C = x.size(1);
     Tensor y = at::empty_like(x);
@@ -735,28 +747,32 @@ std::tuple<Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& 
     Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
     rn_bn_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), y.data_ptr(),
               mean.data_ptr<float>(), rstd.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)mom, (float)eps, relu,
-              cur_stream());
+              optr(res), cur_stream());
     return {y, mean, rstd};
 }
 Tensor batchnorm_eval(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& rmean, const Tensor& rvar,
-                      double eps, bool relu) {
-    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+                      double eps, bool relu, const optional<Tensor>& res) {
+    check_bn(x, res); GUARD(x);
     Tensor y = at::empty_like(x);
     rn_bn_eval(x.data_ptr(), w.data_ptr(), b.data_ptr(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), y.data_ptr(),
-               x.size(0), x.size(1), (float)eps, relu, cur_stream());
+               x.size(0), x.size(1), (float)eps, relu, optr(res), cur_stream());
     return y;
 }
-std::tuple<Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor& x, const Tensor& y, const Tensor& w,
-                                                 const Tensor& mean, const Tensor& rstd, bool relu) {
-    CHECK_BF16(gy); CHECK_CONTIG(gy); GUARD(gy);
+// returns (dx, dw, db, g') with g' = dy ⊙ relu'(y) (the fused residual's gradient) when want_gres
+std::tuple<Tensor, Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor& x, const Tensor& y,
+                                                         const Tensor& w, const Tensor& mean, const Tensor& rstd,
+                                                         bool relu, bool want_gres) {
+    check_bn(gy, c10::nullopt); GUARD(gy);
     const int M = x.size(0), C = x.size(1);
     Tensor dx = at::empty_like(x);
-    Tensor dw = at::empty({C}, x.options().dtype(at::kFloat));
-    Tensor db = at::empty({C}, x.options().dtype(at::kFloat));
+    Tensor dw = at::empty({C}, x.options());  // bf16, the parameter dtype
+    Tensor db = at::empty({C}, x.options());
+    Tensor gres = want_gres ? at::empty_like(x) : at::empty({0}, x.options());
     Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
     rn_bn_bwd(gy.data_ptr(), x.data_ptr(), y.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-              dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu, cur_stream());
-    return {dx, dw, db};
+              dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr<float>(), M, C, relu,
+              want_gres ? gres.data_ptr() : nullptr, cur_stream());
+    return {dx, dw, db, gres};
 }
 
 // ------------------------------------------------------------------ fp8
@@ -840,14 +856,16 @@ TORCH_LIBRARY(replicann, m) {
     m.def("conv_dgrad_implicit(Tensor dy, Tensor w, int H, int W, int P) -> Tensor");
     m.def("conv_wgrad_implicit(Tensor dy2, Tensor x, int KH, int KW, int S, int P) -> Tensor");
     m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp) -> Tensor");
-    m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> Tensor");
-    m.def("maxpool_bwd(Tensor gy, Tensor x, Tensor y, int K, int S, int P) -> Tensor");
+    m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> (Tensor, Tensor)");
+    m.def("maxpool_bwd(Tensor gy, Tensor idx, int H, int W, int K, int S, int P) -> Tensor");
     m.def("avgpool_fwd(Tensor x) -> Tensor");
     m.def("avgpool_bwd(Tensor gy, int H, int W) -> Tensor");
-    m.def("batchnorm_fwd(Tensor x, Tensor w, Tensor b, Tensor(a!) rmean, Tensor(b!) rvar, float mom, float eps, bool relu) "
-          "-> (Tensor, Tensor, Tensor)");
-    m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu) -> Tensor");
-    m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu) -> (Tensor, Tensor, Tensor)");
+    m.def("batchnorm_fwd(Tensor x, Tensor w, Tensor b, Tensor(a!) rmean, Tensor(b!) rvar, float mom, float eps, bool relu, "
+          "Tensor? res=None) -> (Tensor, Tensor, Tensor)");
+    m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu, "
+          "Tensor? res=None) -> Tensor");
+    m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu, "
+          "bool want_gres=False) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("fp8_quantize(Tensor x) -> (Tensor, Tensor)");
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");

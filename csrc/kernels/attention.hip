@@ -1033,18 +1033,13 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast) {
         dim3 grid(B * H, (Tq + 127) / 128);
-        // REPLICANN_ATTN_FWD: 1 = original single-loop kernel, 2 (default) = split-loop v2 at 3 blocks/CU,
-        // 3 = v2 at 2 blocks/CU (read per call so one process can A/B them)
+        // REPLICANN_ATTN_FWD=1 selects the original single-loop kernel (read per call so one process
+        // can A/B them); default: the split-loop v2 (no bias / dropout) at 3 blocks per CU
         const char* ev = std::getenv("REPLICANN_ATTN_FWD");
         const int var = ev ? std::atoi(ev) : 2;
         if (!bias && p_drop == 0.f && var >= 2) {
-            if (var == 3) {
-                if (causal) attn_fwd64v2_k<true, 2><<<grid, 256, 32768, st>>>(a);
-                else attn_fwd64v2_k<false, 2><<<grid, 256, 32768, st>>>(a);
-            } else {
-                if (causal) attn_fwd64v2_k<true, 3><<<grid, 256, 32768, st>>>(a);
-                else attn_fwd64v2_k<false, 3><<<grid, 256, 32768, st>>>(a);
-            }
+            if (causal) attn_fwd64v2_k<true, 3><<<grid, 256, 32768, st>>>(a);
+            else attn_fwd64v2_k<false, 3><<<grid, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
         }
@@ -1079,21 +1074,8 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2(B * H, (Tq + 63) / 64);
         dim3 g1(B * H, (Tk + 63) / 64);
-        // REPLICANN_ATTN_BWD=2: 4 waves per SIMD for both kernels (both fit 128 VGPRs)
-        const char* ev = std::getenv("REPLICANN_ATTN_BWD");
-        const int var = ev ? std::atoi(ev) : 1;
-        if (var == 2 && !bias && p_drop == 0.f) {
-            if (causal) {
-                attn_bwd_dq64_k<true, false, false, 4><<<g2, 256, 32768, st>>>(a);
-                attn_bwd_dkdv64_k<true, false, false, 4><<<g1, 256, 36864, st>>>(a);
-            } else {
-                attn_bwd_dq64_k<false, false, false, 4><<<g2, 256, 32768, st>>>(a);
-                attn_bwd_dkdv64_k<false, false, false, 4><<<g1, 256, 36864, st>>>(a);
-            }
-        } else {
-            RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
-            RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
-        }
+        RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
+        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
     } else {
         if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
         dim3 grid(Tq, B * H);

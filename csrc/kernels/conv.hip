@@ -70,54 +70,90 @@ __global__ void __launch_bounds__(256) col2im_k(const bf16* __restrict__ dcols, 
     }
 }
 
-__global__ void __launch_bounds__(256) maxpool_fwd_k(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H,
-                                                     int W, int C, int K, int S, int P, int OH, int OW) {
-    const long total = (long)N * OH * OW * C;
+// Max-pool, NHWC, V channels per thread (V = 8: one 16-B load per window tap; V = 1 for C % 8 != 0).
+// The forward also writes the window position (kh·K + kw, one byte per output element) of the
+// FIRST maximum in scan order (ATen's tie rule), so the backward is a gather of at most
+// ceil(K/S)² gradient values per input element — no window re-scan, no atomics.
+template <int V>
+__global__ void __launch_bounds__(256) maxpool_fwd_k(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                     uint8_t* __restrict__ idx, int N, int H, int W, int C, int K,
+                                                     int S, int P, int OH, int OW) {
+    const int CV = C / V;
+    const long total = (long)N * OH * OW * CV;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int c = i % C;
-        long t = i / C;
+        const int cv = i % CV;
+        long t = i / CV;
         const int ow = t % OW;
         t /= OW;
         const int oh = t % OH, n = t / OH;
-        float m = -INFINITY;
-        for (int kh = 0; kh < K; ++kh)
+        float m[V];
+        int am[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) { m[j] = -INFINITY; am[j] = 0; }
+        for (int kh = 0; kh < K; ++kh) {
+            const int ih = oh * S - P + kh;
+            if (ih < 0 || ih >= H) continue;
             for (int kw = 0; kw < K; ++kw) {
-                const int ih = oh * S - P + kh, iw = ow * S - P + kw;
-                if (ih >= 0 && ih < H && iw >= 0 && iw < W) m = fmaxf(m, bf2f(x[(((long)n * H + ih) * W + iw) * C + c]));
+                const int iw = ow * S - P + kw;
+                if (iw < 0 || iw >= W) continue;
+                const bf16* src = x + (((long)n * H + ih) * W + iw) * C + cv * V;
+                float v[V];
+                if constexpr (V == 8) load8(src, v);
+                else v[0] = bf2f(src[0]);
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    if (v[j] > m[j]) { m[j] = v[j]; am[j] = kh * K + kw; }
             }
-        y[i] = f2bf(m);
+        }
+        const long o = (((long)n * OH + oh) * OW + ow) * C + cv * V;
+        if constexpr (V == 8) {
+            store8(y + o, m);
+            uint2 packed;
+            packed.x = (uint32_t)am[0] | ((uint32_t)am[1] << 8) | ((uint32_t)am[2] << 16) | ((uint32_t)am[3] << 24);
+            packed.y = (uint32_t)am[4] | ((uint32_t)am[5] << 8) | ((uint32_t)am[6] << 16) | ((uint32_t)am[7] << 24);
+            *reinterpret_cast<uint2*>(idx + o) = packed;
+        } else {
+            y[o] = f2bf(m[0]);
+            idx[o] = (uint8_t)am[0];
+        }
     }
 }
 
-// gradient goes to the FIRST maximum of each window in scan order (matches ATen)
-__global__ void __launch_bounds__(256) maxpool_bwd_k(const bf16* __restrict__ gy, const bf16* __restrict__ x,
-                                                     const bf16* __restrict__ y, bf16* __restrict__ dx, int N, int H,
-                                                     int W, int C, int K, int S, int P, int OH, int OW) {
-    const long total = (long)N * H * W * C;
+template <int V>
+__global__ void __launch_bounds__(256) maxpool_bwd_k(const bf16* __restrict__ gy, const uint8_t* __restrict__ idx,
+                                                     bf16* __restrict__ dx, int N, int H, int W, int C, int K, int S,
+                                                     int P, int OH, int OW) {
+    const int CV = C / V;
+    const long total = (long)N * H * W * CV;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int c = i % C;
-        long t = i / C;
+        const int cv = i % CV;
+        long t = i / CV;
         const int w = t % W;
         t /= W;
         const int h = t % H, n = t / H;
-        float acc = 0.f;
+        float acc[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = 0.f;
         for (int oh = max(0, (h + P - K + S) / S); oh <= min(OH - 1, (h + P) / S); ++oh)
             for (int ow = max(0, (w + P - K + S) / S); ow <= min(OW - 1, (w + P) / S); ++ow) {
-                const long oi = (((long)n * OH + oh) * OW + ow) * C + c;
-                const float ym = bf2f(y[oi]);
-                // first argmax in the window
-                int fh = -1, fw = -1;
-                for (int kh = 0; kh < K && fh < 0; ++kh)
-                    for (int kw = 0; kw < K; ++kw) {
-                        const int ih = oh * S - P + kh, iw = ow * S - P + kw;
-                        if (ih >= 0 && ih < H && iw >= 0 && iw < W && bf2f(x[(((long)n * H + ih) * W + iw) * C + c]) == ym) {
-                            fh = ih; fw = iw;
-                            break;
-                        }
+                const int pos = (h + P - oh * S) * K + (w + P - ow * S);  // this input's place in the window
+                const long oi = (((long)n * OH + oh) * OW + ow) * C + cv * V;
+                if constexpr (V == 8) {
+                    const uint2 a = *reinterpret_cast<const uint2*>(idx + oi);
+                    float g[8];
+                    load8(gy + oi, g);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t b = ((j < 4 ? a.x : a.y) >> (8 * (j & 3))) & 0xFF;
+                        if ((int)b == pos) acc[j] += g[j];
                     }
-                if (fh == h && fw == w) acc += bf2f(gy[oi]);
+                } else {
+                    if ((int)idx[oi] == pos) acc[0] += bf2f(gy[oi]);
+                }
             }
-        dx[i] = f2bf(acc);
+        const long o = (((long)n * H + h) * W + w) * C + cv * V;
+        if constexpr (V == 8) store8(dx + o, acc);
+        else dx[o] = f2bf(acc[0]);
     }
 }
 
@@ -142,53 +178,81 @@ __global__ void __launch_bounds__(256) avgpool_bwd_k(const bf16* __restrict__ gy
     }
 }
 
-// ---- BatchNorm on [M rows][C channels] ----
-// column partial sums of f(row, c) over row splits.  MODE 0: (x, x^2)
-// MODE 1: (dy', dy' * xhat) with dy' = dy * relu'(y)
+// ---- BatchNorm on [M rows][C channels] (NHWC flattened) ----
+// Training statistics in two deterministic steps:
+//   bn_part_k    grid S row-splits × 256 threads; thread t owns channel group t % (C/8) (8 channels,
+//                16-B loads) and rows t / (C/8) + k·(256·8/C); per-split partials → part[S][2C]
+//                (MODE 0: Σx | Σx² ; MODE 1: Σg' | Σg'·x̂ with g' = dy masked by the fused ReLU)
+//   rn_colreduce_seg (common.h) sums the S partial rows in fixed order → [2C] fp32,
+//   bn_finalize_k turns the forward sums into mean / rstd / running statistics.
+// Apply kernels are 8 channels per thread.  An optional residual input is fused into the forward
+// apply (y = relu(BN(x) + res)); the backward then also returns g' = dy ⊙ relu'(y), the residual
+// branch's gradient.  C % 8 == 0 and C ≤ 2048 (all of ResNet-18).
+constexpr int BN_T = 256;
+
 template <int MODE>
-__global__ void __launch_bounds__(256) bn_colsum_k(const bf16* __restrict__ a, const bf16* __restrict__ b,
+__global__ void __launch_bounds__(BN_T) bn_part_k(const bf16* __restrict__ a, const bf16* __restrict__ xin,
                                                   const bf16* __restrict__ yv, const float* __restrict__ mean,
-                                                  const float* __restrict__ rstd, float* __restrict__ p0,
-                                                  float* __restrict__ p1, int M, int C, int rps, int relu) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int wv = threadIdx.x >> 6;
-    const int r0 = blockIdx.y * rps, r1 = min(M, r0 + rps);
-    __shared__ float s0[4][64], s1[4][64];
-    float a0 = 0.f, a1 = 0.f;
-    if (c < C) {
-        const float mu = MODE ? mean[c] : 0.f, rs = MODE ? rstd[c] : 0.f;
-        for (int r = r0 + wv; r < r1; r += 4) {
-            const long e = (long)r * C + c;
+                                                  const float* __restrict__ rstd, float* __restrict__ part, int M,
+                                                  int C, int rps, int relu) {
+    __shared__ float red[2][BN_T * 8];
+    const int CG = C / 8;
+    const int t = threadIdx.x;
+    const int cg = t % CG, ro = t / CG, rpi = BN_T / CG;  // threads t >= rpi*CG idle (CG ∤ 256)
+    const int r0 = blockIdx.x * rps, r1 = min(M, r0 + rps);
+    float s0[8], s1[8], mu[8], rs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s0[j] = 0.f; s1[j] = 0.f; mu[j] = 0.f; rs[j] = 0.f; }
+    const bool active = ro < rpi;
+    if (MODE == 1 && active) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { mu[j] = mean[cg * 8 + j]; rs[j] = rstd[cg * 8 + j]; }
+    }
+    if (active) {
+        for (int r = r0 + ro; r < r1; r += rpi) {
+            const long e = (long)r * C + cg * 8;
+            float v[8];
+            load8(a + e, v);
             if (MODE == 0) {
-                const float v = bf2f(a[e]);
-                a0 += v;
-                a1 += v * v;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] += v[j] * v[j]; }
             } else {
-                float g = bf2f(a[e]);
-                if (relu && bf2f(yv[e]) <= 0.f) g = 0.f;
-                a0 += g;
-                a1 += g * (bf2f(b[e]) - mu) * rs;
+                float xv[8];
+                load8(xin + e, xv);
+                if (relu) {
+                    float yy[8];
+                    load8(yv + e, yy);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = yy[j] > 0.f ? v[j] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] += v[j] * (xv[j] - mu[j]) * rs[j]; }
             }
         }
     }
-    s0[wv][threadIdx.x & 63] = a0;
-    s1[wv][threadIdx.x & 63] = a1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][t * 8 + j] = s0[j]; red[1][t * 8 + j] = s1[j]; }
     __syncthreads();
-    if (wv == 0 && c < C) {
-        p0[(long)blockIdx.y * C + c] = s0[0][threadIdx.x] + s0[1][threadIdx.x] + s0[2][threadIdx.x] + s0[3][threadIdx.x];
-        p1[(long)blockIdx.y * C + c] = s1[0][threadIdx.x] + s1[1][threadIdx.x] + s1[2][threadIdx.x] + s1[3][threadIdx.x];
+    // thread c < C: fixed-order sum over the row groups of its channel
+    for (int c = t; c < C; c += BN_T) {
+        const int g = c / 8, j = c % 8;
+        float u0 = 0.f, u1 = 0.f;
+        for (int k = 0; k < rpi; ++k) {
+            u0 += red[0][(k * CG + g) * 8 + j];
+            u1 += red[1][(k * CG + g) * 8 + j];
+        }
+        part[(long)blockIdx.x * 2 * C + c] = u0;
+        part[(long)blockIdx.x * 2 * C + C + c] = u1;
     }
 }
 
-__global__ void bn_stats_k(const float* __restrict__ p0, const float* __restrict__ p1, int S, int C, int M,
-                           float eps, float mom, float* __restrict__ mean, float* __restrict__ rstd,
-                           float* __restrict__ rmean, float* __restrict__ rvar) {
+__global__ void bn_finalize_k(const float* __restrict__ sums, int C, int M, float eps, float mom,
+                              float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rmean,
+                              float* __restrict__ rvar) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    float s = 0.f, q = 0.f;
-    for (int i = 0; i < S; ++i) { s += p0[(long)i * C + c]; q += p1[(long)i * C + c]; }
-    const float mu = s / M;
-    const float var = fmaxf(q / M - mu * mu, 0.f);
+    const float mu = sums[c] / M;
+    const float var = fmaxf(sums[C + c] / M - mu * mu, 0.f);
     mean[c] = mu;
     rstd[c] = rsqrtf(var + eps);
     if (rmean) {
@@ -197,53 +261,61 @@ __global__ void bn_stats_k(const float* __restrict__ p0, const float* __restrict
     }
 }
 
-__global__ void bn_gsum_k(const float* __restrict__ p0, const float* __restrict__ p1, int S, int C,
-                          float* __restrict__ db, float* __restrict__ dw) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    float s = 0.f, q = 0.f;
-    for (int i = 0; i < S; ++i) { s += p0[(long)i * C + c]; q += p1[(long)i * C + c]; }
-    db[c] = s;
-    dw[c] = q;
-}
-
+// y = [relu](BN(x) [+ res]); per-channel affine from (mean, rstd, w, b) or, in eval mode, running stats
+template <bool EVAL>
 __global__ void __launch_bounds__(256) bn_apply_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const bf16* __restrict__ b, const float* __restrict__ mean,
-                                                  const float* __restrict__ rstd, bf16* __restrict__ y, long total,
-                                                  int C, int relu) {
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int c = i % C;
-        float v = (bf2f(x[i]) - mean[c]) * rstd[c] * bf2f(w[c]) + bf2f(b[c]);
-        if (relu) v = fmaxf(v, 0.f);
-        y[i] = f2bf(v);
+                                                  const float* __restrict__ rstd, const bf16* __restrict__ res,
+                                                  bf16* __restrict__ y, long total8, int C, float eps, int relu) {
+    const int CG = C / 8;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+        const int c0 = (int)(i % CG) * 8;
+        float v[8], wf[8], bf[8];
+        load8(x + i * 8, v);
+        load8(w + c0, wf);
+        load8(b + c0, bf);
+        float rr[8];
+        if (res) load8(res + i * 8, rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float sc = EVAL ? rsqrtf(rstd[c0 + j] + eps) : rstd[c0 + j];  // eval: rstd holds running var
+            float o = (v[j] - mean[c0 + j]) * sc * wf[j] + bf[j];
+            if (res) o += rr[j];
+            v[j] = relu ? fmaxf(o, 0.f) : o;
+        }
+        store8(y + i * 8, v);
     }
 }
 
-// eval mode: running statistics
-__global__ void __launch_bounds__(256) bn_eval_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                 const bf16* __restrict__ b, const float* __restrict__ rm,
-                                                 const float* __restrict__ rv, bf16* __restrict__ y, long total, int C,
-                                                 float eps, int relu) {
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int c = i % C;
-        float v = (bf2f(x[i]) - rm[c]) * rsqrtf(rv[c] + eps) * bf2f(w[c]) + bf2f(b[c]);
-        if (relu) v = fmaxf(v, 0.f);
-        y[i] = f2bf(v);
-    }
-}
-
+// dx = w·rstd·(g' − Σg'/M − x̂·Σ(g'x̂)/M), g' = dy ⊙ relu'(y); optionally g' itself (residual branch)
 __global__ void __launch_bounds__(256) bn_bwd_apply_k(const bf16* __restrict__ gy, const bf16* __restrict__ x,
                                                       const bf16* __restrict__ yv, const bf16* __restrict__ w,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                      const float* __restrict__ db, const float* __restrict__ dw,
-                                                      bf16* __restrict__ dx, long total, int C, int M, int relu) {
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int c = i % C;
-        float g = bf2f(gy[i]);
-        if (relu && bf2f(yv[i]) <= 0.f) g = 0.f;
-        const float xh = (bf2f(x[i]) - mean[c]) * rstd[c];
-        const float v = bf2f(w[c]) * rstd[c] * (g - db[c] / M - xh * dw[c] / M);
-        dx[i] = f2bf(v);
+                                                      const float* __restrict__ sums, bf16* __restrict__ dx,
+                                                      bf16* __restrict__ gres, long total8, int C, int M, int relu) {
+    const int CG = C / 8;
+    const float invM = 1.f / M;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+        const int c0 = (int)(i % CG) * 8;
+        float g[8], xv[8], wf[8];
+        load8(gy + i * 8, g);
+        load8(x + i * 8, xv);
+        load8(w + c0, wf);
+        if (relu) {
+            float yy[8];
+            load8(yv + i * 8, yy);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+        }
+        if (gres) store8(gres + i * 8, g);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = c0 + j;
+            const float xh = (xv[j] - mean[c]) * rstd[c];
+            o[j] = wf[j] * rstd[c] * (g[j] - sums[c] * invM - xh * sums[C + c] * invM);
+        }
+        store8(dx + i * 8, o);
     }
 }
 
@@ -252,10 +324,9 @@ inline int gridn(long n) {
     return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
 }
 
-inline int bn_splits(int M, int C) {
-    int cb = (C + 63) / 64, s = 1;
-    while (cb * s < 1024 && M / (s * 2) >= 64) s *= 2;
-    return s;
+inline int bn_splits(int M) {
+    int S = M / 256;  // >= 256 rows per split
+    return S < 1 ? 1 : (S > 1024 ? 1024 : S);
 }
 
 }  // namespace
@@ -274,15 +345,25 @@ void rn_col2im(const void* dcols, void* dx, int N, int H, int W, int C, int KH, 
     col2im_k<<<gridn((long)N * H * W * C), 256, 0, st>>>((const bf16*)dcols, (bf16*)dx, N, H, W, C, KH, KW, S, P, OH, OW, Kp);
 }
 
-void rn_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int K, int S, int P, int OH, int OW,
-                    hipStream_t st) {
-    maxpool_fwd_k<<<gridn((long)N * OH * OW * C), 256, 0, st>>>((const bf16*)x, (bf16*)y, N, H, W, C, K, S, P, OH, OW);
+// idx: one byte per output element (window position of the first maximum); K*K <= 256
+void rn_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int K, int S, int P, int OH,
+                    int OW, hipStream_t st) {
+    if (C % 8 == 0)
+        maxpool_fwd_k<8><<<gridn((long)N * OH * OW * C / 8), 256, 0, st>>>((const bf16*)x, (bf16*)y, (uint8_t*)idx, N,
+                                                                             H, W, C, K, S, P, OH, OW);
+    else
+        maxpool_fwd_k<1><<<gridn((long)N * OH * OW * C), 256, 0, st>>>((const bf16*)x, (bf16*)y, (uint8_t*)idx, N, H,
+                                                                         W, C, K, S, P, OH, OW);
 }
 
-void rn_maxpool_bwd(const void* gy, const void* x, const void* y, void* dx, int N, int H, int W, int C, int K, int S,
-                    int P, int OH, int OW, hipStream_t st) {
-    maxpool_bwd_k<<<gridn((long)N * H * W * C), 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const bf16*)y,
-                                                               (bf16*)dx, N, H, W, C, K, S, P, OH, OW);
+void rn_maxpool_bwd(const void* gy, const void* idx, void* dx, int N, int H, int W, int C, int K, int S, int P,
+                    int OH, int OW, hipStream_t st) {
+    if (C % 8 == 0)
+        maxpool_bwd_k<8><<<gridn((long)N * H * W * C / 8), 256, 0, st>>>((const bf16*)gy, (const uint8_t*)idx,
+                                                                           (bf16*)dx, N, H, W, C, K, S, P, OH, OW);
+    else
+        maxpool_bwd_k<1><<<gridn((long)N * H * W * C), 256, 0, st>>>((const bf16*)gy, (const uint8_t*)idx, (bf16*)dx,
+                                                                       N, H, W, C, K, S, P, OH, OW);
 }
 
 void rn_avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
@@ -293,38 +374,54 @@ void rn_avgpool_bwd(const void* gy, void* dx, int N, int HW, int C, hipStream_t 
     avgpool_bwd_k<<<gridn((long)N * HW * C), 256, 0, st>>>((const bf16*)gy, (bf16*)dx, N, HW, C);
 }
 
-long rn_bn_ws_floats(int M, int C) { return 2L * bn_splits(M, C) * C; }
+// workspace floats: partials [S][2C] + reduced sums [2C] + the column reduction's scratch
+long rn_bn_ws_floats(int M, int C) { return 2L * C * (bn_splits(M) + 1) + (long)RN_COLRED_S * 2 * C; }
 
-void rn_bn_fwd(const void* x, const void* w, const void* b, float* rmean, float* rvar, void* y, float* mean,
-               float* rstd, float* ws, int M, int C, float mom, float eps, int relu, hipStream_t st) {
-    const int S = bn_splits(M, C);
+static void bn_stats(int mode, const void* a, const void* xin, const void* yv, const float* mean, const float* rstd,
+                     float* ws, int M, int C, int relu, void* db16, void* dw16, hipStream_t st) {
+    const int S = bn_splits(M);
     const int rps = (M + S - 1) / S;
-    dim3 g((C + 63) / 64, S);
-    bn_colsum_k<0><<<g, 256, 0, st>>>((const bf16*)x, nullptr, nullptr, nullptr, nullptr, ws, ws + (long)S * C, M, C,
-                                      rps, 0);
-    bn_stats_k<<<(C + 255) / 256, 256, 0, st>>>(ws, ws + (long)S * C, S, C, M, eps, mom, mean, rstd, rmean, rvar);
-    bn_apply_k<<<gridn((long)M * C), 256, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)b, mean, rstd,
-                                                    (bf16*)y, (long)M * C, C, relu);
+    float* part = ws;
+    float* sums = ws + 2L * C * S;
+    float* tmp = sums + 2L * C;
+    if (mode == 0)
+        bn_part_k<0><<<S, BN_T, 0, st>>>((const bf16*)a, nullptr, nullptr, nullptr, nullptr, part, M, C, rps, 0);
+    else
+        bn_part_k<1><<<S, BN_T, 0, st>>>((const bf16*)a, (const bf16*)xin, (const bf16*)yv, mean, rstd, part, M, C,
+                                         rps, relu);
+    RnColOut o{{sums, sums + C, nullptr}, {(__bf16*)db16, (__bf16*)dw16, nullptr}, C, {0, 0, 0}};
+    rn_colreduce_seg(part, S, 2 * C, tmp, o, st);
+}
+
+int rn_bn_supported(int C) { return C % 8 == 0 && C <= 2048; }
+
+// res (optional): y = relu(BN(x) + res)
+void rn_bn_fwd(const void* x, const void* w, const void* b, float* rmean, float* rvar, void* y, float* mean,
+               float* rstd, float* ws, int M, int C, float mom, float eps, int relu, const void* res, hipStream_t st) {
+    bn_stats(0, x, nullptr, nullptr, nullptr, nullptr, ws, M, C, 0, nullptr, nullptr, st);
+    const float* sums = ws + 2L * C * bn_splits(M);
+    bn_finalize_k<<<(C + 255) / 256, 256, 0, st>>>(sums, C, M, eps, mom, mean, rstd, rmean, rvar);
+    const long t8 = (long)M * C / 8;
+    bn_apply_k<false><<<gridn(t8), 256, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)b, mean, rstd,
+                                                  (const bf16*)res, (bf16*)y, t8, C, eps, relu);
 }
 
 void rn_bn_eval(const void* x, const void* w, const void* b, const float* rmean, const float* rvar, void* y, int M,
-                int C, float eps, int relu, hipStream_t st) {
-    bn_eval_k<<<gridn((long)M * C), 256, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)b, rmean, rvar,
-                                                   (bf16*)y, (long)M * C, C, eps, relu);
+                int C, float eps, int relu, const void* res, hipStream_t st) {
+    const long t8 = (long)M * C / 8;
+    bn_apply_k<true><<<gridn(t8), 256, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)b, rmean, rvar,
+                                                 (const bf16*)res, (bf16*)y, t8, C, eps, relu);
 }
 
-// dw/db: fp32 outputs [C]
+// dw/db: bf16 outputs [C] (the parameter dtype, written by the reduction itself); gres (optional):
+// dy ⊙ relu'(y), the gradient of a fused residual input
 void rn_bn_bwd(const void* gy, const void* x, const void* y, const void* w, const float* mean, const float* rstd,
-               void* dx, float* dw, float* db, float* ws, int M, int C, int relu, hipStream_t st) {
-    const int S = bn_splits(M, C);
-    const int rps = (M + S - 1) / S;
-    dim3 g((C + 63) / 64, S);
-    bn_colsum_k<1><<<g, 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const bf16*)y, mean, rstd, ws,
-                                      ws + (long)S * C, M, C, rps, relu);
-    bn_gsum_k<<<(C + 255) / 256, 256, 0, st>>>(ws, ws + (long)S * C, S, C, db, dw);
-    bn_bwd_apply_k<<<gridn((long)M * C), 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const bf16*)y,
-                                                        (const bf16*)w, mean, rstd, db, dw, (bf16*)dx, (long)M * C, C,
-                                                        M, relu);
+               void* dx, void* dw, void* db, float* ws, int M, int C, int relu, void* gres, hipStream_t st) {
+    bn_stats(1, gy, x, y, mean, rstd, ws, M, C, relu, db, dw, st);
+    const float* sums = ws + 2L * C * bn_splits(M);
+    const long t8 = (long)M * C / 8;
+    bn_bwd_apply_k<<<gridn(t8), 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const bf16*)y, (const bf16*)w, mean,
+                                               rstd, sums, (bf16*)dx, (bf16*)gres, t8, C, M, relu);
 }
 
 }  // extern "C"

@@ -38,9 +38,9 @@ class BatchNorm(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = momentum, eps
 
-    def forward(self, x, relu=False):
+    def forward(self, x, relu=False, residual=None):
         return ops.batch_norm_nhwc(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                   self.training, self.momentum, self.eps, relu)
+                                   self.training, self.momentum, self.eps, relu, residual)
 
 
 class BasicBlock(nn.Module):
@@ -57,9 +57,9 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
-        out = self.bn2(self.conv2(out))
         sc = self.down_bn(self.down_conv(x)) if self.has_down else x
-        return ops.relu(out + sc)
+        # relu(bn2(conv2(out)) + sc) in one BatchNorm pass (its backward also returns sc's gradient)
+        return self.bn2(self.conv2(out), relu=True, residual=sc)
 
 
 class ResNet18(nn.Module):

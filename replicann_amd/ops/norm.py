@@ -105,14 +105,16 @@ def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, 
 # --------------------------------------------------------------------------
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual):
         # x: (N, H, W, C) contiguous channels-last storage
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
+        r2 = residual.reshape(-1, C).contiguous() if residual is not None else None
         y, mean, rstd = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
-                                                 momentum, eps, relu)
+                                                 momentum, eps, relu, r2)
         ctx.save_for_backward(x2, y, weight, bias, mean, rstd)
         ctx.relu = relu
+        ctx.has_res = residual is not None
         ctx.shp = x.shape
         return y.reshape(x.shape)
 
@@ -120,23 +122,28 @@ class _BatchNormFn(torch.autograd.Function):
     def backward(ctx, gy):
         x2, y, weight, bias, mean, rstd = ctx.saved_tensors
         C = ctx.shp[-1]
-        dx, dw, db = _ext.ops().batchnorm_bwd(gy.reshape(-1, C).contiguous(), x2, y, weight, mean,
-                                              rstd, ctx.relu)
-        return dx.reshape(ctx.shp), dw.to(weight.dtype), db.to(bias.dtype), None, None, None, None, None
+        dx, dw, db, gres = _ext.ops().batchnorm_bwd(gy.reshape(-1, C).contiguous(), x2, y, weight, mean,
+                                                    rstd, ctx.relu, ctx.has_res)
+        gr = gres.reshape(ctx.shp) if ctx.has_res else None
+        return dx.reshape(ctx.shp), dw.to(weight.dtype), db.to(bias.dtype), None, None, None, None, None, gr
 
 
 def batch_norm_nhwc(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5,
-                    relu=False):
-    """BatchNorm over (N,H,W) of an NHWC tensor, optional fused ReLU."""
+                    relu=False, residual=None):
+    """BatchNorm over (N,H,W) of an NHWC tensor; optional fused residual add and ReLU:
+    y = [relu](BN(x) [+ residual])  (ResNet's block output in one pass)."""
     if _ext.use_native(x):
         if training:
-            return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu)
+            return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual)
         C = x.shape[-1]
+        r2 = residual.reshape(-1, C).contiguous() if residual is not None else None
         y = _ext.ops().batchnorm_eval(x.reshape(-1, C).contiguous(), weight, bias, running_mean, running_var,
-                                      eps, relu)
+                                      eps, relu, r2)
         return y.reshape(x.shape)
     xc = x.permute(0, 3, 1, 2)
-    y = F.batch_norm(xc, running_mean, running_var, weight, bias, training, momentum, eps)
+    y = F.batch_norm(xc, running_mean, running_var, weight, bias, training, momentum, eps).permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual
     if relu:
         y = F.relu(y)
-    return y.permute(0, 2, 3, 1)
+    return y

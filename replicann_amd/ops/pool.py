@@ -1,5 +1,6 @@
 """NHWC pooling for ResNet-18 (csrc/kernels/conv.hip): 3×3/2 max-pool and global
-average pool.  Max-pool backward re-derives the argmax (no index tensor)."""
+average pool.  The max-pool forward stores the window position of each maximum (one byte
+per output element); the backward gathers the gradient through it."""
 
 from __future__ import annotations
 
@@ -12,16 +13,16 @@ from .. import _ext
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, p):
-        y = _ext.ops().maxpool_fwd(x.contiguous(), k, s, p)
-        ctx.save_for_backward(x, y)
-        ctx.cfg = (k, s, p)
+        y, idx = _ext.ops().maxpool_fwd(x.contiguous(), k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.cfg = (k, s, p, x.shape[1], x.shape[2])
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, y = ctx.saved_tensors
-        k, s, p = ctx.cfg
-        return _ext.ops().maxpool_bwd(gy.contiguous(), x, y, k, s, p), None, None, None
+        (idx,) = ctx.saved_tensors
+        k, s, p, H, W = ctx.cfg
+        return _ext.ops().maxpool_bwd(gy.contiguous(), idx, H, W, k, s, p), None, None, None
 
 
 def maxpool_nhwc(x, kernel=3, stride=2, padding=1):

@@ -33,7 +33,7 @@ def timeit(fn, iters=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("B", type=int, nargs="?", default=64)
-    ap.add_argument("--fwd", default="1,2,3")
+    ap.add_argument("--fwd", default="1,2")
     ap.add_argument("--bwd", default="1")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()

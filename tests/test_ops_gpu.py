@@ -258,12 +258,11 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("fwd,bwd", [("1", "1"), ("2", "1"), ("3", "2")])
-def test_attention_kernel_variants(cuda, monkeypatch, fwd, bwd):
-    """Every D=64 kernel variant (REPLICANN_ATTN_FWD / _BWD) against the fp32 reference, incl. Tq != Tk
-    (causal offset, ragged key blocks) so the masked / unmasked tile loops both run."""
+@pytest.mark.parametrize("fwd", ["1", "2"])
+def test_attention_kernel_variants(cuda, monkeypatch, fwd):
+    """Both D=64 forward kernels (REPLICANN_ATTN_FWD) and the backward against the fp32 reference, incl.
+    Tq != Tk (causal offset, ragged key blocks) so the masked / unmasked tile loops all run."""
     monkeypatch.setenv("REPLICANN_ATTN_FWD", fwd)
-    monkeypatch.setenv("REPLICANN_ATTN_BWD", bwd)
     torch.manual_seed(70)
     _attn_check(2, 320, 3, 64, True)
     _attn_check(1, 100, 2, 64, True, Tk=260)
@@ -450,6 +449,49 @@ def test_batchnorm(cuda, relu):
     assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
     for t, tf in ((x, xf), (w, wf), (b, bf_)):
         assert rel_err(t.grad, tf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("C", [64, 512])
+def test_batchnorm_residual_relu(cuda, C):
+    """ResNet block output in one pass: y = relu(BN(x) + r); grads of x, w, b and the residual r
+    (several row splits → the deterministic two-level statistics reduction)."""
+    torch.manual_seed(18)
+    N, H = 8, 28 if C == 64 else 7
+    x, r = bf(N, H, H, C).requires_grad_(), bf(N, H, H, C).requires_grad_()
+    w, b = bf(C).requires_grad_(), bf(C).requires_grad_()
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    y = ops.batch_norm_nhwc(x, w, b, rm, rv, True, 0.1, 1e-5, True, residual=r)
+    g = bf(*y.shape)
+    y.backward(g)
+    xf, rf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, r, w, b)]
+    rm2, rv2 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    yf = F.relu(F.batch_norm(xf.permute(0, 3, 1, 2), rm2, rv2, wf, bf_, True, 0.1, 1e-5).permute(0, 2, 3, 1) + rf)
+    yf.backward(g.float())
+    assert rel_err(y, yf) < 1e-2
+    assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
+    for t, tf in ((x, xf), (r, rf), (w, wf), (b, bf_)):
+        assert rel_err(t.grad, tf.grad) < 3e-2
+    # eval mode (running statistics) with the residual
+    ye = ops.batch_norm_nhwc(x.detach(), w.detach(), b.detach(), rm, rv, False, 0.1, 1e-5, True, residual=r.detach())
+    yef = F.relu(F.batch_norm(xf.detach().permute(0, 3, 1, 2), rm, rv, wf.detach(), bf_.detach(), False, 0.1,
+                              1e-5).permute(0, 2, 3, 1) + rf.detach())
+    assert rel_err(ye, yef) < 1e-2
+
+
+@pytest.mark.parametrize("C", [3, 16, 64])
+def test_maxpool_ties(cuda, C):
+    """Saved window indices: the gradient goes to the FIRST maximum of each window (ATen's rule),
+    also with many ties (small-integer inputs) and on the scalar path (C % 8 != 0)."""
+    torch.manual_seed(19)
+    x = torch.randint(0, 3, (2, 15, 15, C), device="cuda").to(torch.bfloat16).requires_grad_()
+    y = ops.maxpool_nhwc(x, 3, 2, 1)
+    g = bf(*y.shape)
+    y.backward(g)
+    xf = x.detach().float().requires_grad_()
+    yf = F.max_pool2d(xf.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    yf.backward(g.float())
+    assert torch.equal(y.float(), yf)
+    assert rel_err(x.grad, xf.grad) < 1e-2
 
 
 def test_pools(cuda):
