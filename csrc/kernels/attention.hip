@@ -115,6 +115,42 @@ RN_DEV s16x8 colfrag(const char* t, int rb, int c0, int lane) {
     return r;
 }
 
+// Per-lane parts of the rowfrag / colfrag LDS addresses, computed once per kernel.  Every call
+// site reads row X*16 + (lane&15) (rowfrag) or rows 32*ks + … / columns 16*jd + … (colfrag) with
+// X, ks, jd compile-time: the XOR swizzle then depends on the lane only, so the address is
+// base + per-lane offset + an immediate, instead of ~50 recomputed VALU address ops per tile.
+struct FragOff {
+    uint32_t rf[2];  // rowfrag, k-step s
+    uint32_t cf[4];  // colfrag, column block jd
+};
+RN_DEV FragOff make_fragoff(int lane) {
+    FragOff f;
+    const int g = lane >> 4, c = lane & 15;
+    const int swc = swz(c);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) f.rf[s] = c * 128 + ((((4 * s) + g) ^ swc) << 4);
+    const int qq = c >> 2, pp = c & 3;
+    const int r0 = 4 * g + qq;
+    const int swr = swz(r0);
+#pragma unroll
+    for (int jd = 0; jd < 4; ++jd) f.cf[jd] = r0 * 128 + (((2 * jd + (pp >> 1)) ^ swr) << 4) + (pp & 1) * 8;
+    return f;
+}
+// == rowfrag(t, X * 16 + (lane & 15), s, lane)
+RN_DEV s16x8 rowfragx(const char* t, int X, int s, const FragOff& f) {
+    return *reinterpret_cast<const s16x8*>(t + X * 2048 + f.rf[s]);
+}
+// == colfrag(t, 32 * ks, 16 * jd, lane)
+RN_DEV s16x8 colfragx(const char* t, int ks, int jd, const FragOff& f) {
+    const char* a0 = t + ks * 4096 + f.cf[jd];
+    s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 2048));
+    s16x8 r;
+    r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+    r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+    return r;
+}
+
 RN_DEV s16x8 gload16(const bf16* p, bool ok) {
     if (!ok) return (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
     return *reinterpret_cast<const s16x8*>(p);
@@ -390,6 +426,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const FragOff fo = make_fragoff(lane);
     // grid (B*H, blocks): the block index varies SLOWEST, so under causal masking every head's
     // heaviest query block is dispatched before any lighter one (longest-first over the grid)
     const int nqb = gridDim.y;
@@ -442,8 +479,8 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         s16x8 ka[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            ka[j][0] = rowfrag(kt, j * 16 + c, 0, lane);
-            ka[j][1] = rowfrag(kt, j * 16 + c, 1, lane);
+            ka[j][0] = rowfragx(kt, j, 0, fo);
+            ka[j][1] = rowfragx(kt, j, 1, fo);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -458,7 +495,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) va[s][jd] = colfrag(vt, 32 * s, 16 * jd, lane);
+            for (int jd = 0; jd < 4; ++jd) va[s][jd] = colfragx(vt, s, jd, fo);
         if constexpr (MASKED) {
 #pragma unroll
             for (int qi = 0; qi < 2; ++qi) {
@@ -580,6 +617,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const FragOff fo = make_fragoff(lane);
     // grid (B*H, key blocks): low key blocks see the most queries under causal and, with the block
     // index varying slowest, launch first across ALL heads (longest-first)
     const int kb = blockIdx.y;
@@ -651,10 +689,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
             f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
-            s16x8 a0 = rowfrag(qt_, qi * 16 + c, 0, lane), a1 = rowfrag(qt_, qi * 16 + c, 1, lane);
+            s16x8 a0 = rowfragx(qt_, qi, 0, fo), a1 = rowfragx(qt_, qi, 1, fo);
             sa = MFMA(a0, kf[0], sa, 0, 0, 0);
             sa = MFMA(a1, kf[1], sa, 0, 0, 0);
-            s16x8 o0 = rowfrag(ot_, qi * 16 + c, 0, lane), o1 = rowfrag(ot_, qi * 16 + c, 1, lane);
+            s16x8 o0 = rowfragx(ot_, qi, 0, fo), o1 = rowfragx(ot_, qi, 1, fo);
             da = MFMA(o0, vf[0], da, 0, 0, 0);
             da = MFMA(o1, vf[1], da, 0, 0, 0);
             // lane holds S[q = q0 + 16qi + 4g + r][kv]
@@ -698,9 +736,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
             s16x8 sb = pack_p(dsq[2 * ks], dsq[2 * ks + 1]);
 #pragma unroll
             for (int jd = 0; jd < 4; ++jd) {
-                s16x8 ao = colfrag(ot_, 32 * ks, 16 * jd, lane);
+                s16x8 ao = colfragx(ot_, ks, jd, fo);
                 dvacc[jd] = MFMA(ao, pb, dvacc[jd], 0, 0, 0);
-                s16x8 aq = colfrag(qt_, 32 * ks, 16 * jd, lane);
+                s16x8 aq = colfragx(qt_, ks, jd, fo);
                 dkacc[jd] = MFMA(aq, sb, dkacc[jd], 0, 0, 0);
             }
         }
@@ -748,6 +786,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const FragOff fo = make_fragoff(lane);
     const int nqb = gridDim.y;  // grid (B*H, query blocks): heaviest blocks of every head first
     const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
     const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
@@ -821,10 +860,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
-            sa = MFMA(rowfrag(kt, j * 16 + c, 0, lane), qf[0], sa, 0, 0, 0);
-            sa = MFMA(rowfrag(kt, j * 16 + c, 1, lane), qf[1], sa, 0, 0, 0);
-            da = MFMA(rowfrag(vt, j * 16 + c, 0, lane), df[0], da, 0, 0, 0);
-            da = MFMA(rowfrag(vt, j * 16 + c, 1, lane), df[1], da, 0, 0, 0);
+            sa = MFMA(rowfragx(kt, j, 0, fo), qf[0], sa, 0, 0, 0);
+            sa = MFMA(rowfragx(kt, j, 1, fo), qf[1], sa, 0, 0, 0);
+            da = MFMA(rowfragx(vt, j, 0, fo), df[0], da, 0, 0, 0);
+            da = MFMA(rowfragx(vt, j, 1, fo), df[1], da, 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int kvj = kv0 + j * 16 + 4 * g + r;
@@ -856,7 +895,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         for (int ks = 0; ks < 2; ++ks) {
             s16x8 sb = pack_p(dsv[2 * ks], dsv[2 * ks + 1]);
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfrag(kt, 32 * ks, 16 * jd, lane), sb, dqacc[jd], 0, 0, 0);
+            for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfragx(kt, ks, jd, fo), sb, dqacc[jd], 0, 0, 0);
         }
     };
     int t = 0;

@@ -15,7 +15,8 @@ from pathlib import Path
 
 import torch
 
-_SO = Path(__file__).resolve().parent / "_C.so"
+# REPLICANN_SO: load another build of the library (A/B timing of two kernel revisions only)
+_SO = Path(os.environ.get("REPLICANN_SO") or Path(__file__).resolve().parent / "_C.so")
 _state = {"loaded": False, "error": None}
 _ref = {"on": False}  # process-wide: autograd runs backward on its own device threads
 
