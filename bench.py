@@ -67,7 +67,7 @@ def main():
     cfg = TrainConfig(model=args.model, batch_size=args.batch, seq_len=args.seq, steps=10**9,
                       optimizer="adamw" if not args.model.startswith("resnet") else "sgd",
                       weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,
-                      warmup_steps=10, lr=6e-4, bucket_mb=args.bucket_mb, log_every=10**9,
+                      warmup_steps=10, lr=3e-4 if args.model.startswith("gpt2-medium") else 6e-4, bucket_mb=args.bucket_mb, log_every=10**9,
                       graph=args.graph)
     tr = Trainer(cfg)
     world = tr.world
@@ -124,7 +124,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
         "dtype": "bf16",
-        "data": "synthetic (random tokens, random-init weights)",
+        "data": ("synthetic (random bigram-chain token source, random-init weights)" if is_lm
+                 else "synthetic (random images and labels, random-init weights)"),
         "config": {
             "model": args.model,
             "global_batch": cfg.batch_size * world,

@@ -63,6 +63,7 @@ int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*,
 void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
 int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
+void rn_conv_wgrad_tile(int, int, int*, int*);
 int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int, int, int, long, long, long, int, int,
                  int, int, int, int, int, int, int, int, int, long, int, int, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -665,7 +666,9 @@ Tensor conv_wgrad_implicit(const Tensor& dy2, const Tensor& x, int64_t KH, int64
     TORCH_CHECK(dy2.size(0) == PIX, "conv wgrad: dy rows != output pixels");
     Tensor dw = at::empty({OC, K}, x.options());
     // split-K over the pixels so the (OC/128)×(K/128) tile grid fills the chip
-    const long tiles = (long)((OC + 127) / 128) * ((K + 127) / 128);
+    int bm, bn;
+    rn_conv_wgrad_tile(OC, K, &bm, &bn);
+    const long tiles = (long)((OC + bm - 1) / bm) * ((K + bn - 1) / bn);
     int split = 1;
     while (tiles * split < 512 && PIX / (split * 2) >= 1024) split *= 2;
     Tensor ws = split > 1 ? at::empty({(long)split * OC * K}, x.options().dtype(at::kFloat)) : Tensor();

@@ -43,6 +43,76 @@ __global__ void __launch_bounds__(256) im2col_k(const bf16* __restrict__ x, bf16
     }
 }
 
+// im2col for C % 8 != 0 (the 7×7×3 stem): one lane per 16-B chunk (8 consecutive k) of a
+// cols row, so every store is a whole 16 B and the row index is decoded once per chunk instead
+// of per element; the 8 taps of a chunk are walked incrementally (c, then kw, then kh).
+__global__ void __launch_bounds__(256) im2col_chunk_k(const bf16* __restrict__ x, bf16* __restrict__ cols, int N,
+                                                      int H, int W, int C, int KH, int KW, int S, int P, int OH,
+                                                      int OW, int Kp) {
+    const int chunks = Kp / 8, K = KH * KW * C;
+    const long total = (long)N * OH * OW * chunks;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const long row = i / chunks;
+        const int k0 = (int)(i - row * chunks) * 8;
+        const int ow = row % OW;
+        const long t = row / OW;
+        const int oh = t % OH, n = t / OH;
+        int kk = k0 / C, c = k0 - kk * C;
+        int kh = kk / KW, kw = kk - kh * KW;
+        const bf16* xn = x + (long)n * H * W * C;
+        s16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            short val = 0;
+            const int ih = oh * S - P + kh, iw = ow * S - P + kw;
+            if (k0 + e < K && ih >= 0 && ih < H && iw >= 0 && iw < W)
+                val = __builtin_bit_cast(short, xn[((long)ih * W + iw) * C + c]);
+            v[e] = val;
+            if (++c == C) {
+                c = 0;
+                if (++kw == KW) kw = 0, ++kh;
+            }
+        }
+        *reinterpret_cast<s16x8*>(cols + row * Kp + k0) = v;
+    }
+}
+
+// col2im gather for C % 8 == 0: one lane per (pixel, 8-channel chunk), 16-B loads/stores, only
+// the taps whose output position exists (stride-aligned) are visited.
+__global__ void __launch_bounds__(256) col2im_vec_k(const bf16* __restrict__ dcols, bf16* __restrict__ dx, int N,
+                                                    int H, int W, int C, int KH, int KW, int S, int P, int OH,
+                                                    int OW, int Kp) {
+    const int CV = C / 8;
+    const long total = (long)N * H * W * CV;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int cv = i % CV;
+        long t = i / CV;
+        const int w = t % W;
+        t /= W;
+        const int h = t % H, n = t / H;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        // first kh with (h + P - kh) % S == 0, then every S-th
+        for (int kh = (h + P) % S; kh < KH; kh += S) {
+            const int oh = (h + P - kh) / S;
+            if (h + P - kh < 0) break;
+            if (oh >= OH) continue;
+            for (int kw = (w + P) % S; kw < KW; kw += S) {
+                if (w + P - kw < 0) break;
+                const int ow = (w + P - kw) / S;
+                if (ow >= OW) continue;
+                float v[8];
+                load8(dcols + (((long)n * OH + oh) * OW + ow) * Kp + (kh * KW + kw) * C + cv * 8, v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] += v[e];
+            }
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)acc[e];
+        *reinterpret_cast<bf16x8*>(dx + i * 8) = o;
+    }
+}
+
 __global__ void __launch_bounds__(256) col2im_k(const bf16* __restrict__ dcols, bf16* __restrict__ dx, int N, int H,
                                                 int W, int C, int KH, int KW, int S, int P, int OH, int OW, int Kp) {
     const long total = (long)N * H * W * C;
@@ -336,12 +406,22 @@ extern "C" {
 void rn_im2col(const void* x, void* cols, int N, int H, int W, int C, int KH, int KW, int S, int P, int OH, int OW,
                int Kp, hipStream_t st) {
     const int vec = (C % 8 == 0);
-    long total = (long)N * OH * OW * KH * KW * (vec ? C / 8 : C);
+    if (!vec) {
+        im2col_chunk_k<<<gridn((long)N * OH * OW * (Kp / 8)), 256, 0, st>>>((const bf16*)x, (bf16*)cols, N, H, W, C,
+                                                                            KH, KW, S, P, OH, OW, Kp);
+        return;
+    }
+    long total = (long)N * OH * OW * KH * KW * (C / 8);
     im2col_k<<<gridn(total), 256, 0, st>>>((const bf16*)x, (bf16*)cols, N, H, W, C, KH, KW, S, P, OH, OW, Kp, vec);
 }
 
 void rn_col2im(const void* dcols, void* dx, int N, int H, int W, int C, int KH, int KW, int S, int P, int OH, int OW,
                int Kp, hipStream_t st) {
+    if (C % 8 == 0 && Kp % 8 == 0) {
+        col2im_vec_k<<<gridn((long)N * H * W * C / 8), 256, 0, st>>>((const bf16*)dcols, (bf16*)dx, N, H, W, C, KH, KW,
+                                                                      S, P, OH, OW, Kp);
+        return;
+    }
     col2im_k<<<gridn((long)N * H * W * C), 256, 0, st>>>((const bf16*)dcols, (bf16*)dx, N, H, W, C, KH, KW, S, P, OH, OW, Kp);
 }
 

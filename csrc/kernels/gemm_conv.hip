@@ -22,6 +22,30 @@ void conv_launch(GemmArgs& a, hipStream_t st) {
 
 extern "C" {
 
+// Weight-gradient tile (mode 3; M = output channels, N = taps × channels):
+//   0: 128×128, 4 waves   1: 64×192, 4 waves (M = 64: no half-empty tile)
+//   2: 128×192, 8 waves   3: 256×128, 8 waves
+// REPLICANN_CONVW=<v> forces one (A/B timing); otherwise the measured choice per shape.
+int rn_conv_wgrad_variant(int M, int N) {
+    static int forced = [] {
+        const char* e = getenv("REPLICANN_CONVW");
+        return e ? atoi(e) : -1;
+    }();
+    // measured (scripts/conv_ab.py, ResNet-18 B=256): 128×192 / 8 waves is fastest on every 3×3
+    // layer shape (layer1 0.368 → 0.246 ms, layers 2-4 0.18-0.19 → 0.11-0.135 ms vs 128×128)
+    int v = forced >= 0 ? forced : 2;
+    if ((v == 1 || v == 2) && N % 192 != 0) v = 0;
+    if (v == 1 && M != 64) v = 0;
+    if (v == 3 && M < 256) v = 0;
+    return v;
+}
+void rn_conv_wgrad_tile(int M, int N, int* bm, int* bn) {
+    static const int BMS[4] = {128, 64, 128, 256}, BNS[4] = {128, 192, 192, 128};
+    const int v = rn_conv_wgrad_variant(M, N);
+    *bm = BMS[v];
+    *bn = BNS[v];
+}
+
 // Returns 0, or -1 if the geometry is outside the implicit path (caller falls back to im2col).
 int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bias, float* ws, int M, int N, int K,
                  long lda, long ldb, long ldc, int H, int W, int Cg, int RH, int RW, int KH, int KW, int S, int P,
@@ -60,7 +84,12 @@ int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bi
     }
     if (mode == 3) {
         if (N % 64 != 0 || M % 8 != 0 || lda % 8 != 0) return -1;
-        conv_launch<128, 128, 2, 2, 3, false, false>(a, st);
+        switch (rn_conv_wgrad_variant(M, N)) {
+            case 1: conv_launch<64, 192, 1, 4, 3, false, false>(a, st); break;
+            case 2: conv_launch<128, 192, 2, 4, 3, false, false>(a, st); break;
+            case 3: conv_launch<256, 128, 4, 2, 3, false, false>(a, st); break;
+            default: conv_launch<128, 128, 2, 2, 3, false, false>(a, st); break;
+        }
         return 0;
     }
     return -1;

@@ -10,11 +10,34 @@ import torch
 
 
 class SyntheticLM:
-    """Random token sequences (B, T+1) → (inputs, next-token targets)."""
+    """Synthetic token sequences (B, T+1) → (inputs, next-token targets).
 
-    def __init__(self, batch, seq_len, vocab, device, pool=4, seed=0):
+    ``structured=True`` (default): a learnable source — tokens from a random
+    ``active``-id subset of the vocabulary, each followed by a fixed random
+    successor with probability ``p_follow`` (else a uniform active id), so a
+    model that trains correctly shows a falling loss within a few steps.  The
+    shapes, and therefore every kernel and its cost, are those of uniform
+    random tokens over the full vocabulary (``structured=False``); the logits
+    still span all ``vocab`` ids."""
+
+    def __init__(self, batch, seq_len, vocab, device, pool=4, seed=0, structured=True, active=1024,
+                 p_follow=0.75):
         g = torch.Generator(device="cpu").manual_seed(seed)
-        self.pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=g).to(device) for _ in range(pool)]
+        if not structured:
+            self.pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=g).to(device) for _ in range(pool)]
+        else:
+            active = min(active, vocab)
+            ids = torch.randperm(vocab, generator=g)[:active]
+            succ = torch.randint(0, active, (active,), generator=g)
+            self.pool = []
+            for _ in range(pool):
+                t = torch.empty(batch, seq_len + 1, dtype=torch.long)
+                t[:, 0] = torch.randint(0, active, (batch,), generator=g)
+                follow = torch.rand(batch, seq_len, generator=g) < p_follow
+                rnd = torch.randint(0, active, (batch, seq_len), generator=g)
+                for i in range(seq_len):
+                    t[:, i + 1] = torch.where(follow[:, i], succ[t[:, i]], rnd[:, i])
+                self.pool.append(ids[t].to(device))
         self.i = 0
 
     def __next__(self):

@@ -35,6 +35,7 @@ for step in "$@"; do
     mbattn) run mbattn 300 python scripts/microbench.py attn ln xent ;;
     det) run det 300 python -m pytest tests/test_determinism_gpu.py -q ;;
     stock) run stock 600 python scripts/bench_stock_torch.py --steps 10 --warmup 3 ;;
+    stock_all) for m in gpt2-small gpt2-medium vit-b16 resnet18; do run stock_$m 600 python scripts/bench_stock_torch.py --model $m --steps 5 --warmup 2; done ;;
     *) ncustom=$(( ${ncustom:-0} + 1 )); run custom$ncustom 600 bash -c "$step" ;;
   esac
 done

@@ -410,7 +410,8 @@ def test_conv2d(cuda, cfg):
 
 
 @pytest.mark.parametrize("C,OC,Kk,S,P,HW", [(64, 64, 3, 1, 1, 14), (64, 128, 3, 2, 1, 15), (128, 64, 3, 1, 1, 9),
-                                           (64, 128, 1, 2, 0, 16), (128, 128, 3, 1, 1, 7), (64, 64, 3, 1, 0, 10)])
+                                           (64, 128, 1, 2, 0, 16), (128, 128, 3, 1, 1, 7), (64, 64, 3, 1, 0, 10),
+                                           (64, 256, 3, 1, 1, 8)])
 def test_conv2d_implicit_gemm(cuda, C, OC, Kk, S, P, HW):
     """Implicit-GEMM path (channels % 64 == 0): fwd, dgrad (stride 1 implicit / stride 2 col2im), wgrad."""
     from replicann_amd.ops.conv import implicit_ok
