@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU micro-batch (default: 64 sequences for GPT-2, i.e. GPT-2's own 512-sequence "
-                         "global batch on 8 GPUs, sized for 288 GB HBM; 256 images ViT and ResNet)")
+                         "global batch on 8 GPUs, sized for 288 GB HBM; 512 images ViT, 256 ResNet)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra torch.profiler steps (not timed)")
@@ -62,8 +62,8 @@ def main():
         raise RuntimeError(f"native extension missing: {_ext.load_error()}")
 
     is_lm = args.model.startswith("gpt2")
-    if args.batch is None:
-        args.batch = 64 if is_lm else 256
+    if args.batch is None:  # ViT: 512 x 8 GPUs = ViT-B's 4096 global batch
+        args.batch = 64 if is_lm else (512 if args.model.startswith("vit") else 256)
     cfg = TrainConfig(model=args.model, batch_size=args.batch, seq_len=args.seq, steps=10**9,
                       optimizer="adamw" if not args.model.startswith("resnet") else "sgd",
                       weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,

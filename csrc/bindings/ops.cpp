@@ -65,7 +65,7 @@ int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
 void rn_conv_wgrad_tile(int, int, int*, int*);
 int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int, int, int, long, long, long, int, int,
-                 int, int, int, int, int, int, int, int, int, long, int, int, hipStream_t);
+                 int, int, int, int, int, int, int, int, int, long, int, int, int, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -84,7 +84,7 @@ void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, flo
 void rn_bn_eval(const void*, const void*, const void*, const float*, const float*, void*, int, int, float, int,
                 const void*, hipStream_t);
 void rn_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
-               float*, int, int, int, void*, hipStream_t);
+               float*, int, int, int, void*, int, hipStream_t);
 }
 
 namespace {
@@ -641,7 +641,7 @@ Tensor conv_fwd_implicit(const Tensor& x, const Tensor& w, const optional<Tensor
     if (M == 0) return y;
     if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == OC); }
     const int rc = rn_conv_gemm(1, x.data_ptr(), w.data_ptr(), y.data_ptr(), optr(bias), nullptr, M, OC, K, 0, K, OC, H,
-                                W, C, OH, OW, KH, KW, (int)S, (int)P, C, 0, 0, 1, 0, cur_stream());
+                                W, C, OH, OW, KH, KW, (int)S, (int)P, C, 0, 0, 1, 0, 0, cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv fwd: unsupported geometry");
     return y;
 }
@@ -654,27 +654,41 @@ Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t
     const int M = N * (int)H * (int)W, K = KH * KW * OC;
     if (M == 0) return dx;
     const int rc = rn_conv_gemm(2, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, nullptr, M, C, K, 0, 0, C, OH,
-                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0, cur_stream());
+                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0, 0, cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv dgrad: unsupported geometry");
     return dx;
 }
-Tensor conv_wgrad_implicit(const Tensor& dy2, const Tensor& x, int64_t KH, int64_t KW, int64_t S, int64_t P) {
+Tensor conv_wgrad_implicit(const Tensor& dy2, const Tensor& x, int64_t KH, int64_t KW, int64_t S, int64_t P,
+                           const optional<Tensor>& out, bool accumulate) {
     CHECK_BF16(dy2); CHECK_CONTIG(dy2); CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
     const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
     const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
     const int OC = dy2.size(1), PIX = N * OH * OW, K = KH * KW * C;
     TORCH_CHECK(dy2.size(0) == PIX, "conv wgrad: dy rows != output pixels");
-    Tensor dw = at::empty({OC, K}, x.options());
+    Tensor dw;
+    if (out && out->defined()) {  // e.g. the flat gradient view of the weight (accumulate: direct grad)
+        CHECK_BF16(*out); CHECK_CONTIG(*out);
+        TORCH_CHECK(out->numel() == (long)OC * K && out->device() == x.device(), "conv wgrad: out shape");
+        dw = *out;
+    } else {
+        TORCH_CHECK(!accumulate, "conv wgrad: accumulate needs out");
+        dw = at::empty({OC, K}, x.options());
+    }
     // split-K over the pixels so the (OC/128)×(K/128) tile grid fills the chip
     int bm, bn;
     rn_conv_wgrad_tile(OC, K, &bm, &bn);
     const long tiles = (long)((OC + bm - 1) / bm) * ((K + bn - 1) / bn);
     int split = 1;
-    while (tiles * split < 512 && PIX / (split * 2) >= 1024) split *= 2;
+    static const long target = [] {  // workgroups to aim for (REPLICANN_CONVW_TARGET: A/B only)
+        const char* e = getenv("REPLICANN_CONVW_TARGET");
+        return e ? atol(e) : 512L;
+    }();
+    while (tiles * split < target && PIX / (split * 2) >= 1024) split *= 2;
     Tensor ws = split > 1 ? at::empty({(long)split * OC * K}, x.options().dtype(at::kFloat)) : Tensor();
     const int rc = rn_conv_gemm(3, dy2.data_ptr(), x.data_ptr(), dw.data_ptr(), nullptr,
                                 ws.defined() ? ws.data_ptr<float>() : nullptr, OC, K, PIX, OC, 0, K, H, W, C, OH, OW,
-                                (int)KH, (int)KW, (int)S, (int)P, C, 0, 0, split, 0, cur_stream());
+                                (int)KH, (int)KW, (int)S, (int)P, C, 0, 0, split, 0, accumulate ? 1 : 0,
+                                cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv wgrad: unsupported geometry");
     return dw;
 }
@@ -764,17 +778,27 @@ Tensor batchnorm_eval(const Tensor& x, const Tensor& w, const Tensor& b, const T
 // returns (dx, dw, db, g') with g' = dy ⊙ relu'(y) (the fused residual's gradient) when want_gres
 std::tuple<Tensor, Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor& x, const Tensor& y,
                                                          const Tensor& w, const Tensor& mean, const Tensor& rstd,
-                                                         bool relu, bool want_gres) {
+                                                         bool relu, bool want_gres, const optional<Tensor>& dw_acc,
+                                                         const optional<Tensor>& db_acc) {
     check_bn(gy, c10::nullopt); GUARD(gy);
     const int M = x.size(0), C = x.size(1);
     Tensor dx = at::empty_like(x);
-    Tensor dw = at::empty({C}, x.options());  // bf16, the parameter dtype
-    Tensor db = at::empty({C}, x.options());
+    // dw_acc / db_acc: gradient views to ADD into (direct accumulation), both or neither
+    const bool acc = dw_acc && dw_acc->defined();
+    TORCH_CHECK(acc == (db_acc && db_acc->defined()), "batchnorm_bwd: dw_acc and db_acc go together");
+    if (acc) {
+        for (const Tensor* t : {&*dw_acc, &*db_acc}) {
+            CHECK_BF16(*t); CHECK_CONTIG(*t);
+            TORCH_CHECK(t->numel() == C && t->device() == x.device(), "batchnorm_bwd: accumulation target shape");
+        }
+    }
+    Tensor dw = acc ? *dw_acc : at::empty({C}, x.options());  // bf16, the parameter dtype
+    Tensor db = acc ? *db_acc : at::empty({C}, x.options());
     Tensor gres = want_gres ? at::empty_like(x) : at::empty({0}, x.options());
     Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
     rn_bn_bwd(gy.data_ptr(), x.data_ptr(), y.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
               dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr<float>(), M, C, relu,
-              want_gres ? gres.data_ptr() : nullptr, cur_stream());
+              want_gres ? gres.data_ptr() : nullptr, acc ? 1 : 0, cur_stream());
     return {dx, dw, db, gres};
 }
 
@@ -857,7 +881,8 @@ TORCH_LIBRARY(replicann, m) {
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("conv_fwd_implicit(Tensor x, Tensor w, Tensor? bias, int S, int P) -> Tensor");
     m.def("conv_dgrad_implicit(Tensor dy, Tensor w, int H, int W, int P) -> Tensor");
-    m.def("conv_wgrad_implicit(Tensor dy2, Tensor x, int KH, int KW, int S, int P) -> Tensor");
+    m.def("conv_wgrad_implicit(Tensor dy2, Tensor x, int KH, int KW, int S, int P, Tensor(a!)? out=None, "
+          "bool accumulate=False) -> Tensor");
     m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> (Tensor, Tensor)");
     m.def("maxpool_bwd(Tensor gy, Tensor idx, int H, int W, int K, int S, int P) -> Tensor");
@@ -868,7 +893,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu, "
           "Tensor? res=None) -> Tensor");
     m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu, "
-          "bool want_gres=False) -> (Tensor, Tensor, Tensor, Tensor)");
+          "bool want_gres=False, Tensor(c!)? dw_acc=None, Tensor(d!)? db_acc=None) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("fp8_quantize(Tensor x) -> (Tensor, Tensor)");
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");

@@ -158,7 +158,7 @@ __global__ void rn_colred2_k(const float* __restrict__ tmp, int S, int C, long l
     if (c >= C) return;
     float s = 0.f;
     for (int i = 0; i < S; ++i) s += tmp[(long)i * ld + c];
-    if (out32) out32[c] = s + (accum ? out32[c] : 0.f);
+    if (out32) out32[c] = s + (accum == 1 ? out32[c] : 0.f);
     if (out16) out16[c] = (__bf16)(s + (accum ? (float)out16[c] : 0.f));
 }
 
@@ -180,7 +180,7 @@ struct RnColOut {
     float* o32[3];
     __bf16* o16[3];
     int seg;
-    int accum[3];  // per segment: add into the outputs
+    int accum[3];  // per segment: 1 = add into both outputs, 2 = add into the bf16 output only
 };
 
 __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in, int R, int C,
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in,
 #pragma unroll
         for (int i = 0; i < RN_COLRED_S; ++i) acc += i < S ? t[i] : 0.f;
         const int k = c / out.seg, o = c - k * out.seg;
-        if (out.o32[k]) out.o32[k][o] = acc + (out.accum[k] ? out.o32[k][o] : 0.f);
+        if (out.o32[k]) out.o32[k][o] = acc + (out.accum[k] == 1 ? out.o32[k][o] : 0.f);
         if (out.o16[k]) out.o16[k][o] = (__bf16)(acc + (out.accum[k] ? (float)out.o16[k][o] : 0.f));
     }
     if (lane == 0) __hip_atomic_store(&rn_colsum_cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

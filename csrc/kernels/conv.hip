@@ -458,7 +458,7 @@ void rn_avgpool_bwd(const void* gy, void* dx, int N, int HW, int C, hipStream_t 
 long rn_bn_ws_floats(int M, int C) { return 2L * C * (bn_splits(M) + 1) + (long)RN_COLRED_S * 2 * C; }
 
 static void bn_stats(int mode, const void* a, const void* xin, const void* yv, const float* mean, const float* rstd,
-                     float* ws, int M, int C, int relu, void* db16, void* dw16, hipStream_t st) {
+                     float* ws, int M, int C, int relu, void* db16, void* dw16, hipStream_t st, int accum16 = 0) {
     const int S = bn_splits(M);
     const int rps = (M + S - 1) / S;
     float* part = ws;
@@ -469,7 +469,8 @@ static void bn_stats(int mode, const void* a, const void* xin, const void* yv, c
     else
         bn_part_k<1><<<S, BN_T, 0, st>>>((const bf16*)a, (const bf16*)xin, (const bf16*)yv, mean, rstd, part, M, C,
                                          rps, relu);
-    RnColOut o{{sums, sums + C, nullptr}, {(__bf16*)db16, (__bf16*)dw16, nullptr}, C, {0, 0, 0}};
+    const int a16 = accum16 ? 2 : 0;  // direct gradient accumulation: add into db16/dw16, never into sums
+    RnColOut o{{sums, sums + C, nullptr}, {(__bf16*)db16, (__bf16*)dw16, nullptr}, C, {a16, a16, 0}};
     rn_colreduce_seg(part, S, 2 * C, tmp, o, st);
 }
 
@@ -493,11 +494,13 @@ void rn_bn_eval(const void* x, const void* w, const void* b, const float* rmean,
                                                  (const bf16*)res, (bf16*)y, t8, C, eps, relu);
 }
 
-// dw/db: bf16 outputs [C] (the parameter dtype, written by the reduction itself); gres (optional):
+// dw/db: bf16 outputs [C] (the parameter dtype, written by the reduction itself; with `accum` ADDED
+// into them: the flat gradient buffer's views, no AccumulateGrad pass); gres (optional):
 // dy ⊙ relu'(y), the gradient of a fused residual input
 void rn_bn_bwd(const void* gy, const void* x, const void* y, const void* w, const float* mean, const float* rstd,
-               void* dx, void* dw, void* db, float* ws, int M, int C, int relu, void* gres, hipStream_t st) {
-    bn_stats(1, gy, x, y, mean, rstd, ws, M, C, relu, db, dw, st);
+               void* dx, void* dw, void* db, float* ws, int M, int C, int relu, void* gres, int accum,
+               hipStream_t st) {
+    bn_stats(1, gy, x, y, mean, rstd, ws, M, C, relu, db, dw, st, accum);
     const float* sums = ws + 2L * C * bn_splits(M);
     const long t8 = (long)M * C / 8;
     bn_bwd_apply_k<<<gridn(t8), 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const bf16*)y, (const bf16*)w, mean,

@@ -27,7 +27,12 @@ import torch
 import torch.nn.functional as F
 
 from .. import _ext
-from .linear import gemm
+from .linear import _direct_grad, _notify, gemm
+
+
+def weight_param(ctx):
+    w = ctx.weight
+    return w if isinstance(w, torch.nn.Parameter) and w.is_contiguous() else None
 
 
 def _out_hw(H, W, kh, kw, stride, pad):
@@ -51,6 +56,7 @@ class _ConvImplicitFn(torch.autograd.Function):
         w = weight.contiguous()
         y = ops.conv_fwd_implicit(x, w, bias, stride, pad)
         ctx.save_for_backward(x, w)
+        ctx.weight = weight  # the Parameter itself (direct gradient accumulation), not saved data
         ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None
         return y
 
@@ -66,7 +72,12 @@ class _ConvImplicitFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             _, gb = ops.bias_act_grad(gy2, None, 0, True)
         if ctx.needs_input_grad[1]:
-            gw = ops.conv_wgrad_implicit(gy2, x, KH, KW, ctx.stride, ctx.pad).reshape(OC, KH, KW, C)
+            w_acc = _direct_grad(weight_param(ctx))
+            if w_acc is not None and w_acc.dtype == torch.bfloat16:  # straight into the flat gradient buffer
+                ops.conv_wgrad_implicit(gy2, x, KH, KW, ctx.stride, ctx.pad, w_acc.view(OC, -1), True)
+                _notify(ctx.weight)
+            else:
+                gw = ops.conv_wgrad_implicit(gy2, x, KH, KW, ctx.stride, ctx.pad).reshape(OC, KH, KW, C)
         if ctx.needs_input_grad[0]:
             if ctx.stride == 1:
                 gx = ops.conv_dgrad_implicit(gy, w, H, W, ctx.pad)

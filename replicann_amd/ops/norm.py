@@ -113,6 +113,7 @@ class _BatchNormFn(torch.autograd.Function):
         y, mean, rstd = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
                                                  momentum, eps, relu, r2)
         ctx.save_for_backward(x2, y, weight, bias, mean, rstd)
+        ctx.params = (weight, bias)  # the Parameters themselves (direct gradient accumulation)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.shp = x.shape
@@ -120,11 +121,21 @@ class _BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        from .linear import _direct_grad, _notify
         x2, y, weight, bias, mean, rstd = ctx.saved_tensors
         C = ctx.shp[-1]
+        pw, pb = ctx.params
+        dw_acc, db_acc = _direct_grad(pw), _direct_grad(pb)
+        direct = (dw_acc is not None and db_acc is not None and dw_acc.dtype == torch.bfloat16
+                  and db_acc.dtype == torch.bfloat16)
         dx, dw, db, gres = _ext.ops().batchnorm_bwd(gy.reshape(-1, C).contiguous(), x2, y, weight, mean,
-                                                    rstd, ctx.relu, ctx.has_res)
+                                                    rstd, ctx.relu, ctx.has_res,
+                                                    dw_acc if direct else None, db_acc if direct else None)
         gr = gres.reshape(ctx.shp) if ctx.has_res else None
+        if direct:  # the reduction added dw / db into the flat gradient views
+            _notify(pw)
+            _notify(pb)
+            return dx.reshape(ctx.shp), None, None, None, None, None, None, None, gr
         return dx.reshape(ctx.shp), dw.to(weight.dtype), db.to(bias.dtype), None, None, None, None, None, gr
 
 

@@ -586,3 +586,28 @@ def test_mlp_fp8_matches_bf16(cuda):
         assert rel_err(y, ref) < 0.05
     y.float().pow(2).mean().backward()
     assert torch.isfinite(xs.grad.float()).all()
+
+
+def test_conv_bn_direct_grad_accumulation(cuda):
+    """Implicit-conv weight and BatchNorm weight/bias gradients added by the kernels straight into
+    the flat gradient buffer (no AccumulateGrad) equal autograd's, accumulated over two backwards."""
+    from replicann_amd.models.resnet import BasicBlock
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(23)
+    ref, blk = BasicBlock(64, 128, 2).cuda(), BasicBlock(64, 128, 2).cuda()
+    for m in (ref, blk):
+        for p in m.parameters():  # bf16 parameters, fp32 BN running statistics (as the Trainer does)
+            p.data = p.data.bfloat16()
+    blk.load_state_dict(ref.state_dict())
+    flat = FlatParams(blk, dtype=torch.bfloat16, device="cuda", grad_dtype=torch.bfloat16)
+    seen = []
+    flat.ready_hooks.append(lambda p: seen.append(id(p)))
+    xs = [bf(4, 16, 16, 64) for _ in range(2)]
+    for x in xs:
+        ref(x).float().square().mean().backward()
+        blk(x).float().square().mean().backward()
+    n_direct = 0
+    for (name, p), (_, q) in zip(ref.named_parameters(), blk.named_parameters()):
+        assert rel_err(q.grad, p.grad) < 2e-2, name
+        n_direct += id(q) in seen
+    assert n_direct >= 5  # conv1/conv2/shortcut weights + BN params took the direct path
