@@ -8,6 +8,6 @@ ARGS="${1:-64 --fwd 2 --bwd 1 --rounds 1}"
 timeout -k 10 60 rocprofv3 -L > gpurun_out/pmc_attn/counters.txt 2>&1 || true
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
    --kernel-trace --output-format csv -d gpurun_out/pmc_attn -o a -- python3 scripts/attn_ab.py $ARGS > /dev/null 2>&1
-timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VALU \
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE SQ_INSTS_MFMA \
    --kernel-trace --output-format csv -d gpurun_out/pmc_attn -o b -- python3 scripts/attn_ab.py $ARGS > /dev/null 2>&1
 ls gpurun_out/pmc_attn
