@@ -197,8 +197,14 @@ RN_DEV uint32_t lds_addr(const char* p) {
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is "reserved": declaring the clobber is still right
-RN_DEV void dma16_async(const u32x4& rs, uint32_t voff, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
+RN_DEV void dma16_async(const u32x4& rs_, uint32_t voff, uint32_t lds) {
+    // re-assert uniformity: after the loop unrolling the divergence analysis can lose track of the
+    // (readfirstlane-built) descriptor and hand the "s" constraint a VGPR tuple
+    u32x4 rs;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rs[i] = __builtin_amdgcn_readfirstlane(rs_[i]);
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+                 "s"(__builtin_amdgcn_readfirstlane(lds))
                  : "memory", "m0");
 }
 #pragma clang diagnostic pop
@@ -421,7 +427,13 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
 //     land under the softmax VALU work instead of being waited for between PV MFMAs;
 //   * QKᵀ issues the k-step-0 MFMAs of all 8 output tiles before the k-step-1 ones (no
 //     back-to-back dependent MFMAs).
-template <bool CAUSAL, int OCC>
+// LEAN (variant 3): (a) the O / l rescale by alpha = exp2(m_old - m_new) runs only when some row
+// of the wave raised its running max this tile (a wave-uniform ballot; after the first tiles the
+// max rarely moves), (b) the row sums of P come from the matrix cores — P·1 as two extra MFMAs
+// per query fragment against an all-ones A operand — instead of 32 v_add_f32 per tile.  Both
+// trade VALU issue slots, which bound this kernel at head_dim 64, for idle MFMA / scalar slots;
+// l then sums the bf16-rounded P that also feeds P·V.
+template <bool CAUSAL, int OCC, bool LEAN = false>
 __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -468,6 +480,8 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
         for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const short one = 0x3F80;  // bf16 1.0
+    [[maybe_unused]] const s16x8 ones = {one, one, one, one, one, one, one, one};
 
     auto tile = [&](const int t, auto masked_c) {
         constexpr bool MASKED = decltype(masked_c)::value;
@@ -477,6 +491,8 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         const int kv0 = t * 64;
         f32x4 sacc[2][4];
         s16x8 ka[4][2];
+        [[maybe_unused]] bool moved = false;
+        [[maybe_unused]] float alph[2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             ka[j][0] = rowfragx(kt, j, 0, fo);
@@ -526,6 +542,10 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
                 alpha = __builtin_amdgcn_exp2f((m[qi] - mn) * sl2);  // exp2(-inf) = 0 on the first tile
                 nms = -mn * sl2;
             }
+            if constexpr (LEAN) {
+                moved |= (mn != m[qi]);
+                alph[qi] = alpha;
+            }
             m[qi] = mn;
             float ls = 0.f;
 #pragma unroll
@@ -533,13 +553,26 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[qi][j][r], sl2, nms));
-                    ls += pv;
+                    if constexpr (!LEAN) ls += pv;
                     sacc[qi][j][r] = pv;
                 }
-            l[qi] = l[qi] * alpha + ls;
+            if constexpr (!LEAN) {
+                l[qi] = l[qi] * alpha + ls;
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alpha;
+                for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alpha;
+            }
         }
+        if constexpr (LEAN) {
+            if (__builtin_amdgcn_ballot_w64(moved)) {  // wave-uniform
+#pragma unroll
+                for (int qi = 0; qi < 2; ++qi) {
+                    l[qi] *= alph[qi];
+#pragma unroll
+                    for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alph[qi];
+                }
+            }
+        }
+        f32x4 lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             s16x8 pb[2];
@@ -549,6 +582,14 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
             for (int jd = 0; jd < 4; ++jd)
 #pragma unroll
                 for (int qi = 0; qi < 2; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
+            if constexpr (LEAN) {
+#pragma unroll
+                for (int qi = 0; qi < 2; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
+            }
+        }
+        if constexpr (LEAN) {
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi) l[qi] += lsum[qi][0];  // every row of P·1 holds the sum
         }
     };
     auto sync_prefetch = [&](int t) {
@@ -559,6 +600,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
             stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
         }
     };
+    // (not unrolled by buffer like the backward kernels: at occupancy 3 the unrolled loop spills)
     int t = 0;
     for (; t < nfull; ++t) {
         sync_prefetch(t);
@@ -574,7 +616,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
-        const float lt = sum4groups(l[qi]);
+        const float lt = LEAN ? l[qi] : sum4groups(l[qi]);  // LEAN: P·1 already summed over all 64 keys
         const int qg = q0 + qi * 16 + c;
         const float inv = lt > 0.f ? 1.f / lt : 0.f;
         if (qg < p.Tq) {
@@ -677,9 +719,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
         __syncthreads();
         if (qt + 1 < nqt) stage(qt + 1, ((qt - qt0) & 1) ^ 1);
     };
-    auto body = [&](int qt, auto masked_c) {
+    auto body = [&](int qt, auto masked_c, auto buf_c) {  // buf_c: compile-time buffer, see the forward
         constexpr bool MASKED = decltype(masked_c)::value;
-        const int cur = (qt - qt0) & 1;
+        constexpr int cur = decltype(buf_c)::value;
         const int q0 = qt * 64;
         const char* qt_ = Qt(cur);
         const char* ot_ = Ot(cur);
@@ -743,19 +785,29 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
             }
         }
     };
-    int qt = qt0;
-    for (; qt < nqt && masked_tile(qt); ++qt) {  // diagonal head
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    auto step = [&](int qt, auto masked_c, auto buf_c) {
         sync_stage(qt);
-        if (!(CAUSAL && qt * 64 + 63 + off < kvw)) body(qt, std::true_type{});  // wave-uniform skip
-    }
-    for (; qt < nqt && !masked_tile(qt); ++qt) {
-        sync_stage(qt);
-        body(qt, std::false_type{});
-    }
-    for (; qt < nqt; ++qt) {  // ragged tail
-        sync_stage(qt);
-        if (!(CAUSAL && qt * 64 + 63 + off < kvw)) body(qt, std::true_type{});
-    }
+        if (decltype(masked_c)::value && CAUSAL && qt * 64 + 63 + off < kvw) return;  // wave-uniform skip
+        body(qt, masked_c, buf_c);
+    };
+    // tiles [qt, end) with buffer (qt - qt0) & 1 resolved at compile time
+    auto run = [&](int qt, int end, auto masked_c) {
+        if (qt < end && ((qt - qt0) & 1)) step(qt++, masked_c, B1{});
+        for (; qt + 1 < end; qt += 2) {
+            step(qt, masked_c, B0{});
+            step(qt + 1, masked_c, B1{});
+        }
+        if (qt < end) step(qt++, masked_c, B0{});
+        return qt;
+    };
+    int qt = qt0, qe = qt0;
+    while (qe < nqt && masked_tile(qe)) ++qe;
+    qt = run(qt, qe, std::true_type{});  // diagonal head
+    while (qe < nqt && !masked_tile(qe)) ++qe;
+    qt = run(qt, qe, std::false_type{});
+    run(qt, nqt, std::true_type{});  // ragged tail
 #undef Qt
 #undef Ot
 #undef Lt
@@ -850,9 +902,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
         }
     };
-    auto body = [&](int t, auto masked_c) {
+    auto body = [&](int t, auto masked_c, auto buf_c) {  // buf_c: compile-time buffer, see the forward
         constexpr bool MASKED = decltype(masked_c)::value;
-        const int cur = t & 1;
+        constexpr int cur = decltype(buf_c)::value;
         const int kv0 = t * 64;
         const char* kt = Kt(cur);
         const char* vt = Vt(cur);
@@ -898,15 +950,26 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfragx(kt, ks, jd, fo), sb, dqacc[jd], 0, 0, 0);
         }
     };
-    int t = 0;
-    for (; t < nkv && !masked_tile(t); ++t) {
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    auto step = [&](int t, auto masked_c, auto buf_c) {
         sync_stage(t);
-        body(t, std::false_type{});
-    }
-    for (; t < nkv; ++t) {  // diagonal / ragged tail
-        sync_stage(t);
-        if (!(CAUSAL && t * 64 > qw + 15 + off)) body(t, std::true_type{});  // wave-uniform skip
-    }
+        if (decltype(masked_c)::value && CAUSAL && t * 64 > qw + 15 + off) return;  // wave-uniform skip
+        body(t, masked_c, buf_c);
+    };
+    auto run = [&](int t, int end, auto masked_c) {
+        if (t < end && (t & 1)) step(t++, masked_c, B1{});
+        for (; t + 1 < end; t += 2) {
+            step(t, masked_c, B0{});
+            step(t + 1, masked_c, B1{});
+        }
+        if (t < end) step(t++, masked_c, B0{});
+        return t;
+    };
+    int te = 0;
+    while (te < nkv && !masked_tile(te)) ++te;
+    const int t = run(0, te, std::false_type{});
+    run(t, nkv, std::true_type{});  // diagonal / ragged tail
     if (p.bsum) {  // dQ column partials; row = (b, 64-query block)
         const int E = p.H * 64;
         float* row = p.bsum + ((long)b * gridDim.y + qb) * 3 * E + h * 64;
@@ -1072,11 +1135,15 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast) {
         dim3 grid(B * H, (Tq + 127) / 128);
-        // REPLICANN_ATTN_FWD=1 selects the original single-loop kernel (read per call so one process
-        // can A/B them); default: the split-loop v2 (no bias / dropout) at 3 blocks per CU
+        // REPLICANN_ATTN_FWD=1 selects the original single-loop kernel, 2 the split-loop v2, 3 (default)
+        // v2 with the LEAN softmax bookkeeping (read per call so one process can A/B them); no bias /
+        // dropout in v2/v3, 3 blocks per CU
         const char* ev = std::getenv("REPLICANN_ATTN_FWD");
-        const int var = ev ? std::atoi(ev) : 2;
-        if (!bias && p_drop == 0.f && var >= 2) {
+        const int var = ev ? std::atoi(ev) : 3;  // 3 = v2 + LEAN softmax bookkeeping
+        if (!bias && p_drop == 0.f && var >= 3) {
+            if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
+            else attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
+        } else if (!bias && p_drop == 0.f && var == 2) {
             if (causal) attn_fwd64v2_k<true, 3><<<grid, 256, 32768, st>>>(a);
             else attn_fwd64v2_k<false, 3><<<grid, 256, 32768, st>>>(a);
         } else {

@@ -258,7 +258,7 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("fwd", ["1", "2"])
+@pytest.mark.parametrize("fwd", ["1", "2", "3"])
 def test_attention_kernel_variants(cuda, monkeypatch, fwd):
     """Both D=64 forward kernels (REPLICANN_ATTN_FWD) and the backward against the fp32 reference, incl.
     Tq != Tk (causal offset, ragged key blocks) so the masked / unmasked tile loops all run."""
