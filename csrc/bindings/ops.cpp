@@ -240,9 +240,10 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             // (e.g. 48 tiles × 5 = 240) beats the next power of two by up to 25 %
             // up to 128 slabs for tiny outputs over a huge K (e.g. a conv-stem weight gradient: 64×147
             // outputs, 3 M pixels), where even 16 splits leave most CUs idle
-            const int splits[12] = {1, 2, 3, 4, 5, 6, 8, 12, 16, 32, 64, 128};
+            // (7 and 14: 36 output tiles of 256² — GPT-2's 3072×768 weight gradients — × 7 = 252 WGs)
+            const int splits[16] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 24, 32, 64, 128};
             const long out_tiles = ((M + 255) / 256) * ((N + 255) / 256);
-            const int nsplit = split_k < 0 ? (out_tiles * 16 < 256 ? 12 : 9) : 1;
+            const int nsplit = split_k < 0 ? (out_tiles * 16 < 256 ? 16 : 12) : 1;
             Tensor tws = at::empty({rn_gemm_ws_floats(M, N, splits[nsplit - 1])}, a.options().dtype(at::kFloat));
             hipEvent_t e0, e1;
             (void)hipEventCreate(&e0);
