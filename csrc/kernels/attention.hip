@@ -51,6 +51,9 @@ struct AttnArgs {
     // optional [B * ceil(T/64)][3 * H * 64] fp32: per-64-row-block column sums of dQ | dK | dV
     // (the packed-QKV projection's bias gradient, reduced later) — fast path, self-attention
     float* bsum;
+    // lse units: the D = 64 forward kernels store log2(Σ exp) in base-2 units (the backward then
+    // needs one FMA per score, exp2(s·scale·log2e − lse2)); the generic forward stores natural log.
+    int lse_log2;
 };
 
 // Sum a wave-tile's [16 rows][64 cols] accumulator (lane holds row lane&15, cols 16jd+4g+r)
@@ -413,7 +416,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
                 *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
             }
             if (g == 0)
-                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * xs + log2f(lt)) * LN2 : INFINITY;
+                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * xs + log2f(lt)) : INFINITY;  // base 2
         }
     }
 }
@@ -627,7 +630,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
                 *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
             }
             if (g == 0)
-                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * sl2 + log2f(lt)) * LN2 : INFINITY;
+                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * sl2 + log2f(lt)) : INFINITY;  // base 2
         }
     }
 }
@@ -750,7 +753,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
                     if (qg < p.Tq && kv < p.Tk)
                         x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kv] * LOG2E;
                 }
-                float pv = __builtin_amdgcn_exp2f(x - ls[r] * LOG2E);
+                float pv = __builtin_amdgcn_exp2f(x - ls[r]);  // lse in base-2 units: one FMA with x
                 float dpv = da[r];
                 float pd = pv;
                 if constexpr (DROP) {
@@ -858,7 +861,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         df[s] = gload16(dobase + (long)qg * p.do_st + s * 32 + g * 8, qg < p.Tq);
     }
     const bool qok = qg < p.Tq;
-    const float lse2 = qok ? p.lse[((long)b * p.H + h) * p.Tq + qg] * LOG2E : INFINITY;
+    const float lse2 = qok ? p.lse[((long)b * p.H + h) * p.Tq + qg] : INFINITY;  // base-2 units
     // delta = rowsum(dO ∘ O), computed here from the dO fragments already in
     // registers (no separate delta kernel); written out for the dK/dV kernel.
     float dl;
@@ -1057,7 +1060,7 @@ __global__ void __launch_bounds__(256) attn_bwd_generic_k(AttnArgs p) {
         dl += dov[d] * bf2f(op[d]);
     }
     dl = block_sum(dl, red);
-    const float L = p.lse[((long)b * p.H + h) * p.Tq + qi];
+    const float L = p.lse[((long)b * p.H + h) * p.Tq + qi] * (p.lse_log2 ? LN2 : 1.f);
     const float rd = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
     for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
         const bf16* kp = p.k + b * p.k_sb + (long)kj * p.k_st + h * p.k_sh;
@@ -1176,6 +1179,9 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
                       (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
                       (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
     if (bsum && !(fast && Tq == Tk)) return -2;  // bias partials: fast self-attention path only
+    // the forward chose its path with its own stride test: lse is base 2 iff that one was fast
+    a.lse_log2 = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
+    if (fast && !a.lse_log2) return -1;  // cannot happen (the backward test is stricter); never mix units
     if (fast) {
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2(B * H, (Tq + 63) / 64);
