@@ -18,7 +18,8 @@ class SyntheticLM:
     model that trains correctly shows a falling loss within a few steps.  The
     shapes, and therefore every kernel and its cost, are those of uniform
     random tokens over the full vocabulary (``structured=False``); the logits
-    still span all ``vocab`` ids."""
+    still span all ``vocab`` ids.  The source (id subset, successor table) is
+    shared by all data-parallel ranks; ``seed`` only draws the sequences."""
 
     def __init__(self, batch, seq_len, vocab, device, pool=4, seed=0, structured=True, active=1024,
                  p_follow=0.75):
@@ -27,8 +28,9 @@ class SyntheticLM:
             self.pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=g).to(device) for _ in range(pool)]
         else:
             active = min(active, vocab)
-            ids = torch.randperm(vocab, generator=g)[:active]
-            succ = torch.randint(0, active, (active,), generator=g)
+            gs = torch.Generator(device="cpu").manual_seed(1234)  # the SAME source on every rank
+            ids = torch.randperm(vocab, generator=gs)[:active]
+            succ = torch.randint(0, active, (active,), generator=gs)
             self.pool = []
             for _ in range(pool):
                 t = torch.empty(batch, seq_len + 1, dtype=torch.long)
