@@ -835,18 +835,21 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     }
 }
 
-// dQ: grid (ceil(Tq/64), B*H); wave w owns queries q0 + 16w + (lane&15)
-template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 2>
+// dQ: grid (B*H, ceil(Tq/(64·QG))); query group qg (< QG) of wave w owns queries
+// qb·64·QG + 64·qg + 16w + (lane&15).  With QG = 2 every K / V fragment read from LDS feeds
+// the MFMAs of two query groups (half the LDS reads per MFMA) and each wave carries two
+// independent dependency chains (S → P → dS → dQ) for the scheduler to interleave.
+template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 2, int QG = 1>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const FragOff fo = make_fragoff(lane);
+    constexpr int QB = 64 * QG;  // queries per block
     const int nqb = gridDim.y;  // grid (B*H, query blocks): heaviest blocks of every head first
     const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
     const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-    const int qw = qb * 64 + wave * 16;
-    const int qg = qw + c;
+    const int qw_last = qb * QB + 64 * (QG - 1) + wave * 16;  // this wave's first query of its LAST group
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
 
@@ -854,37 +857,43 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     const bf16* dobase = p.dout + b * p.do_sb + h * p.do_sh;
     const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + h * p.k_sh);
     const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
-    s16x8 qf[2], df[2];
+    int qgl[QG];
+    bool qok[QG];
+    s16x8 qf[QG][2], df[QG][2];
+    float lse2[QG], dl[QG];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        qf[s] = gload16(qbase + (long)qg * p.q_st + s * 32 + g * 8, qg < p.Tq);
-        df[s] = gload16(dobase + (long)qg * p.do_st + s * 32 + g * 8, qg < p.Tq);
-    }
-    const bool qok = qg < p.Tq;
-    const float lse2 = qok ? p.lse[((long)b * p.H + h) * p.Tq + qg] : INFINITY;  // base-2 units
-    // delta = rowsum(dO ∘ O), computed here from the dO fragments already in
-    // registers (no separate delta kernel); written out for the dK/dV kernel.
-    float dl;
-    {
+    for (int u = 0; u < QG; ++u) {
+        qgl[u] = qb * QB + 64 * u + wave * 16 + c;
+        qok[u] = qgl[u] < p.Tq;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            qf[u][s] = gload16(qbase + (long)qgl[u] * p.q_st + s * 32 + g * 8, qok[u]);
+            df[u][s] = gload16(dobase + (long)qgl[u] * p.do_st + s * 32 + g * 8, qok[u]);
+        }
+        lse2[u] = qok[u] ? p.lse[((long)b * p.H + h) * p.Tq + qgl[u]] : INFINITY;  // base-2 units
+        // delta = rowsum(dO ∘ O), computed here from the dO fragments already in
+        // registers (no separate delta kernel); written out for the dK/dV kernel.
         const bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
         float part = 0.f;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            s16x8 of = gload16(obase + (long)qg * p.o_st + s * 32 + g * 8, qok);
+            s16x8 of = gload16(obase + (long)qgl[u] * p.o_st + s * 32 + g * 8, qok[u]);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                part += (float)__builtin_bit_cast(bf16, (short)of[j]) * (float)__builtin_bit_cast(bf16, (short)df[s][j]);
+                part += (float)__builtin_bit_cast(bf16, (short)of[j]) * (float)__builtin_bit_cast(bf16, (short)df[u][s][j]);
         }
-        dl = sum4groups(part);
-        if (qok && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qg] = dl;
+        dl[u] = sum4groups(part);
+        if (qok[u] && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qgl[u]] = dl[u];
+        asm volatile("" : "+v"(qf[u][0]), "+v"(qf[u][1]), "+v"(df[u][0]), "+v"(df[u][1]), "+v"(dl[u]));  // loads retired here
     }
-    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(df[0]), "+v"(df[1]), "+v"(dl));  // loads retired here
-    f32x4 dqacc[4];
+    f32x4 dqacc[QG][4];
 #pragma unroll
-    for (int jd = 0; jd < 4; ++jd) dqacc[jd] = (f32x4){0, 0, 0, 0};
+    for (int u = 0; u < QG; ++u)
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) dqacc[u][jd] = (f32x4){0, 0, 0, 0};
 
     int kv_end = p.Tk;
-    if (CAUSAL) kv_end = min(p.Tk, qb * 64 + 64 + off);
+    if (CAUSAL) kv_end = min(p.Tk, qb * QB + QB + off);
     const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
 #define Kt(i) (smem + (i) * 16384)
 #define Vt(i) (smem + 8192 + (i) * 16384)
@@ -895,7 +904,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     // masked (diagonal / ragged) and unmasked tiles in separate loops, see the dK/dV kernel
     auto masked_tile = [&](int t) {
-        return (t * 64 + 64 > p.Tk) || (qb * 64 + 64 > p.Tq) || (CAUSAL && t * 64 + 63 > qb * 64 + off);
+        return (t * 64 + 64 > p.Tk) || (qb * QB + QB > p.Tq) || (CAUSAL && t * 64 + 63 > qb * QB + off);
     };
     auto sync_stage = [&](int t) {
         vm_wait_all();
@@ -905,86 +914,113 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
         }
     };
-    auto body = [&](int t, auto masked_c, auto buf_c) {  // buf_c: compile-time buffer, see the forward
+    auto body = [&](int t, auto masked_c, auto buf_c) {
         constexpr bool MASKED = decltype(masked_c)::value;
-        constexpr int cur = decltype(buf_c)::value;
+        constexpr int cur = decltype(buf_c)::value;  // compile-time buffer, see the dK/dV kernel
         const int kv0 = t * 64;
         const char* kt = Kt(cur);
         const char* vt = Vt(cur);
-        f32x4 dsv[4];
+        f32x4 dsv[QG][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
-            sa = MFMA(rowfragx(kt, j, 0, fo), qf[0], sa, 0, 0, 0);
-            sa = MFMA(rowfragx(kt, j, 1, fo), qf[1], sa, 0, 0, 0);
-            da = MFMA(rowfragx(vt, j, 0, fo), df[0], da, 0, 0, 0);
-            da = MFMA(rowfragx(vt, j, 1, fo), df[1], da, 0, 0, 0);
+            const s16x8 k0 = rowfragx(kt, j, 0, fo), k1 = rowfragx(kt, j, 1, fo);
+            const s16x8 v0 = rowfragx(vt, j, 0, fo), v1 = rowfragx(vt, j, 1, fo);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int kvj = kv0 + j * 16 + 4 * g + r;
-                float x = sa[r] * sl2;
-                if constexpr (BIAS) {
-                    if (qok && kvj < p.Tk)
-                        x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvj] * LOG2E;
+            for (int u = 0; u < QG; ++u) {
+                f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
+                sa = MFMA(k0, qf[u][0], sa, 0, 0, 0);
+                sa = MFMA(k1, qf[u][1], sa, 0, 0, 0);
+                da = MFMA(v0, df[u][0], da, 0, 0, 0);
+                da = MFMA(v1, df[u][1], da, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int kvj = kv0 + j * 16 + 4 * g + r;
+                    float x = sa[r] * sl2;
+                    if constexpr (BIAS) {
+                        if (qok[u] && kvj < p.Tk)
+                            x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qgl[u]) * p.Tk + kvj] * LOG2E;
+                    }
+                    float pv = __builtin_amdgcn_exp2f(x - lse2[u]);
+                    float dpv = da[r];
+                    if constexpr (DROP) {
+                        const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qgl[u], kvj)) >= p.p_drop;
+                        dpv = keep ? dpv * rd : 0.f;
+                    }
+                    dsv[u][j][r] = pv * (dpv - dl[u]);
                 }
-                float pv = __builtin_amdgcn_exp2f(x - lse2);
-                float dpv = da[r];
-                if constexpr (DROP) {
-                    const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qg, kvj)) >= p.p_drop;
-                    dpv = keep ? dpv * rd : 0.f;
-                }
-                dsv[j][r] = pv * (dpv - dl);
             }
         }
         if constexpr (MASKED) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int u = 0; u < QG; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int kvj = kv0 + j * 16 + 4 * g + r;
-                    if (kvj >= p.Tk || !qok || (CAUSAL && kvj > qg + off)) dsv[j][r] = 0.f;
-                }
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int kvj = kv0 + j * 16 + 4 * g + r;
+                        if (kvj >= p.Tk || !qok[u] || (CAUSAL && kvj > qgl[u] + off)) dsv[u][j][r] = 0.f;
+                    }
         }
         // dQ^T[d][q] += K^T[d][kv] dS^T[kv][q]
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            s16x8 sb = pack_p(dsv[2 * ks], dsv[2 * ks + 1]);
+            s16x8 sb[QG];
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) dqacc[jd] = MFMA(colfragx(kt, ks, jd, fo), sb, dqacc[jd], 0, 0, 0);
+            for (int u = 0; u < QG; ++u) sb[u] = pack_p(dsv[u][2 * ks], dsv[u][2 * ks + 1]);
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                const s16x8 kc = colfragx(kt, ks, jd, fo);
+#pragma unroll
+                for (int u = 0; u < QG; ++u) dqacc[u][jd] = MFMA(kc, sb[u], dqacc[u][jd], 0, 0, 0);
+            }
         }
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
     auto step = [&](int t, auto masked_c, auto buf_c) {
         sync_stage(t);
-        if (decltype(masked_c)::value && CAUSAL && t * 64 > qw + 15 + off) return;  // wave-uniform skip
-        body(t, masked_c, buf_c);
+        // wave-uniform skip: every query of this wave (its last group included) precedes the tile
+        if (decltype(masked_c)::value && CAUSAL && t * 64 > qw_last + 15 + off) return;
+        [[clang::always_inline]] body(t, masked_c, buf_c);
     };
+    // (always_inline: with two query groups hipcc otherwise outlines the causal masked step into a
+    // real call whose captured state round-trips through scratch)
     auto run = [&](int t, int end, auto masked_c) {
-        if (t < end && (t & 1)) step(t++, masked_c, B1{});
+        if (t < end && (t & 1)) [[clang::always_inline]] step(t++, masked_c, B1{});
         for (; t + 1 < end; t += 2) {
-            step(t, masked_c, B0{});
-            step(t + 1, masked_c, B1{});
+            [[clang::always_inline]] step(t, masked_c, B0{});
+            [[clang::always_inline]] step(t + 1, masked_c, B1{});
         }
-        if (t < end) step(t++, masked_c, B0{});
+        if (t < end) [[clang::always_inline]] step(t++, masked_c, B0{});
         return t;
     };
     int te = 0;
     while (te < nkv && !masked_tile(te)) ++te;
     const int t = run(0, te, std::false_type{});
     run(t, nkv, std::true_type{});  // diagonal / ragged tail
-    if (p.bsum) {  // dQ column partials; row = (b, 64-query block)
-        const int E = p.H * 64;
-        float* row = p.bsum + ((long)b * gridDim.y + qb) * 3 * E + h * 64;
-        block_colsum64(dqacc, p.scale, reinterpret_cast<float*>(smem), row, wave, lane);
-    }
-    if (qok) {
-        bf16* dqp = p.dq + b * p.dq_sb + (long)qg * p.dq_st + h * p.dq_sh;
+#undef Kt
+#undef Vt
+    if (p.bsum) {  // dQ column partials; row = (b, 64-query block) — the dK/dV kernel's row layout
+        const int E = p.H * 64, nb64 = (p.Tq + 63) / 64;
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) {
-            bf16x4 q4 = {(bf16)(dqacc[jd][0] * p.scale), (bf16)(dqacc[jd][1] * p.scale),
-                         (bf16)(dqacc[jd][2] * p.scale), (bf16)(dqacc[jd][3] * p.scale)};
-            *reinterpret_cast<bf16x4*>(dqp + jd * 16 + 4 * g) = q4;
+        for (int u = 0; u < QG; ++u) {
+            const int blk = qb * QG + u;
+            if (blk < nb64) {  // block-uniform
+                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * 64;
+                block_colsum64(dqacc[u], p.scale, reinterpret_cast<float*>(smem), row, wave, lane);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < QG; ++u) {
+        if (qok[u]) {
+            bf16* dqp = p.dq + b * p.dq_sb + (long)qgl[u] * p.dq_st + h * p.dq_sh;
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                bf16x4 q4 = {(bf16)(dqacc[u][jd][0] * p.scale), (bf16)(dqacc[u][jd][1] * p.scale),
+                             (bf16)(dqacc[u][jd][2] * p.scale), (bf16)(dqacc[u][jd][3] * p.scale)};
+                *reinterpret_cast<bf16x4*>(dqp + jd * 16 + 4 * g) = q4;
+            }
         }
     }
 }
@@ -1186,7 +1222,17 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2(B * H, (Tq + 63) / 64);
         dim3 g1(B * H, (Tk + 63) / 64);
-        RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
+        // REPLICANN_ATTN_DQ: 2 (default) = two 64-query groups per wave (plain causal / non-causal;
+        // bwd -11 % at GPT-2-small shapes), 1 = one
+        const char* eq = std::getenv("REPLICANN_ATTN_DQ");
+        const int dqv = eq ? std::atoi(eq) : 2;
+        if (dqv >= 2 && !bias && p_drop == 0.f) {
+            dim3 g2b(B * H, (Tq + 127) / 128);
+            if (causal) attn_bwd_dq64_k<true, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
+            else attn_bwd_dq64_k<false, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
+        } else {
+            RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
+        }
         RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
     } else {
         if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;

@@ -258,11 +258,12 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("fwd", ["1", "2", "3"])
-def test_attention_kernel_variants(cuda, monkeypatch, fwd):
+@pytest.mark.parametrize("fwd,dq", [("1", "1"), ("2", "1"), ("3", "1"), ("3", "2")])
+def test_attention_kernel_variants(cuda, monkeypatch, fwd, dq):
     """Both D=64 forward kernels (REPLICANN_ATTN_FWD) and the backward against the fp32 reference, incl.
     Tq != Tk (causal offset, ragged key blocks) so the masked / unmasked tile loops all run."""
     monkeypatch.setenv("REPLICANN_ATTN_FWD", fwd)
+    monkeypatch.setenv("REPLICANN_ATTN_DQ", dq)  # dQ kernel: 1 or 2 query groups per wave
     torch.manual_seed(70)
     _attn_check(2, 320, 3, 64, True)
     _attn_check(1, 100, 2, 64, True, Tk=260)
@@ -296,9 +297,11 @@ def test_attention_packed_grad(cuda):
     assert rel_err(o, of) < 2e-2 and rel_err(qkv.grad, qf.grad) < 4e-2
 
 
-@pytest.mark.parametrize("causal,T", [(True, 256), (False, 200)])
-def test_attention_packed_qkv_bias_grad(cuda, causal, T):
-    """Σ_rows dQKV (the c_attn bias gradient) reduced inside the attention backward kernels."""
+@pytest.mark.parametrize("causal,T,dq", [(True, 256, "1"), (False, 200, "1"), (True, 320, "2"), (False, 200, "2")])
+def test_attention_packed_qkv_bias_grad(cuda, monkeypatch, causal, T, dq):
+    """Σ_rows dQKV (the c_attn bias gradient) reduced inside the attention backward kernels
+    (incl. the two-query-group dQ kernel with an odd number of 64-query blocks)."""
+    monkeypatch.setenv("REPLICANN_ATTN_DQ", dq)
     from replicann_amd.utils.flat import FlatParams
     torch.manual_seed(11)
     B, H, D = 3, 4, 64
