@@ -656,19 +656,24 @@ __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
     const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + q] = s;
 }
 
-// dK, dV: grid (ceil(Tk/64), B*H); wave w owns keys kv0 + 16w + (lane&15)
-template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 3>
+// dK, dV: grid (B*H, ceil(Tk/(64·KG))); key group u (< KG) of wave w owns keys
+// kb·64·KG + 64·u + 16w + (lane&15).  KG = 2: every Q / dO fragment read from LDS feeds both key
+// groups' MFMAs and each wave carries two independent S → P → dS chains (as in the dQ kernel).
+template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 3, int KG = 1>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const FragOff fo = make_fragoff(lane);
+    constexpr int KB = 64 * KG;  // keys per block
     // grid (B*H, key blocks): low key blocks see the most queries under causal and, with the block
     // index varying slowest, launch first across ALL heads (longest-first)
     const int kb = blockIdx.y;
     const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-    const int kvw = kb * 64 + wave * 16;  // this wave's first key
-    const int kv = kvw + c;
+    const int kvw = kb * KB + wave * 16;  // this wave's first key (group 0)
+    int kvl[KG];
+#pragma unroll
+    for (int u = 0; u < KG; ++u) kvl[u] = kvw + 64 * u + c;
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
 
@@ -681,7 +686,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
 
     int qt0 = 0;
-    if (CAUSAL) qt0 = max(0, (kb * 64 - off)) / 64;
+    if (CAUSAL) qt0 = max(0, (kb * KB - off)) / 64;
     const int nqt = (p.Tq + 63) / 64;
     // buffer i: Q tile [0, 8K), dO tile [8K, 16K), lse [16K, 17K), delta [17K, 18K)
 #define Qt(i) (smem + (i) * 18432)
@@ -699,23 +704,28 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     };
     if (qt0 < nqt) stage(qt0, 0);
 
-    s16x8 kf[2], vf[2];
+    s16x8 kf[KG][2], vf[KG][2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        kf[s] = gload16(kbase + (long)kv * p.k_st + s * 32 + g * 8, kv < p.Tk);
-        vf[s] = gload16(vbase + (long)kv * p.v_st + s * 32 + g * 8, kv < p.Tk);
+    for (int u = 0; u < KG; ++u) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            kf[u][s] = gload16(kbase + (long)kvl[u] * p.k_st + s * 32 + g * 8, kvl[u] < p.Tk);
+            vf[u][s] = gload16(vbase + (long)kvl[u] * p.v_st + s * 32 + g * 8, kvl[u] < p.Tk);
+        }
+        asm volatile("" : "+v"(kf[u][0]), "+v"(kf[u][1]), "+v"(vf[u][0]), "+v"(vf[u][1]));  // wait here, not in the loop
     }
-    asm volatile("" : "+v"(kf[0]), "+v"(kf[1]), "+v"(vf[0]), "+v"(vf[1]));  // wait for them here, not in the loop
-    f32x4 dvacc[4], dkacc[4];
+    f32x4 dvacc[KG][4], dkacc[KG][4];
 #pragma unroll
-    for (int jd = 0; jd < 4; ++jd) { dvacc[jd] = (f32x4){0, 0, 0, 0}; dkacc[jd] = (f32x4){0, 0, 0, 0}; }
+    for (int u = 0; u < KG; ++u)
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) { dvacc[u][jd] = (f32x4){0, 0, 0, 0}; dkacc[u][jd] = (f32x4){0, 0, 0, 0}; }
 
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     // Tiles split into masked (causal diagonal of this block's keys, ragged Tq / Tk) and unmasked
     // ones, each class in its own loop: a per-wave `continue` or a runtime mask branch inside one
     // loop makes hipcc carry the accumulators through a phi (a VGPR copy block every tile).
     auto masked_tile = [&](int qt) {
-        return (qt * 64 + 64 > p.Tq) || (kb * 64 + 64 > p.Tk) || (CAUSAL && kb * 64 + 63 > qt * 64 + off);
+        return (qt * 64 + 64 > p.Tq) || (kb * KB + KB > p.Tk) || (CAUSAL && kb * KB + KB - 1 > qt * 64 + off);
     };
     auto sync_stage = [&](int qt) {
         vm_wait_all();
@@ -730,61 +740,75 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
         const char* ot_ = Ot(cur);
         const float* lt_ = reinterpret_cast<const float*>(Lt(cur));
         const float* dt_ = reinterpret_cast<const float*>(Dt(cur));
-        f32x4 pq[4], dsq[4];
+        f32x4 pq[KG][4], dsq[KG][4];
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
-            f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
-            s16x8 a0 = rowfragx(qt_, qi, 0, fo), a1 = rowfragx(qt_, qi, 1, fo);
-            sa = MFMA(a0, kf[0], sa, 0, 0, 0);
-            sa = MFMA(a1, kf[1], sa, 0, 0, 0);
-            s16x8 o0 = rowfragx(ot_, qi, 0, fo), o1 = rowfragx(ot_, qi, 1, fo);
-            da = MFMA(o0, vf[0], da, 0, 0, 0);
-            da = MFMA(o1, vf[1], da, 0, 0, 0);
+            const s16x8 a0 = rowfragx(qt_, qi, 0, fo), a1 = rowfragx(qt_, qi, 1, fo);
+            const s16x8 o0 = rowfragx(ot_, qi, 0, fo), o1 = rowfragx(ot_, qi, 1, fo);
             // lane holds S[q = q0 + 16qi + 4g + r][kv]
             const int ql = qi * 16 + 4 * g;
             const float4 l4 = *reinterpret_cast<const float4*>(lt_ + ql);
             const float4 d4 = *reinterpret_cast<const float4*>(dt_ + ql);
             const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int qg = q0 + ql + r;
-                float x = sa[r] * sl2;
-                if constexpr (BIAS) {
-                    if (qg < p.Tq && kv < p.Tk)
-                        x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kv] * LOG2E;
+            for (int u = 0; u < KG; ++u) {
+                f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
+                sa = MFMA(a0, kf[u][0], sa, 0, 0, 0);
+                sa = MFMA(a1, kf[u][1], sa, 0, 0, 0);
+                da = MFMA(o0, vf[u][0], da, 0, 0, 0);
+                da = MFMA(o1, vf[u][1], da, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int qg = q0 + ql + r;
+                    float x = sa[r] * sl2;
+                    if constexpr (BIAS) {
+                        if (qg < p.Tq && kvl[u] < p.Tk)
+                            x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvl[u]] * LOG2E;
+                    }
+                    float pv = __builtin_amdgcn_exp2f(x - ls[r]);  // lse in base-2 units: one FMA with x
+                    float dpv = da[r];
+                    float pd = pv;
+                    if constexpr (DROP) {
+                        const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qg, kvl[u])) >= p.p_drop;
+                        pd = keep ? pv * rd : 0.f;
+                        dpv = keep ? dpv * rd : 0.f;
+                    }
+                    pq[u][qi][r] = pd;
+                    dsq[u][qi][r] = pv * (dpv - dl[r]);
                 }
-                float pv = __builtin_amdgcn_exp2f(x - ls[r]);  // lse in base-2 units: one FMA with x
-                float dpv = da[r];
-                float pd = pv;
-                if constexpr (DROP) {
-                    const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qg, kv)) >= p.p_drop;
-                    pd = keep ? pv * rd : 0.f;
-                    dpv = keep ? dpv * rd : 0.f;
-                }
-                pq[qi][r] = pd;
-                dsq[qi][r] = pv * (dpv - dl[r]);
             }
         }
         if constexpr (MASKED) {
 #pragma unroll
-            for (int qi = 0; qi < 4; ++qi)
+            for (int u = 0; u < KG; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int qg = q0 + qi * 16 + 4 * g + r;
-                    if (kv >= p.Tk || qg >= p.Tq || (CAUSAL && kv > qg + off)) { pq[qi][r] = 0.f; dsq[qi][r] = 0.f; }
-                }
+                for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int qg = q0 + qi * 16 + 4 * g + r;
+                        if (kvl[u] >= p.Tk || qg >= p.Tq || (CAUSAL && kvl[u] > qg + off)) {
+                            pq[u][qi][r] = 0.f;
+                            dsq[u][qi][r] = 0.f;
+                        }
+                    }
         }
         // dV^T[d][kv] += dO^T[d][q] Pd[q][kv];  dK^T[d][kv] += Q^T[d][q] dS[q][kv]
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            s16x8 pb = pack_p(pq[2 * ks], pq[2 * ks + 1]);
-            s16x8 sb = pack_p(dsq[2 * ks], dsq[2 * ks + 1]);
+            s16x8 pb[KG], sb[KG];
+#pragma unroll
+            for (int u = 0; u < KG; ++u) {
+                pb[u] = pack_p(pq[u][2 * ks], pq[u][2 * ks + 1]);
+                sb[u] = pack_p(dsq[u][2 * ks], dsq[u][2 * ks + 1]);
+            }
 #pragma unroll
             for (int jd = 0; jd < 4; ++jd) {
-                s16x8 ao = colfragx(ot_, ks, jd, fo);
-                dvacc[jd] = MFMA(ao, pb, dvacc[jd], 0, 0, 0);
-                s16x8 aq = colfragx(qt_, ks, jd, fo);
-                dkacc[jd] = MFMA(aq, sb, dkacc[jd], 0, 0, 0);
+                const s16x8 ao = colfragx(ot_, ks, jd, fo);
+#pragma unroll
+                for (int u = 0; u < KG; ++u) dvacc[u][jd] = MFMA(ao, pb[u], dvacc[u][jd], 0, 0, 0);
+                const s16x8 aq = colfragx(qt_, ks, jd, fo);
+#pragma unroll
+                for (int u = 0; u < KG; ++u) dkacc[u][jd] = MFMA(aq, sb[u], dkacc[u][jd], 0, 0, 0);
             }
         }
     };
@@ -792,17 +816,18 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     using B1 = std::integral_constant<int, 1>;
     auto step = [&](int qt, auto masked_c, auto buf_c) {
         sync_stage(qt);
-        if (decltype(masked_c)::value && CAUSAL && qt * 64 + 63 + off < kvw) return;  // wave-uniform skip
-        body(qt, masked_c, buf_c);
+        // wave-uniform skip: every query of the tile precedes this wave's first key
+        if (decltype(masked_c)::value && CAUSAL && qt * 64 + 63 + off < kvw) return;
+        [[clang::always_inline]] body(qt, masked_c, buf_c);
     };
-    // tiles [qt, end) with buffer (qt - qt0) & 1 resolved at compile time
+    // tiles [qt, end) with buffer (qt - qt0) & 1 resolved at compile time (always_inline: see dQ)
     auto run = [&](int qt, int end, auto masked_c) {
-        if (qt < end && ((qt - qt0) & 1)) step(qt++, masked_c, B1{});
+        if (qt < end && ((qt - qt0) & 1)) [[clang::always_inline]] step(qt++, masked_c, B1{});
         for (; qt + 1 < end; qt += 2) {
-            step(qt, masked_c, B0{});
-            step(qt + 1, masked_c, B1{});
+            [[clang::always_inline]] step(qt, masked_c, B0{});
+            [[clang::always_inline]] step(qt + 1, masked_c, B1{});
         }
-        if (qt < end) step(qt++, masked_c, B0{});
+        if (qt < end) [[clang::always_inline]] step(qt++, masked_c, B0{});
         return qt;
     };
     int qt = qt0, qe = qt0;
@@ -815,22 +840,32 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
 #undef Ot
 #undef Lt
 #undef Dt
-    if (p.bsum) {  // dK / dV column partials for the QKV bias gradient
-        const int E = p.H * 64;
-        float* row = p.bsum + ((long)b * gridDim.y + kb) * 3 * E + h * 64;
-        block_colsum64(dkacc, p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
-        block_colsum64(dvacc, 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
-    }
-    if (kv < p.Tk) {
-        bf16* dkp = p.dk + b * p.dk_sb + (long)kv * p.dk_st + h * p.dk_sh;
-        bf16* dvp = p.dv + b * p.dv_sb + (long)kv * p.dv_st + h * p.dv_sh;
+    if (p.bsum) {  // dK / dV column partials for the QKV bias gradient; row = (b, 64-key block)
+        const int E = p.H * 64, nb64 = (p.Tk + 63) / 64;
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) {
-            bf16x4 k4 = {(bf16)(dkacc[jd][0] * p.scale), (bf16)(dkacc[jd][1] * p.scale),
-                         (bf16)(dkacc[jd][2] * p.scale), (bf16)(dkacc[jd][3] * p.scale)};
-            bf16x4 v4 = {(bf16)dvacc[jd][0], (bf16)dvacc[jd][1], (bf16)dvacc[jd][2], (bf16)dvacc[jd][3]};
-            *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
-            *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
+        for (int u = 0; u < KG; ++u) {
+            const int blk = kb * KG + u;
+            if (blk < nb64) {  // block-uniform
+                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * 64;
+                block_colsum64(dkacc[u], p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
+                block_colsum64(dvacc[u], 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+        if (kvl[u] < p.Tk) {
+            bf16* dkp = p.dk + b * p.dk_sb + (long)kvl[u] * p.dk_st + h * p.dk_sh;
+            bf16* dvp = p.dv + b * p.dv_sb + (long)kvl[u] * p.dv_st + h * p.dv_sh;
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                bf16x4 k4 = {(bf16)(dkacc[u][jd][0] * p.scale), (bf16)(dkacc[u][jd][1] * p.scale),
+                             (bf16)(dkacc[u][jd][2] * p.scale), (bf16)(dkacc[u][jd][3] * p.scale)};
+                bf16x4 v4 = {(bf16)dvacc[u][jd][0], (bf16)dvacc[u][jd][1], (bf16)dvacc[u][jd][2],
+                             (bf16)dvacc[u][jd][3]};
+                *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
+                *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
+            }
         }
     }
 }
@@ -1233,7 +1268,17 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         } else {
             RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         }
-        RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
+        // REPLICANN_ATTN_DKDV: 2 (default) = two 64-key groups per wave (plain causal / non-causal;
+        // -2.4 % bwd at GPT-2-small shapes, occupancy 2 at 240 VGPRs), 1 = one
+        const char* ek = std::getenv("REPLICANN_ATTN_DKDV");
+        const int kvv = ek ? std::atoi(ek) : 2;
+        if (kvv >= 2 && !bias && p_drop == 0.f) {
+            dim3 g1b(B * H, (Tk + 127) / 128);
+            if (causal) attn_bwd_dkdv64_k<true, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
+            else attn_bwd_dkdv64_k<false, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
+        } else {
+            RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
+        }
     } else {
         if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
         dim3 grid(Tq, B * H);

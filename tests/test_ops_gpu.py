@@ -258,12 +258,13 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("fwd,dq", [("1", "1"), ("2", "1"), ("3", "1"), ("3", "2")])
-def test_attention_kernel_variants(cuda, monkeypatch, fwd, dq):
+@pytest.mark.parametrize("fwd,dq,dkdv", [("1", "1", "1"), ("2", "1", "1"), ("3", "1", "2"), ("3", "2", "1"), ("3", "2", "2")])
+def test_attention_kernel_variants(cuda, monkeypatch, fwd, dq, dkdv):
     """Both D=64 forward kernels (REPLICANN_ATTN_FWD) and the backward against the fp32 reference, incl.
     Tq != Tk (causal offset, ragged key blocks) so the masked / unmasked tile loops all run."""
     monkeypatch.setenv("REPLICANN_ATTN_FWD", fwd)
     monkeypatch.setenv("REPLICANN_ATTN_DQ", dq)  # dQ kernel: 1 or 2 query groups per wave
+    monkeypatch.setenv("REPLICANN_ATTN_DKDV", dkdv)  # dK/dV kernel: 1 or 2 key groups per wave
     torch.manual_seed(70)
     _attn_check(2, 320, 3, 64, True)
     _attn_check(1, 100, 2, 64, True, Tk=260)
@@ -298,10 +299,12 @@ def test_attention_packed_grad(cuda):
 
 
 @pytest.mark.parametrize("causal,T,dq", [(True, 256, "1"), (False, 200, "1"), (True, 320, "2"), (False, 200, "2")])
-def test_attention_packed_qkv_bias_grad(cuda, monkeypatch, causal, T, dq):
+@pytest.mark.parametrize("dkdv", ["1", "2"])
+def test_attention_packed_qkv_bias_grad(cuda, monkeypatch, causal, T, dq, dkdv):
     """Σ_rows dQKV (the c_attn bias gradient) reduced inside the attention backward kernels
     (incl. the two-query-group dQ kernel with an odd number of 64-query blocks)."""
     monkeypatch.setenv("REPLICANN_ATTN_DQ", dq)
+    monkeypatch.setenv("REPLICANN_ATTN_DKDV", dkdv)
     from replicann_amd.utils.flat import FlatParams
     torch.manual_seed(11)
     B, H, D = 3, 4, 64
