@@ -65,7 +65,7 @@ int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
 void rn_conv_wgrad_tile(int, int, int*, int*);
 int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int, int, int, long, long, long, int, int,
-                 int, int, int, int, int, int, int, int, int, long, int, int, int, hipStream_t);
+                 int, int, int, int, int, int, int, int, int, long, int, int, int, float*, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -80,7 +80,7 @@ int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*
 long rn_bn_ws_floats(int, int);
 int rn_bn_supported(int);
 void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, float*, float*, float*, int, int, float,
-               float, int, const void*, hipStream_t);
+               float, int, const void*, const float*, int, hipStream_t);
 void rn_bn_eval(const void*, const void*, const void*, const float*, const float*, void*, int, int, float, int,
                 const void*, hipStream_t);
 void rn_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
@@ -631,7 +631,11 @@ void attn_bwd_out(const Tensor& dout, const Tensor& q, const Tensor& k, const Te
 // ------------------------------------------------------------------ implicit-GEMM conv
 // x / dy NHWC bf16 contiguous, w (OC, KH, KW, C) contiguous; the gathered tensor's channel count
 // must be a multiple of 64 (callers check conv_implicit_ok first).
-Tensor conv_fwd_implicit(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int64_t S, int64_t P) {
+// stats: also return [ceil(M/256)][2·OC] fp32 per-256-row Σ | Σ² of y (the following BatchNorm's batch
+// statistics, reduced in batchnorm_fwd instead of re-reading y)
+static std::tuple<Tensor, Tensor> conv_fwd_implicit_impl(const Tensor& x, const Tensor& w,
+                                                         const optional<Tensor>& bias, int64_t S, int64_t P,
+                                                         bool stats) {
     CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w); GUARD(x);
     const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
     const int OC = w.size(0), KH = w.size(1), KW = w.size(2);
@@ -639,12 +643,22 @@ Tensor conv_fwd_implicit(const Tensor& x, const Tensor& w, const optional<Tensor
     const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
     Tensor y = at::empty({N, OH, OW, OC}, x.options());
     const int M = N * OH * OW, K = KH * KW * C;
-    if (M == 0) return y;
+    Tensor part = stats ? at::empty({(M + 255) / 256, 2L * OC}, x.options().dtype(at::kFloat))
+                        : at::empty({0}, x.options().dtype(at::kFloat));
+    if (M == 0) return {y, part};
+    float* cp = stats ? part.data_ptr<float>() : nullptr;
     if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == OC); }
     const int rc = rn_conv_gemm(1, x.data_ptr(), w.data_ptr(), y.data_ptr(), optr(bias), nullptr, M, OC, K, 0, K, OC, H,
-                                W, C, OH, OW, KH, KW, (int)S, (int)P, C, 0, 0, 1, 0, 0, cur_stream());
+                                W, C, OH, OW, KH, KW, (int)S, (int)P, C, 0, 0, 1, 0, 0, cp, cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv fwd: unsupported geometry");
-    return y;
+    return {y, part};
+}
+Tensor conv_fwd_implicit(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int64_t S, int64_t P) {
+    return std::get<0>(conv_fwd_implicit_impl(x, w, bias, S, P, false));
+}
+std::tuple<Tensor, Tensor> conv_fwd_implicit_stats(const Tensor& x, const Tensor& w, const optional<Tensor>& bias,
+                                                   int64_t S, int64_t P) {
+    return conv_fwd_implicit_impl(x, w, bias, S, P, true);
 }
 Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t P) {  // stride 1
     CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w); GUARD(dy);
@@ -655,7 +669,7 @@ Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t
     const int M = N * (int)H * (int)W, K = KH * KW * OC;
     if (M == 0) return dx;
     const int rc = rn_conv_gemm(2, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, nullptr, M, C, K, 0, 0, C, OH,
-                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0, 0, cur_stream());
+                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0, 0, nullptr, cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv dgrad: unsupported geometry");
     return dx;
 }
@@ -689,7 +703,7 @@ Tensor conv_wgrad_implicit(const Tensor& dy2, const Tensor& x, int64_t KH, int64
     const int rc = rn_conv_gemm(3, dy2.data_ptr(), x.data_ptr(), dw.data_ptr(), nullptr,
                                 ws.defined() ? ws.data_ptr<float>() : nullptr, OC, K, PIX, OC, 0, K, H, W, C, OH, OW,
                                 (int)KH, (int)KW, (int)S, (int)P, C, 0, 0, split, 0, accumulate ? 1 : 0,
-                                cur_stream());
+                                nullptr, cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv wgrad: unsupported geometry");
     return dw;
 }
@@ -755,17 +769,24 @@ static void check_bn(const Tensor& x, const optional<Tensor>& res) {
 }
 std::tuple<Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
                                                  const Tensor& rmean, const Tensor& rvar, double mom, double eps,
-                                                 bool relu, const optional<Tensor>& res) {
+                                                 bool relu, const optional<Tensor>& res,
+                                                 const optional<Tensor>& partials) {
     check_bn(x, res); GUARD(x);
     TORCH_CHECK(rmean.scalar_type() == at::kFloat && rvar.scalar_type() == at::kFloat, "BN running stats must be fp32");
     const int M = x.size(0), C = x.size(1);
+    // partials: [R][2C] fp32 Σ | Σ² row-block partials of x from its producer (conv_fwd_implicit_stats)
+    const bool hp = partials && partials->defined();
+    if (hp)
+        TORCH_CHECK(partials->scalar_type() == at::kFloat && partials->dim() == 2 && partials->size(1) == 2L * C &&
+                        partials->is_contiguous() && partials->device() == x.device(),
+                    "batchnorm_fwd: partials must be fp32 [R][2C]");
     Tensor y = at::empty_like(x);
     Tensor mean = at::empty({C}, x.options().dtype(at::kFloat));
     Tensor rstd = at::empty({C}, x.options().dtype(at::kFloat));
     Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
     rn_bn_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), y.data_ptr(),
               mean.data_ptr<float>(), rstd.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)mom, (float)eps, relu,
-              optr(res), cur_stream());
+              optr(res), hp ? partials->data_ptr<float>() : nullptr, hp ? (int)partials->size(0) : 0, cur_stream());
     return {y, mean, rstd};
 }
 Tensor batchnorm_eval(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& rmean, const Tensor& rvar,
@@ -881,6 +902,7 @@ TORCH_LIBRARY(replicann, m) {
           "Tensor(d!)? qkv_bias_grad=None) -> ()");
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("conv_fwd_implicit(Tensor x, Tensor w, Tensor? bias, int S, int P) -> Tensor");
+    m.def("conv_fwd_implicit_stats(Tensor x, Tensor w, Tensor? bias, int S, int P) -> (Tensor, Tensor)");
     m.def("conv_dgrad_implicit(Tensor dy, Tensor w, int H, int W, int P) -> Tensor");
     m.def("conv_wgrad_implicit(Tensor dy2, Tensor x, int KH, int KW, int S, int P, Tensor(a!)? out=None, "
           "bool accumulate=False) -> Tensor");
@@ -890,7 +912,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("avgpool_fwd(Tensor x) -> Tensor");
     m.def("avgpool_bwd(Tensor gy, int H, int W) -> Tensor");
     m.def("batchnorm_fwd(Tensor x, Tensor w, Tensor b, Tensor(a!) rmean, Tensor(b!) rvar, float mom, float eps, bool relu, "
-          "Tensor? res=None) -> (Tensor, Tensor, Tensor)");
+          "Tensor? res=None, Tensor? partials=None) -> (Tensor, Tensor, Tensor)");
     m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu, "
           "Tensor? res=None) -> Tensor");
     m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu, "
@@ -928,6 +950,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("attn_bwd_out", &attn_bwd_out);
     m.impl("im2col", &im2col);
     m.impl("conv_fwd_implicit", &conv_fwd_implicit);
+    m.impl("conv_fwd_implicit_stats", &conv_fwd_implicit_stats);
     m.impl("conv_dgrad_implicit", &conv_dgrad_implicit);
     m.impl("conv_wgrad_implicit", &conv_wgrad_implicit);
     m.impl("col2im", &col2im);

@@ -615,10 +615,14 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
             }
             __syncthreads();
             bf16* dst = (bf16*)p.C;
-            // column partial sums (act-backward only): with NT % CPR == 0 every thread
-            // always visits the same 8-column chunk, so it sums its rows in registers
-            constexpr bool CSUM_OK = act_bwd(ACT) && colpart_cfg_ok<BN, NTH>();
+            // column partial sums (act-backward: Σ of the output = a bias gradient; implicit-conv
+            // forward: Σ and Σ² of the output = the following BatchNorm's batch statistics): with
+            // NT % CPR == 0 every thread always visits the same 8-column chunk, so it sums its rows
+            // in registers
+            constexpr bool BNSTAT = CONV == 1;
+            constexpr bool CSUM_OK = (act_bwd(ACT) || BNSTAT) && colpart_cfg_ok<BN, NTH>();
             float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            [[maybe_unused]] float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) {
                 const int q = threadIdx.x + it * NTH;
@@ -639,6 +643,15 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                     }
                 }
                 if (!auxp) {  // no residual / accumulate / activation-backward operand
+                    if constexpr (BNSTAT && CSUM_OK) {  // statistics of the stored (bf16) values
+                        if (!changed) {
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                csum[t] += f[t];
+                                csq[t] = __builtin_fmaf(f[t], f[t], csq[t]);
+                            }
+                        }
+                    }
                     if (changed) store8(dst + goff, f);
                     else *reinterpret_cast<s16x8*>(dst + goff) = v;
                     continue;
@@ -675,10 +688,23 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
 #pragma unroll
                     for (int t = 0; t < 8; ++t) red[rg * BN + cc * 8 + t] = csum[t];
                     __syncthreads();
+                    // act-backward: colpart [tiles_m][N]; conv forward: [tiles_m][2N] = Σ | Σ²
+                    const long prow = BNSTAT ? 2L * p.N : (long)p.N;
                     for (int col = threadIdx.x; col < BN; col += NTH) {
                         float tot = 0.f;
                         for (int g2 = 0; g2 < RG; ++g2) tot += red[g2 * BN + col];
-                        if (n0 + col < p.N) p.colpart[(long)tm * p.N + n0 + col] = tot;
+                        if (n0 + col < p.N) p.colpart[(long)tm * prow + n0 + col] = tot;
+                    }
+                    if constexpr (BNSTAT) {
+                        __syncthreads();  // first pass of `red` read
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) red[rg * BN + cc * 8 + t] = csq[t];
+                        __syncthreads();
+                        for (int col = threadIdx.x; col < BN; col += NTH) {
+                            float tot = 0.f;
+                            for (int g2 = 0; g2 < RG; ++g2) tot += red[g2 * BN + col];
+                            if (n0 + col < p.N) p.colpart[(long)tm * prow + p.N + n0 + col] = tot;
+                        }
                     }
                 }
             }

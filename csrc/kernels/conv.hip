@@ -476,10 +476,19 @@ static void bn_stats(int mode, const void* a, const void* xin, const void* yv, c
 
 int rn_bn_supported(int C) { return C % 8 == 0 && C <= 2048; }
 
-// res (optional): y = relu(BN(x) + res)
+// res (optional): y = relu(BN(x) + res).  partials (optional): [prows][2C] Σx | Σx² row-block partials
+// from x's producer (the implicit-conv GEMM epilogue): only their fixed-order column reduction runs,
+// not a statistics pass over x.
 void rn_bn_fwd(const void* x, const void* w, const void* b, float* rmean, float* rvar, void* y, float* mean,
-               float* rstd, float* ws, int M, int C, float mom, float eps, int relu, const void* res, hipStream_t st) {
-    bn_stats(0, x, nullptr, nullptr, nullptr, nullptr, ws, M, C, 0, nullptr, nullptr, st);
+               float* rstd, float* ws, int M, int C, float mom, float eps, int relu, const void* res,
+               const float* partials, int prows, hipStream_t st) {
+    if (partials) {
+        float* sums = ws + 2L * C * bn_splits(M);
+        RnColOut o{{sums, sums + C, nullptr}, {nullptr, nullptr, nullptr}, C, {0, 0, 0}};
+        rn_colreduce_seg(partials, prows, 2 * C, sums + 2L * C, o, st);
+    } else {
+        bn_stats(0, x, nullptr, nullptr, nullptr, nullptr, ws, M, C, 0, nullptr, nullptr, st);
+    }
     const float* sums = ws + 2L * C * bn_splits(M);
     bn_finalize_k<<<(C + 255) / 256, 256, 0, st>>>(sums, C, M, eps, mom, mean, rstd, rmean, rvar);
     const long t8 = (long)M * C / 8;

@@ -49,7 +49,8 @@ void rn_conv_wgrad_tile(int M, int N, int* bm, int* bn) {
 // Returns 0, or -1 if the geometry is outside the implicit path (caller falls back to im2col).
 int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bias, float* ws, int M, int N, int K,
                  long lda, long ldb, long ldc, int H, int W, int Cg, int RH, int RW, int KH, int KW, int S, int P,
-                 int KC, int BC, long bld, int split, int out_f32, int accumulate, hipStream_t st) {
+                 int KC, int BC, long bld, int split, int out_f32, int accumulate, float* colpart,
+                 hipStream_t st) {
     // the gathered operand's dimension must be whole 64-channel taps: GEMM K for fwd/dgrad,
     // GEMM N for wgrad (whose K = output pixels has an arbitrary tail, zero-filled by the loaders)
     if (KC % 64 != 0 || (mode != 3 && K % 64 != 0)) return -1;
@@ -58,6 +59,9 @@ int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bi
     GemmArgs a = {};
     a.A = (const bf16*)A; a.B = (const bf16*)B; a.C = C; a.bias = (const bf16*)bias; a.ws = ws;
     a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.out_f32 = out_f32; a.accumulate = accumulate;
+    // mode 1 only: [ceil(M / 256)][2N] fp32 per-M-tile Σ | Σ² of the bf16 output (BatchNorm stats);
+    // both mode-1 tiles are 256 rows and NT % (BN / 8) == 0
+    a.colpart = mode == 1 ? colpart : nullptr;
     ConvGeom& g = a.cv;
     g.H = H; g.W = W; g.C = Cg; g.RH = RH; g.RW = RW; g.KH = KH; g.KW = KW; g.S = S; g.P = P;
     g.KC = KC; g.BC = BC; g.bld = bld;

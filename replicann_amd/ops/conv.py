@@ -23,11 +23,17 @@ tensor, so the 9×-sized im2col matrix is never written, read or saved.
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from .. import _ext
 from .linear import _direct_grad, _notify, gemm
+
+
+def _fused_bn_stats():
+    return os.environ.get("REPLICANN_BN_FUSED_STATS", "1") != "0"
 
 
 def weight_param(ctx):
@@ -54,7 +60,13 @@ class _ConvImplicitFn(torch.autograd.Function):
         ops = _ext.ops()
         x = x.contiguous()
         w = weight.contiguous()
-        y = ops.conv_fwd_implicit(x, w, bias, stride, pad)
+        if _fused_bn_stats() and any(ctx.needs_input_grad[:2]):
+            # training: the GEMM epilogue also emits per-256-row Σ | Σ² of y, which the BatchNorm
+            # that follows every ResNet conv reduces instead of re-reading y for its statistics
+            y, part = ops.conv_fwd_implicit_stats(x, w, bias, stride, pad)
+            y._rn_bn_partials = part
+        else:
+            y = ops.conv_fwd_implicit(x, w, bias, stride, pad)
         ctx.save_for_backward(x, w)
         ctx.weight = weight  # the Parameter itself (direct gradient accumulation), not saved data
         ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None

@@ -110,8 +110,12 @@ class _BatchNormFn(torch.autograd.Function):
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         r2 = residual.reshape(-1, C).contiguous() if residual is not None else None
+        # Σ | Σ² partials of x from its producer's epilogue (implicit-conv forward), if it left them
+        part = getattr(x, "_rn_bn_partials", None)
+        if part is not None and (part.dim() != 2 or part.shape[1] != 2 * C):
+            part = None
         y, mean, rstd = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
-                                                 momentum, eps, relu, r2)
+                                                 momentum, eps, relu, r2, part)
         ctx.save_for_backward(x2, y, weight, bias, mean, rstd)
         ctx.params = (weight, bias)  # the Parameters themselves (direct gradient accumulation)
         ctx.relu = relu

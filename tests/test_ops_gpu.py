@@ -617,3 +617,32 @@ def test_conv_bn_direct_grad_accumulation(cuda):
         assert rel_err(q.grad, p.grad) < 2e-2, name
         n_direct += id(q) in seen
     assert n_direct >= 5  # conv1/conv2/shortcut weights + BN params took the direct path
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("N,HW,C,OC", [(3, 15, 64, 128), (2, 9, 128, 64)])
+def test_conv_bn_fused_statistics(cuda, monkeypatch, fused, N, HW, C, OC):
+    """Implicit-conv forward emitting the BatchNorm batch statistics from its GEMM epilogue
+    (REPLICANN_BN_FUSED_STATS=1, M % 256 != 0 here) vs the BN's own statistics pass, both
+    against fp32 conv + batch_norm (outputs, running statistics, input / weight gradients)."""
+    monkeypatch.setenv("REPLICANN_BN_FUSED_STATS", fused)
+    torch.manual_seed(29)
+    x = bf(N, HW, HW, C).requires_grad_()
+    w = bf(OC, 3, 3, C, scale=0.05).requires_grad_()
+    g = (torch.rand(OC, device="cuda") + 0.5).bfloat16().requires_grad_()
+    b = bf(OC, scale=0.1).requires_grad_()
+    rm, rv = torch.zeros(OC, device="cuda"), torch.ones(OC, device="cuda")
+    yc = ops.conv2d_nhwc(x, w, None, 1, 1)
+    assert (getattr(yc, "_rn_bn_partials", None) is not None) == (fused == "1")
+    y = ops.batch_norm_nhwc(yc, g, b, rm, rv, True, 0.1, 1e-5, relu=True)
+    go = bf(*y.shape)
+    y.backward(go)
+    xf, wf, gf, bf_ = [t.detach().float().requires_grad_() for t in (x, w, g, b)]
+    rmf, rvf = torch.zeros(OC, device="cuda"), torch.ones(OC, device="cuda")
+    ycf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), None, 1, 1)
+    yf = F.relu(F.batch_norm(ycf, rmf, rvf, gf, bf_, True, 0.1, 1e-5)).permute(0, 2, 3, 1)
+    yf.backward(go.float())
+    assert rel_err(y, yf) < 2e-2
+    assert rel_err(rm, rmf) < 2e-2 and rel_err(rv, rvf) < 2e-2
+    for t, tf in ((x, xf), (w, wf), (g, gf), (b, bf_)):
+        assert rel_err(t.grad, tf.grad) < 3e-2
