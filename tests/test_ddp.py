@@ -70,8 +70,9 @@ def _worker(rank, world, port, bucket_mb, q):
             ddp.finish()
             opt.step()
         params = flat.data.clone()
-        q.put((rank, grad_avg, grad_acc, params, len(ddp.buckets),
-               net.a.weight.detach().clone() if rank == 0 else None))
+        # numpy copies are pickled by value: torch tensors would travel as shared-memory
+        # fds that vanish when this worker exits before the parent unpickles them
+        q.put((rank, grad_avg.numpy(), grad_acc.numpy(), params.numpy(), len(ddp.buckets), None))
     finally:
         dist.destroy_process_group()
 
@@ -99,6 +100,8 @@ def test_ddp_gloo(world, bucket_mb):
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    res = [(r, torch.from_numpy(ga), torch.from_numpy(gc), torch.from_numpy(pp), nb, w)
+           for r, ga, gc, pp, nb, w in res]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

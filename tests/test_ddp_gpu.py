@@ -58,7 +58,9 @@ def _worker(rank, world, port, q):
         hooked = ddp.launched_in_backward
         ddp.finish()
         torch.cuda.synchronize()
-        q.put((rank, (flat.grad.float() / world).cpu(), hooked, len(ddp.buckets)))
+        # numpy is pickled by value (a CPU tensor would travel as a shared-memory fd
+        # that can vanish when this worker exits before the parent unpickles it)
+        q.put((rank, (flat.grad.float() / world).cpu().numpy(), hooked, len(ddp.buckets)))
     finally:
         dist.destroy_process_group()
 
@@ -75,6 +77,7 @@ def test_ddp_native_path_two_ranks_one_gpu():
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    res = [(r, torch.from_numpy(g), h, nb) for r, g, h, nb in res]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
