@@ -91,8 +91,34 @@ def _compile(src: Path, hdr: str, torch_inc) -> Path:
     return obj
 
 
+IO_OUT = Path(__file__).resolve().parent / "_io.so"
+
+
+def build_runtime(verbose: bool = True) -> Path:
+    """Host-only C++ runtime pieces (``csrc/runtime/*.cpp``: the token-shard
+    loader) → ``replicann_amd/_io.so``, loaded with ctypes (no torch or HIP
+    dependency, so it also works on CPU-only hosts)."""
+    srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall"]
+    key = hashlib.sha1(("".join(s.read_text() for s in srcs) + " ".join(flags)).encode()).hexdigest()[:16]
+    stamp = IO_OUT.with_suffix(".stamp")
+    if IO_OUT.exists() and stamp.exists() and stamp.read_text() == key:
+        return IO_OUT
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "/opt/rocm/llvm/bin/clang++"
+    r = subprocess.run([cxx, *flags, *map(str, srcs), "-o", str(IO_OUT) + ".tmp"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"runtime build failed:\n{r.stderr[-6000:]}")
+    os.replace(str(IO_OUT) + ".tmp", IO_OUT)
+    stamp.write_text(key)
+    if verbose:
+        print(f"[replicann build] linked {IO_OUT}")
+    return IO_OUT
+
+
 def build(verbose: bool = True, jobs: int | None = None) -> Path:
-    """Compile every kernel + binding and link ``_C.so``. Returns its path."""
+    """Compile every kernel + binding and link ``_C.so`` (plus the host runtime
+    ``_io.so``). Returns the ``_C.so`` path."""
+    build_runtime(verbose)
     BUILD.mkdir(parents=True, exist_ok=True)
     torch_inc, torch_lib = _torch_paths()
     hdr = _headers_digest()

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import glob
 import json
 import time
 from dataclasses import asdict, dataclass, field
@@ -26,6 +27,7 @@ from .optim import FusedAdamW, FusedSGD, cosine_lr
 from .parallel import DistributedDataParallel, init_distributed
 from .utils.checkpoint import load_checkpoint, save_checkpoint
 from .utils.data import SyntheticImages, SyntheticLM, SyntheticMNIST
+from .utils.token_data import TokenFileLM
 from .utils.flat import FlatParams
 from .utils.metrics import MetricsLogger, is_rank0, phase
 
@@ -83,6 +85,9 @@ class TrainConfig:
     resume: str | None = None
     seed: int = 0
     device: str | None = None
+    data: str | None = None       # LM token shards (comma-separated paths / globs); None = synthetic
+    data_dtype: str = "uint16"    # uint16 | uint32 shard element type
+    data_mode: str = "train"      # train (random windows) | eval (non-overlapping windows)
     model_kwargs: dict = field(default_factory=dict)
 
 
@@ -125,6 +130,11 @@ class Trainer:
         seed = c.seed * 1000 + self.rank
         if self.kind == "lm":
             vocab = self.model.config.vocab_size
+            if c.data:
+                paths = sorted(p for pat in c.data.split(",") for p in (glob.glob(pat) or [pat]))
+                return TokenFileLM(paths, c.batch_size, c.seq_len, self.device, seed=c.seed, rank=self.rank,
+                                   world=self.world, mode=c.data_mode, dtype=c.data_dtype,
+                                   start_batch=self.step_idx * c.grad_accum, vocab=vocab)
             return SyntheticLM(c.batch_size, c.seq_len, vocab, self.device, seed=seed)
         if self.kind == "image":
             m = self.model
@@ -291,7 +301,7 @@ def evaluate(model, data, steps=10):
 
 def eval_main(argv=None):
     """``python -m replicann.eval``: mean loss (+ accuracy) of a model — random init, or a
-    checkpoint written by ``train(checkpoint=...)`` — over synthetic batches."""
+    checkpoint written by ``train(checkpoint=...)`` — over synthetic batches, or over ``--data`` token shards in eval order."""
     ap = argparse.ArgumentParser(description="replicann evaluation entrypoint")
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--batch-size", type=int, default=8)
@@ -300,9 +310,12 @@ def eval_main(argv=None):
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--device", default=None)
     ap.add_argument("--model-kwargs", type=json.loads, default={})
+    ap.add_argument("--data", default=None, help="LM token shards (comma-separated paths / globs)")
+    ap.add_argument("--data-dtype", default="uint16")
     a = ap.parse_args(argv)
     cfg = TrainConfig(model=a.model, batch_size=a.batch_size, seq_len=a.seq_len, steps=1, device=a.device,
-                      resume=a.checkpoint, model_kwargs=a.model_kwargs, graph="off")
+                      resume=a.checkpoint, model_kwargs=a.model_kwargs, graph="off", data=a.data,
+                      data_dtype=a.data_dtype, data_mode="eval")
     tr = Trainer(cfg)
     out = evaluate(tr.model, tr.data, steps=a.steps)
     if is_rank0():
