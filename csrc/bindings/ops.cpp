@@ -55,6 +55,7 @@ long rn_gemm_ws_floats(int, int, int);
 int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, float*, const float*, int, int, int,
             long, long, long, int, int, int, int, int, int, int, hipStream_t, float*);
 int rn_gemm_cfg_bm(int);
+long rn_gemm_colpart_rows(int, int);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
                 int, int, float, int, float, uint64_t, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
@@ -142,10 +143,19 @@ std::string gemm_tuning_table() {
 }
 
 // "cfg 7": the vendor library (hipBLASLt through at::mm) for PLAIN GEMMs only — no
-// epilogue (bias / activation / residual / accumulate / alpha), bf16 out.  It is one
-// more candidate the autotuner times per shape, never a fallback: fused GEMMs always
-// run on the MFMA kernels above.
+// epilogue (bias / activation / residual / accumulate / alpha), bf16 out.  Reachable only
+// by an explicit cfg=7 or, for A/B measurements, REPLICANN_GEMM_LIB=1 (then one more
+// autotuner candidate); never a fallback.  Every default-path GEMM runs on the MFMA kernels.
 constexpr int kLibCfg = 7;
+// The library is NOT among the autotuner's candidates unless REPLICANN_GEMM_LIB=1 (A/B runs only).
+static bool lib_candidate() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("REPLICANN_GEMM_LIB");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
 static void lib_gemm(const Tensor& A, const Tensor& B, bool ta, bool tb, Tensor& c) {
     at::mm_out(c, ta ? A.t() : A, tb ? B.t() : B);
 }
@@ -190,7 +200,8 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         CHECK_BF16(*bias_grad);
         TORCH_CHECK(bias_grad->numel() == N && bias_grad->is_contiguous());
     }
-    Tensor colpart = want_bg ? at::empty({(M + 127) / 128, N}, a.options().dtype(at::kFloat)) : Tensor();
+    // rows: enough for every config (128-row tiles: ceil(M/128); cfg 9: 2 per 256-row tile)
+    Tensor colpart = want_bg ? at::empty({2 * ((M + 255) / 256), N}, a.options().dtype(at::kFloat)) : Tensor();
     float* cp = want_bg ? colpart.data_ptr<float>() : nullptr;
     if (act_bwd)
         TORCH_CHECK(!ta && !tb && N % 8 == 0 && preact && preact->defined() && !accumulate && !(bias && bias->defined()),
@@ -234,8 +245,8 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             Tensor scratch = at::empty({M, N}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
             const bool plain = !(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
                                !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
-            const int ncfg = plain ? 6 : 5;
-            const int cfgs[6] = {0, 1, 6, 2, 8, kLibCfg};
+            const int ncfg = (plain && lib_candidate()) ? 7 : 6;
+            const int cfgs[7] = {9, 1, 6, 0, 2, 8, kLibCfg};
             // non-powers of two too: the split that makes tiles × split just fill the 256 CUs
             // (e.g. 48 tiles × 5 = 240) beats the next power of two by up to 25 %
             // up to 128 slabs for tiny outputs over a huge K (e.g. a conv-stem weight gradient: 64×147
@@ -319,9 +330,8 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
     }
     TORCH_CHECK(rc == 0, "rn_gemm rejected shape M=", M, " N=", N, " K=", Kp);
     if (want_bg) {
-        const int bm = rn_gemm_cfg_bm((int)cfg);
         Tensor tmp = at::empty({rn_colsum_ws((int)N)}, a.options().dtype(at::kFloat));
-        rn_colsum_f32(colpart.data_ptr<float>(), (int)((M + bm - 1) / bm), (int)N, tmp.data_ptr<float>(),
+        rn_colsum_f32(colpart.data_ptr<float>(), (int)rn_gemm_colpart_rows((int)cfg, (int)M), (int)N, tmp.data_ptr<float>(),
                       bias_grad->data_ptr(), 1, cur_stream());
     }
     return c;

@@ -192,6 +192,13 @@ RN_DEV u32x4 rsrc_sgpr(const void* base) {
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+// LDS byte address (32-bit) of a dynamic-shared pointer, without the generic-pointer null check
+RN_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void*)p; }
+RN_DEV void dma16_at(const u32x4& rs, uint32_t voff, uint32_t lds_byte) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane(lds_byte);
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(l)
+                 : "memory", "m0");
+}
 RN_DEV void dma16(const u32x4& rs, uint32_t voff, const char* lds) {
     const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds);
     asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(l)

@@ -1,0 +1,616 @@
+// Persistent 256×256 bf16 GEMM with a half-tile LDS-DMA stream and staggered wave groups
+// (tile config 9; the default for every plain/fused GEMM whose shape it accepts).
+//
+// Why a second main loop (gemm_impl.h keeps the one-tile-per-block kernels for conv and fp8):
+//   * the one-tile-per-block kernel pays a prologue (first DMA round trip from HBM) and an
+//     epilogue (output stores) per 256² tile with the matrix cores idle: at K = 768 that was
+//     ≈35 % of the GEMM (profiles/gemm_k_sweep_r1d.txt);
+//   * its 2-stage ring (128 KiB of the 160 KiB LDS) leaves one K-tile of slack for a DMA and
+//     drains it with a vmcnt(0) barrier per K-tile.
+//
+// Structure (MI355X guide §5 "256² 8-phase template", T1–T5, rebuilt for this framework's
+// three operand layouts and fused epilogues):
+//   * one workgroup per CU (512 threads = 8 waves, 128 KiB LDS), the grid walks the output
+//     tiles (× split-K slices) persistently; block ids are remapped per XCD so the blocks of
+//     one XCD work on contiguous tiles (shared A/B panels in that XCD's L2);
+//   * operands stream through LDS as HALF-TILES of 16 KiB — A rows 0-127 ("At"), B columns
+//     0-127 ("Bl"), B columns 128-255 ("Br"), A rows 128-255 ("Ab") of one 64-deep K-tile,
+//     issued in that order, one half-tile per phase, 6 half-tiles ahead of the phase that
+//     reads them, into an 8-slot ring.  The stream runs straight through tile boundaries, so
+//     the next tile's operands are already in flight during an epilogue;
+//   * a K-tile is 4 phases, one per 128×128 quadrant of the block tile (each wave owns a 64×32
+//     piece of every quadrant: its 128×64 output is spread over both A halves and both B
+//     halves): q0 = (At, Bl), q1 = (At, Br), q2 = (Ab, Br), q3 = (Ab, Bl).  Each phase:
+//       vmcnt wait (counted: 3 half-tiles stay in flight) → issue one half-tile (2 LDS-DMA per
+//       wave) → ds_read this phase's fragments → s_barrier → lgkmcnt(0) → 16 MFMAs → s_barrier;
+//   * waves 4-7 run one barrier behind waves 0-3 (one extra s_barrier up front): on every SIMD
+//     one wave's fragment reads and DMA issue overlap its partner's MFMAs (guide T3/T4 stagger);
+//   * the DMA of a slot is issued ≥ 2 phases after its last read and read ≥ 1 phase after the
+//     wait that retires it (the guide's RAW/WAR placement rules for a staggered pair);
+//   * B fragments are loaded with a column permutation so that after the MFMAs each lane holds
+//     8 CONTIGUOUS output columns of one row: the epilogue stores 16 B per lane straight from
+//     the accumulators (no LDS staging, which would need the ring), through buffer stores whose
+//     range check drops out-of-bounds lanes — every wave issues the same number of stores, so
+//     the counted vmcnt waits after an epilogue stay exact;
+//   * bias comes through the scalar cache (s_load, lgkmcnt) so a bias epilogue does not drain
+//     the in-flight operand DMA; epilogues that read a full tile (residual, saved
+//     pre-activation, accumulate target) do wait for it.
+//
+// LDS images (all written lane-linearly by the DMA, the XOR swizzle applied to the per-lane
+// SOURCE address and again on the read, guide rule 21):
+//   K-contiguous operand, A side: [128 rows][64 k] 128-B rows, chunk c of row r at c ^ swz_kc(r);
+//   K-contiguous operand, B side: same image, swizzle swz_kcp (rows are read in the permuted
+//     order; the swizzle keeps every ds_read_b128 lane group on 16 distinct 16-B slots);
+//   MN-contiguous operand: two [64 k][64 mn] sub-images, read with ds_read_b64_tr_b16; the B
+//     side uses swz_mnp, which is conflict-free for the permuted column blocks.
+#pragma once
+#include <type_traits>
+
+#include "gemm_impl.h"
+
+namespace rn_gemm_detail {
+
+constexpr int PK_HALF = 16384;  // bytes per half-tile slot
+constexpr int PK_LDS = 8 * PK_HALF;
+
+RN_DEV int swz_kcp(int r) { return (((r >> 3) & 3) << 1) | ((r >> 1) & 1); }
+RN_DEV int swz_mnp(int k) { return ((k >> 1) & 1) | (((k >> 3) & 1) << 2); }
+
+// One 16 KiB half-tile (128 mn × 64 k) into `lds`, 2 LDS-DMA instructions per wave.
+// PERM: the B-side swizzles.  `live` false: out-of-range source for every lane (the DMA
+// writes zeros and reads nothing) — keeps the per-wave instruction count uniform.
+template <bool KC, bool PERM>
+RN_DEV void pk_stage(const u32x4& rs, long ld, int mn_lim, int k_lim, char* lds, int wave, int lane, bool live) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ins = wave * 2 + i;
+        uint32_t voff;
+        if constexpr (KC) {
+            const int r = ins * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ (PERM ? swz_kcp(r) : swz_kc(r));
+            const int k = cg * 8;
+            const bool ok = live && (r < mn_lim) && (k < k_lim);
+            voff = ok ? (uint32_t)(((long)r * ld + k) * 2) : 0xFFFFFFF0u;
+        } else {
+            const int sub = ins >> 3, within = ins & 7;
+            const int r = within * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ (PERM ? swz_mnp(r) : swz_mn(r));
+            const int mn = sub * 64 + cg * 8;
+            const bool ok = live && (r < k_lim) && (mn < mn_lim);
+            voff = ok ? (uint32_t)(((long)r * ld + mn) * 2) : 0xFFFFFFF0u;
+        }
+        dma16(rs, voff, lds + ins * 1024);
+    }
+}
+
+// A fragment (k-step s) of rows mnbase + (lane & 15) of a half-tile image.
+template <bool KC>
+RN_DEV s16x8 pk_frag_a(const char* lds, int mnbase, int s, int lane) {
+    return frag<KC>(lds, mnbase, s, lane);
+}
+
+// B fragment j (0/1) of the wave's 32 columns starting at colbase (multiple of 32) of a
+// half-tile image, permuted: MFMA operand row i = lane & 15 holds column
+//   colbase + 8·(i>>2) + 4·(j ^ a(i>>2)) + (i&3),   a(g) = 0 (KC image) or g & 1 (MN image),
+// so output group G = lane>>4 ends up with columns colbase + 8G .. 8G+7 over j = 0, 1.
+template <bool KC>
+RN_DEV s16x8 pk_frag_b(const char* lds, int colbase, int j, int s, int lane) {
+    if constexpr (KC) {
+        const int i = lane & 15;
+        const int row = colbase + 8 * (i >> 2) + 4 * j + (i & 3);
+        const int chunk = s * 4 + (lane >> 4);
+        return *reinterpret_cast<const s16x8*>(lds + row * 128 + ((chunk ^ swz_kcp(row)) << 4));
+    } else {
+        const char* sub = lds + (colbase >> 6) * 8192;
+        const int cl = colbase & 63;
+        const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+        const int c = (cl >> 3) + p;
+        const int half = j ^ (p & 1);
+        const int k0 = s * 32 + 8 * g + q;
+        const int k1 = k0 + 4;
+        const char* a0 = sub + k0 * 128 + ((c ^ swz_mnp(k0)) << 4) + half * 8;
+        const char* a1 = sub + k1 * 128 + ((c ^ swz_mnp(k1)) << 4) + half * 8;
+        s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+        s16x8 r;
+        r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+        r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+        return r;
+    }
+}
+
+RN_DEV __amdgpu_buffer_rsrc_t pk_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t bp = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+
+RN_DEV u32x4 pk_rsrc_u(const void* base, uint32_t bytes) {
+    const uint64_t bp = (uint64_t)base;
+    u32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    r[2] = bytes;
+    r[3] = 0x00020000u;
+    return r;
+}
+
+// 16-B buffer store the compiler does not see: it then inserts no vmcnt waits of its own for
+// the epilogue stores (its counts would ignore the in-flight operand DMA, and a WAR wait on the
+// store data registers would drain it); s_nop 1 covers the store-data read hazard (guide §5.7).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+RN_DEV void pk_st16(const u32x4 v, const u32x4& rs, uint32_t voff) {
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+#pragma clang diagnostic pop
+
+RN_DEV uint32_t pk_pack2(float a, float b) {
+    bf16x2 v = {(bf16)a, (bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+// bf16 pairs -> f32 by shifts (exact).  NOTE: __builtin_bit_cast(bf16x2, u[d]) on an element of
+// a vector reference miscompiles on ROCm 7.2 (every d reads element 0).
+RN_DEV void pk_unpack8(const u32x4 u, float* f) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        f[2 * d] = __builtin_bit_cast(float, w[d] << 16);
+        f[2 * d + 1] = __builtin_bit_cast(float, w[d] & 0xFFFF0000u);
+    }
+}
+
+// Stores each wave issues per epilogue (all issued, out-of-range lanes dropped by the
+// buffer range check), for the counted vmcnt waits of the 4 phases after it.
+template <int ACT, bool SPLIT, bool F32>
+constexpr int pk_epi_stores() {
+    return 16 * ((SPLIT || F32) ? 2 : 1) + (act_fwd(ACT) ? 16 : 0) + (act_bwd(ACT) ? 4 : 0);
+}
+
+// DBG (timing-only ablation builds, never instantiated by the launchers): bit 0 skips the
+// main-loop operand DMA, bit 1 the counted vmcnt waits.
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0>
+__global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
+    constexpr int BM = 256, BN = 256;
+    constexpr int S_EPI = pk_epi_stores<ACT, SPLIT, F32>();
+    static_assert(6 + S_EPI <= 63, "vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 2, wc = wave & 3;  // wr: stagger group and A row block; wc: B column block
+    const int G = lane >> 4;                  // output column group of this lane
+    const int tiles = p.tiles_m * p.tiles_n;
+    const int items = tiles * p.split;
+    const int grid = gridDim.x;
+    const int bid = xcd_remap(blockIdx.x, grid);
+    const int my_items = (items - bid + grid - 1) / grid;
+    const int nk = p.k_per_split / BK;
+    const int nphase = my_items * nk * 4;
+
+    float alpha = 1.f;
+    if (p.alpha) alpha = *p.alpha;
+    asm volatile("" ::"v"(alpha));  // its load retires here, before any DMA is in flight
+
+    // ---- DMA issue stream: half-tile σ = 4·t + h of K-tile t (stream order over the block's
+    // items) goes to slot σ % 8.  Phase q of compute K-tile u issues h = (q + 2) % 4 of K-tile
+    // u + 1 (q0, q1) or u + 2 (q2, q3): the half index is a compile-time constant per phase and
+    // the source comes from a cursor that advances once per K-tile. ----
+    auto item_coords = [&](int li, int& m0, int& n0, int& kb, int& ke, int& tm) {
+        const int item = bid + li * grid;
+        const int sid = item / tiles;
+        int tn;
+        group_tile(item - sid * tiles, p.tiles_m, p.tiles_n, tm, tn);
+        m0 = tm * BM;
+        n0 = tn * BN;
+        kb = sid * p.k_per_split;
+        ke = min(p.K, kb + p.k_per_split);
+    };
+    // per-lane (mn, k) coordinates of this wave's two DMA instructions of a half-tile, and their
+    // in-tile byte offsets (kept: 4 VGPRs; the coordinates are recomputed on ragged tiles only)
+    auto lane_mnk = [&](bool isA, int i, int& mn, int& k) {
+        const int ins = wave * 2 + i;
+        const bool kc = isA ? AK : BKC;
+        if (kc) {
+            mn = ins * 8 + (lane >> 3);
+            k = ((lane & 7) ^ (isA ? swz_kc(mn) : swz_kcp(mn))) * 8;
+        } else {
+            k = (ins & 7) * 8 + (lane >> 3);
+            mn = (ins >> 3) * 64 + ((lane & 7) ^ (isA ? swz_mn(k) : swz_mnp(k))) * 8;
+        }
+    };
+    uint32_t a_off[2], b_off[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int mn, k;
+        lane_mnk(true, i, mn, k);
+        a_off[i] = (uint32_t)((AK ? (long)mn * p.lda + k : (long)k * p.lda + mn) * 2);
+        lane_mnk(false, i, mn, k);
+        b_off[i] = (uint32_t)((BKC ? (long)mn * p.ldb + k : (long)k * p.ldb + mn) * 2);
+    }
+    const long a_step = AK ? (long)BK : (long)BK * p.lda, b_step = BKC ? (long)BK : (long)BK * p.ldb;
+    const long a_half = AK ? 128L * p.lda : 128L, b_half = BKC ? 128L * p.ldb : 128L;
+    // cursor: the K-tile being issued (limits 0 once the block's items are exhausted: every
+    // lane then reads out of range and the DMA only zero-fills its slot)
+    const bf16* ca = p.A;
+    const bf16* cb = p.B;
+    int cml = 0, cnl = 0, ckl = 0, ckt = 0, cli = 0, ct = 0;
+    bool in_loop = false;
+    auto cur_set = [&]() {
+        int m0, n0, kb, ke, tm;
+        item_coords(cli, m0, n0, kb, ke, tm);
+        ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + m0;
+        cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + n0;
+        cml = p.M - m0;
+        cnl = p.N - n0;
+        ckl = ke - kb;
+    };
+    auto cur_adv = [&]() {
+        ++ct;
+        if (++ckt < nk) {
+            ca += a_step;
+            cb += b_step;
+            ckl -= BK;
+            return;
+        }
+        ckt = 0;
+        if (++cli < my_items) cur_set();
+        else cml = cnl = ckl = 0;
+    };
+    const uint32_t lds0 = lds_addr(smem) + wave * 2048;  // this wave's 2 KiB of every slot
+    auto issue_h = [&](auto hc) {
+        constexpr int H = decltype(hc)::value;
+        if constexpr (DBG & 1) {
+            if (in_loop) return;
+        }
+        const uint32_t dst = lds0 + (uint32_t)(((ct & 1) * 4 + H) * PK_HALF);
+        const bool isA = (H == 0 || H == 3);
+        const bf16* base = isA ? (H == 3 ? ca + a_half : ca) : (H == 2 ? cb + b_half : cb);
+        const int mnl = isA ? (H == 3 ? cml - 128 : cml) : (H == 2 ? cnl - 128 : cnl);
+        const u32x4 rs = rsrc_sgpr(base);
+        if (mnl >= 128 && ckl >= BK) {  // interior half-tile: no per-lane checks
+#pragma unroll
+            for (int i = 0; i < 2; ++i) dma16_at(rs, isA ? a_off[i] : b_off[i], dst + i * 1024);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                int mn, kk;
+                lane_mnk(isA, i, mn, kk);
+                const uint32_t o = isA ? a_off[i] : b_off[i];
+                dma16_at(rs, (mn < mnl && kk < ckl) ? o : 0xFFFFFFF0u, dst + i * 1024);
+            }
+        }
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    using H2 = std::integral_constant<int, 2>;
+    using H3 = std::integral_constant<int, 3>;
+
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    s16x8 Af[4][2], Bl[2][2], Br[2][2];
+
+    // ---- epilogue of one output tile, straight from the accumulators ----
+    auto epilogue = [&](int m0, int n0, int tm, int sid) {
+        const int mlim = p.M - m0, nlim = p.N - n0;
+        // per-tile byte-range descriptors (tile-relative offsets stay far below 2^31)
+        const long ldc = SPLIT ? (long)p.N : p.ldc;
+        constexpr int ES = (SPLIT || F32) ? 4 : 2;
+        char* cbase = SPLIT ? (char*)(p.ws + ((long)sid * p.M + m0) * p.N + n0) : (char*)p.C + ((long)m0 * ldc + n0) * ES;
+        const __amdgpu_buffer_rsrc_t crs = pk_rsrc(cbase, 0x7FFFFFF0u);
+        const u32x4 crs_u = pk_rsrc_u(cbase, 0x7FFFFFF0u);
+        auto off = [&](int mh, int i, int nh, int es) -> uint32_t {
+            const int r = mh * 128 + wr * 64 + i * 16 + (lane & 15);
+            const int c = nh * 128 + wc * 32 + 8 * G;
+            return (r < mlim && c < nlim) ? (uint32_t)(((long)r * ldc + c) * es) : 0xFFFFFFF0u;
+        };
+        // bias: the wave's 2 × 32 columns through the scalar cache, then each lane picks its 8
+        float bias[2][8];
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) bias[nh][t] = 0.f;
+        if (!SPLIT && p.bias) {
+#pragma unroll
+            for (int nh = 0; nh < 2; ++nh) {
+                const int cb = n0 + nh * 128 + wc * 32;
+                if (cb + 32 <= p.N) {
+                    const __attribute__((address_space(4))) u32x4* bp =
+                        (const __attribute__((address_space(4))) u32x4*)(p.bias + cb);
+                    u32x4 b0 = bp[0], b1 = bp[1], b2 = bp[2], b3 = bp[3];
+                    // opaque SGPR values: otherwise the select below becomes a per-lane select of
+                    // ADDRESSES and the scalar loads turn into vector loads (a vmcnt(0) drain)
+                    asm volatile("" : "+s"(b0), "+s"(b1), "+s"(b2), "+s"(b3));
+                    const u32x4 bsel = G == 0 ? b0 : (G == 1 ? b1 : (G == 2 ? b2 : b3));
+                    pk_unpack8(bsel, bias[nh]);
+                } else if (cb + 8 * G < p.N) {  // ragged last column block (N % 32 != 0)
+                    const u32x4 u = *reinterpret_cast<const u32x4*>(p.bias + cb + 8 * G);
+                    pk_unpack8(u, bias[nh]);
+                }
+            }
+        }
+        // full-tile operand read by the epilogue: saved pre-activation (act backward), residual,
+        // or the accumulate target (bf16 out)
+        const bf16* auxp = SPLIT ? nullptr
+                                 : (act_bwd(ACT) ? p.pre : (p.res ? p.res : ((p.accumulate && !F32) ? (const bf16*)p.C : nullptr)));
+        // (loaded one 128-row half at a time: 32 VGPRs, all 8 loads of a half in flight together)
+        u32x4 aux[4][2];
+        const __amdgpu_buffer_rsrc_t ars = pk_rsrc(auxp ? auxp + (long)m0 * p.ldc + n0 : nullptr, 0x7FFFFFF0u);
+        const u32x4 prs = pk_rsrc_u(act_fwd(ACT) && p.pre ? (void*)(p.pre + (long)m0 * p.ldc + n0) : nullptr,
+                                    act_fwd(ACT) && p.pre ? 0x7FFFFFF0u : 0u);
+        float csum[2][8];
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) csum[nh][t] = 0.f;
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+            if (auxp) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int nh = 0; nh < 2; ++nh)
+                        aux[i][nh] = __builtin_amdgcn_raw_buffer_load_b128(ars, off(mh, i, nh, 2), 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int nh = 0; nh < 2; ++nh) {
+                    float v[8];
+                    const bool swp = !BKC && (G & 1);  // MN image: odd lane groups hold fragment 1 first
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        // compile-time register indices on both sides of the select (a runtime
+                        // index would send the accumulators to scratch)
+                        const float x0 = acc[mh][nh][i][c >> 2][c & 3], x1 = acc[mh][nh][i][(c >> 2) ^ 1][c & 3];
+                        v[c] = (swp ? x1 : x0) * alpha;
+                    }
+                    if constexpr (SPLIT) {
+                        const uint32_t o = off(mh, i, nh, 4);
+                        pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1]),
+                                    __builtin_bit_cast(uint32_t, v[2]), __builtin_bit_cast(uint32_t, v[3])},
+                            crs_u, o);
+                        pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[4]), __builtin_bit_cast(uint32_t, v[5]),
+                                    __builtin_bit_cast(uint32_t, v[6]), __builtin_bit_cast(uint32_t, v[7])},
+                            crs_u, o == 0xFFFFFFF0u ? o : o + 16);
+                        continue;
+                    }
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) v[c] += bias[nh][c];
+                    if constexpr (act_fwd(ACT)) {
+                        // pre-activation store (dropped when no pre buffer: zero-size descriptor);
+                        // the activation is applied to the bf16-rounded value the backward sees
+                        const u32x4 pu = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
+                                          pk_pack2(v[6], v[7])};
+                        pk_st16(pu, prs, off(mh, i, nh, 2));
+                        if (p.pre) pk_unpack8(pu, v);
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) v[c] = act_f<ACT>(v[c]);
+                    }
+                    if (auxp) {
+                        float ax[8];
+                        pk_unpack8(aux[i][nh], ax);
+                        if constexpr (act_bwd(ACT)) {
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) {
+                                v[c] = (float)(bf16)v[c] * act_grad_f<ACT>(ax[c]);
+                                csum[nh][c] += (float)(bf16)v[c];
+                            }
+                        } else {
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) v[c] += ax[c];
+                        }
+                    }
+                    const uint32_t o = off(mh, i, nh, ES);
+                    if constexpr (F32) {
+                        float c8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                        if (p.accumulate) {
+                            const u32x4 c0 = __builtin_amdgcn_raw_buffer_load_b128(crs, o, 0, 0);
+                            const u32x4 c1 = __builtin_amdgcn_raw_buffer_load_b128(crs, o == 0xFFFFFFF0u ? o : o + 16, 0, 0);
+                            const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+                            for (int d = 0; d < 8; ++d) c8[d] = __builtin_bit_cast(float, w[d]);
+                        }
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) v[c] += c8[c];
+                        pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1]),
+                                    __builtin_bit_cast(uint32_t, v[2]), __builtin_bit_cast(uint32_t, v[3])},
+                            crs_u, o);
+                        pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[4]), __builtin_bit_cast(uint32_t, v[5]),
+                                    __builtin_bit_cast(uint32_t, v[6]), __builtin_bit_cast(uint32_t, v[7])},
+                            crs_u, o == 0xFFFFFFF0u ? o : o + 16);
+                    } else {
+                        if (p.res && p.accumulate) {  // both: residual above, accumulate target here
+                            float c8[8];
+                            pk_unpack8(__builtin_amdgcn_raw_buffer_load_b128(crs, o, 0, 0), c8);
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) v[c] += c8[c];
+                        }
+                        const u32x4 ou = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
+                                          pk_pack2(v[6], v[7])};
+                        pk_st16(ou, crs_u, o);
+                    }
+                }
+        }
+        if constexpr (act_bwd(ACT)) {
+            // per-wave column sums of the stored dH (bias gradient of the layer it feeds):
+            // reduce over the 16 rows of the lane group, one partial row per (M-tile, wr)
+#pragma unroll
+            for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    float s = csum[nh][c];
+                    s += __shfl_xor(s, 1, 64);
+                    s += __shfl_xor(s, 2, 64);
+                    s += __shfl_xor(s, 4, 64);
+                    s += __shfl_xor(s, 8, 64);
+                    csum[nh][c] = s;
+                }
+            float* cpb = p.colpart ? p.colpart + ((long)tm * 2 + wr) * p.N + n0 : nullptr;
+            const u32x4 cprs = pk_rsrc_u(cpb, cpb ? 0x7FFFFFF0u : 0u);
+#pragma unroll
+            for (int nh = 0; nh < 2; ++nh) {
+                const int c = nh * 128 + wc * 32 + 8 * G;
+                const uint32_t o = ((lane & 15) == 0 && c < nlim) ? (uint32_t)(c * 4) : 0xFFFFFFF0u;
+                pk_st16((u32x4){__builtin_bit_cast(uint32_t, csum[nh][0]), __builtin_bit_cast(uint32_t, csum[nh][1]),
+                            __builtin_bit_cast(uint32_t, csum[nh][2]), __builtin_bit_cast(uint32_t, csum[nh][3])},
+                    cprs, o);
+                pk_st16((u32x4){__builtin_bit_cast(uint32_t, csum[nh][4]), __builtin_bit_cast(uint32_t, csum[nh][5]),
+                            __builtin_bit_cast(uint32_t, csum[nh][6]), __builtin_bit_cast(uint32_t, csum[nh][7])},
+                    cprs, o == 0xFFFFFFF0u ? o : o + 16);
+            }
+        }
+    };
+
+    // ---- prologue: σ = 0..5 in flight (K-tile 0, halves 0/1 of K-tile 1), σ 0/1 landed ----
+    if (my_items > 0) {
+        cur_set();
+        issue_h(H0{});
+        issue_h(H1{});
+        issue_h(H2{});
+        issue_h(H3{});
+        cur_adv();
+        issue_h(H0{});
+        issue_h(H1{});
+        vm_wait<8>();
+    }
+    asm volatile("s_barrier" ::: "memory");
+    if (wr == 1) asm volatile("s_barrier" ::: "memory");  // stagger: waves 4-7 one barrier behind
+    in_loop = true;
+    __builtin_amdgcn_sched_barrier(0);
+
+    int c_m0 = 0, c_n0 = 0, c_kb = 0, c_ke = 0, c_tm = 0, c_sid = 0;
+    if (my_items > 0) item_coords(0, c_m0, c_n0, c_kb, c_ke, c_tm);
+    c_sid = my_items > 0 ? (bid / tiles) : 0;
+    int c_li = 0, c_kt = 0;
+    int since_epi = 4;
+
+    // phase wait: σ ≤ φ+2 must have landed (this wave's DMA); younger = the 3 half-tiles
+    // issued in the previous 3 phases (6 ops) plus, within 4 phases of an epilogue, its stores
+    auto phase_wait = [&]() {
+        if constexpr (DBG & 2) return;
+        if (since_epi < 4) vm_wait<6 + S_EPI>();
+        else vm_wait<6>();
+        ++since_epi;
+    };
+    auto sync_mma_begin = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+    };
+    auto sync_mma_end = [&]() {
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+#define RN_PK_MMA(MH, NH, BF)                                                                          \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                 \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                 \
+    _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                                 \
+        acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j_][s_], Af[i_][s_], acc[MH][NH][i_][j_], 0, 0, 0);
+
+#pragma unroll 1
+    for (int u = 0; u < my_items * nk; ++u) {
+        const char* sl = smem + (u & 1) * (4 * PK_HALF);
+        // q0: At + Bl  (fragment reads first: their latency runs under the DMA issue)
+        phase_wait();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl, wr * 64 + i * 16, s, lane);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) Bl[j][s] = pk_frag_b<BKC>(sl + PK_HALF, wc * 32, j, s, lane);
+        }
+        issue_h(H2{});
+        sync_mma_begin();
+        RN_PK_MMA(0, 0, Bl)
+        sync_mma_end();
+        // q1: At + Br
+        phase_wait();
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) Br[j][s] = pk_frag_b<BKC>(sl + 2 * PK_HALF, wc * 32, j, s, lane);
+        issue_h(H3{});
+        sync_mma_begin();
+        RN_PK_MMA(0, 1, Br)
+        sync_mma_end();
+        // q2: Ab + Br
+        phase_wait();
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl + 3 * PK_HALF, wr * 64 + i * 16, s, lane);
+        cur_adv();
+        issue_h(H0{});
+        sync_mma_begin();
+        RN_PK_MMA(1, 1, Br)
+        sync_mma_end();
+        // q3: Ab + Bl (all fragments already in registers)
+        phase_wait();
+        issue_h(H1{});
+        sync_mma_begin();
+        RN_PK_MMA(1, 0, Bl)
+        sync_mma_end();
+        if (++c_kt == nk) {
+            epilogue(c_m0, c_n0, c_tm, c_sid);
+            since_epi = 0;
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            c_kt = 0;
+            ++c_li;
+            if (c_li < my_items) {
+                item_coords(c_li, c_m0, c_n0, c_kb, c_ke, c_tm);
+                c_sid = (bid + c_li * grid) / tiles;
+            }
+        }
+    }
+#undef RN_PK_MMA
+    if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger barrier
+    (void)nphase;
+    (void)c_kb;
+    (void)c_ke;
+}
+
+// Launch: persistent grid of min(items, 256 × blocks-per-CU) workgroups (1 per CU: 128 KiB LDS).
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32>
+void launch_pk_t(GemmArgs& a, hipStream_t st) {
+    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32>;
+    static int attr_dev = -1;  // the >64 KiB LDS opt-in, per device the process launches on
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (attr_dev != dev) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, PK_LDS);
+        attr_dev = dev;
+    }
+    const int items = a.tiles_m * a.tiles_n * a.split;
+    int cus = 256;
+    {
+        static int cu_dev = -1, cu_n = 256;
+        if (cu_dev != dev) {
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cu_n = prop.multiProcessorCount;
+            cu_dev = dev;
+        }
+        cus = cu_n;
+    }
+    const int grid = items < cus ? items : cus;
+    kern<<<grid, 512, PK_LDS, st>>>(a);
+}
+
+}  // namespace rn_gemm_detail

@@ -56,6 +56,10 @@ void rn_gemm_launch_cfg4(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg5(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg6(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg8(GemmArgs&, bool, bool, int, hipStream_t);
+void rn_gemm_launch_pk_tt(GemmArgs&, int, hipStream_t);
+void rn_gemm_launch_pk_tf(GemmArgs&, int, hipStream_t);
+void rn_gemm_launch_pk_ff(GemmArgs&, int, hipStream_t);
+void rn_gemm_launch_pk_ft(GemmArgs&, int, hipStream_t);
 
 namespace {
 
@@ -66,6 +70,10 @@ inline long ntiles(int M, int N, int bm, int bn) { return (long)((M + bm - 1) / 
 // 2 per CU, a 256² block 1 per CU and ~13 % faster per FLOP (half the L2→LDS
 // bytes per FLOP); a launch takes ceil(tiles / resident slots) rounds.
 struct Choice { int cfg, split; };
+
+inline bool pk_ok(int N, long ldc, int out_f32, int act) {
+    return N % 8 == 0 && ldc % 8 == 0 && !(out_f32 && act != ACT_NONE);
+}
 
 inline Choice pick(int M, int N, int K, int split_req) {
     const double flop_s_cu = 2.9e12;  // effective per-CU bf16 rate of the 128² config
@@ -103,13 +111,19 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 //   trans_a = 0: A stored [M][lda] (K contiguous);   1: A stored [K][lda] (M contiguous)
 //   trans_b = 0: B stored [K][ldb] (N contiguous);   1: B stored [N][ldb] (K contiguous)
 //   cfg: -1 auto, 0 = 128x128, 1 = 256x256 pipelined, 2 = 256x128 pipelined, 3 = 128x256,
-//        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined, 8 = 256x128 3-stage ring
-//        (7 is the vendor-library candidate handled in the bindings);  split: -1 auto, 0/1 none
+//        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined, 8 = 256x128 3-stage ring,
+//        9 = persistent 256x256 half-tile stream (gemm_pk.h; needs N % 8 == 0, ldc % 8 == 0)
+//        (7 is the vendor-library candidate handled in the bindings, off by default);
+//        split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
 // colpart (optional, act-backward only): [ceil(M / BM)][N] fp32 per-M-tile column sums of C
 // (BM of the config actually used: rn_gemm_cfg_bm).  Returns -3 if the requested config /
 // split cannot produce them (the caller then reduces C itself).
-int rn_gemm_cfg_bm(int cfg) { return (cfg == 0 || cfg == 3 || cfg == 5) ? 128 : 256; }
+int rn_gemm_cfg_bm(int cfg) { return (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 9) ? 128 : 256; }
+// rows of the column-partial matrix a config writes (cfg 9: one row per (256-row tile, wave row))
+long rn_gemm_colpart_rows(int cfg, int M) {
+    return cfg == 9 ? 2L * ((M + 255) / 256) : (long)((M + rn_gemm_cfg_bm(cfg) - 1) / rn_gemm_cfg_bm(cfg));
+}
 
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
@@ -125,9 +139,10 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     a.pre = (bf16*)pre; a.ws = ws; a.alpha = alpha; a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
     if (cfg < 0 || split < 0) {
         Choice ch = pick(M, N, K, split);
-        if (cfg < 0) cfg = ch.cfg;
+        if (cfg < 0) cfg = pk_ok(N, ldc, out_f32, act) ? 9 : ch.cfg;
         if (split < 0) split = ch.split;
     }
+    if (cfg == 9 && !pk_ok(N, ldc, out_f32, act)) cfg = 1;  // shapes the persistent kernel does not take
     a.split = split < 1 ? 1 : split;
     int kps = (K + a.split - 1) / a.split;
     kps = (kps + BK - 1) / BK * BK;
@@ -148,6 +163,14 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
         case 5: rn_gemm_launch_cfg5(a, ak, bk, act, st); break;
         case 6: rn_gemm_launch_cfg6(a, ak, bk, act, st); break;
         case 8: rn_gemm_launch_cfg8(a, ak, bk, act, st); break;
+        case 9:
+            a.tiles_m = (M + 255) / 256;
+            a.tiles_n = (N + 255) / 256;
+            if (ak && bk) rn_gemm_launch_pk_tt(a, act, st);
+            else if (ak) rn_gemm_launch_pk_tf(a, act, st);
+            else if (bk) rn_gemm_launch_pk_ft(a, act, st);
+            else rn_gemm_launch_pk_ff(a, act, st);
+            break;
         default: rn_gemm_launch_cfg0(a, ak, bk, act, st); break;
     }
     return 0;

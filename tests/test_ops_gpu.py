@@ -26,7 +26,7 @@ def test_native_loaded(cuda):
 
 
 # ----------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 8, 9])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 96), (1000, 384, 520), (64, 24, 8), (520, 776, 1088)])
 def test_gemm_layouts(cuda, ta, tb, M, N, K, cfg):
@@ -37,6 +37,43 @@ def test_gemm_layouts(cuda, ta, tb, M, N, K, cfg):
     out = ops.gemm(a, b, ta=ta, tb=tb, cfg=cfg)
     assert out.shape == (M, N)
     assert rel_err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(8192, 2304, 768), (4352, 4200, 200), (8200, 1032, 72), (2048, 512, 64)])
+def test_gemm_persistent_multi_tile(cuda, ta, tb, M, N, K):
+    """cfg 9 walks several output tiles per workgroup with the operand stream running across tile
+    boundaries (epilogue while the next tile's half-tiles are in flight); ragged M/N/K tails."""
+    torch.manual_seed(11)
+    a = bf(K, M) if ta else bf(M, K)
+    b = bf(N, K) if tb else bf(K, N)
+    bias, res = bf(N), bf(M, N)
+    af = a.float().t() if ta else a.float()
+    bf_ = b.float().t() if tb else b.float()
+    ref = af @ bf_
+    out = ops.gemm(a, b, ta=ta, tb=tb, cfg=9)
+    assert rel_err(out, ref) < 1e-2
+    out = ops.gemm(a, b, ta=ta, tb=tb, cfg=9, bias=bias, residual=res)
+    assert rel_err(out, ref + bias.float() + res.float()) < 1e-2
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    out = ops.gemm(a, b, ta=ta, tb=tb, cfg=9, bias=bias, act=2, preact=pre)
+    h = ref + bias.float()
+    assert rel_err(pre, h) < 1e-2 and rel_err(out, F.gelu(h, approximate="tanh")) < 1e-2
+    o32 = ops.gemm(a, b, ta=ta, tb=tb, cfg=9, out_dtype=torch.float32)
+    assert o32.dtype == torch.float32 and rel_err(o32, ref) < 5e-3
+
+
+def test_gemm_persistent_act_backward_multi_tile(cuda):
+    torch.manual_seed(12)
+    M, N, K = 4600, 3072, 768
+    dy, w, pre = bf(M, K), bf(K, N, scale=0.05), bf(M, N)
+    bg = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+    out = torch.ops.replicann.gemm(dy, w, False, False, None, None, 4, pre, None, False, 0, False, None, 9, bg)
+    du = (dy.float() @ w.float()).bfloat16().float()
+    pf = pre.float().requires_grad_()
+    (g,) = torch.autograd.grad(F.gelu(pf, approximate="tanh"), pf, du)
+    assert rel_err(out, g) < 1e-2
+    assert rel_err(bg.float(), out.float().sum(0)) < 2e-2
 
 
 def test_gemm_alpha(cuda):
@@ -55,14 +92,15 @@ def test_gemm_identity_asymmetric(cuda):
     torch.testing.assert_close(out.float(), b.float().t(), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("cfg", [-1, 1, 9])
 @pytest.mark.parametrize("act", [0, 1, 2])
-def test_gemm_epilogue(cuda, act):
+def test_gemm_epilogue(cuda, act, cfg):
     torch.manual_seed(1)
     M, N, K = 300, 264, 192
     a, w = bf(M, K), bf(N, K, scale=0.1)
     bias, res = bf(N), bf(M, N)
     pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    out = ops.gemm(a, w, tb=True, bias=bias, residual=res, act=act, preact=pre if act else None)
+    out = ops.gemm(a, w, tb=True, bias=bias, residual=res, act=act, preact=pre if act else None, cfg=cfg)
     h = a.float() @ w.float().t() + bias.float()
     y = {0: h, 1: F.relu(h), 2: F.gelu(h, approximate="tanh")}[act] + res.float()
     assert rel_err(out, y) < 1e-2
@@ -70,7 +108,7 @@ def test_gemm_epilogue(cuda, act):
         assert rel_err(pre, h) < 1e-2
 
 
-@pytest.mark.parametrize("split,cfg", [(2, 0), (4, 1), (8, -1), (3, 2)])
+@pytest.mark.parametrize("split,cfg", [(2, 0), (4, 1), (8, -1), (3, 2), (4, 9), (7, 9)])
 def test_gemm_splitk_fp32_accumulate(cuda, split, cfg):
     torch.manual_seed(2)
     M, N, K = 192, 320, 4096
@@ -101,7 +139,7 @@ def test_linear_autograd(cuda):
 
 
 @pytest.mark.parametrize("act", [3, 4])
-@pytest.mark.parametrize("cfg,split", [(0, 0), (1, 0), (6, 0), (2, 0), (0, 4), (-1, 0)])
+@pytest.mark.parametrize("cfg,split", [(0, 0), (1, 0), (6, 0), (2, 0), (0, 4), (-1, 0), (9, 0), (9, 3)])
 def test_gemm_act_backward_epilogue(cuda, act, cfg, split):
     """dH = (dY·W) ⊙ act'(pre) fused into the dgrad GEMM epilogue (3 = ReLU', 4 = GELU')."""
     torch.manual_seed(7)
