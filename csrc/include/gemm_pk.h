@@ -168,8 +168,8 @@ constexpr int pk_epi_stores() {
     return 16 * ((SPLIT || F32) ? 2 : 1) + (act_fwd(ACT) ? 16 : 0) + (act_bwd(ACT) ? 4 : 0);
 }
 
-// DBG (timing-only ablation builds, never instantiated by the launchers): bit 0 skips the
-// main-loop operand DMA, bit 1 the counted vmcnt waits.
+// DBG (timing-only ablation builds: gemm_pk_dbg.hip, cfg 90 + DBG; outputs are wrong): bit 0
+// skips the main-loop operand DMA, bit 1 the counted vmcnt waits, bit 2 the epilogue body.
 template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     constexpr int BM = 256, BN = 256;
@@ -518,51 +518,63 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                                 \
         acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j_][s_], Af[i_][s_], acc[MH][NH][i_][j_], 0, 0, 0);
 
+#define RN_PK_MMA_S(MH, NH, BF, S)                                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                 \
+    _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                                 \
+        acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j_][S], Af[i_][S], acc[MH][NH][i_][j_], 0, 0, 0);
+    // one phase: counted wait, this phase's fragment reads, the DMA of one half-tile (in the read
+    // segment, or between the two k-steps' MFMAs with DBG bit 3), barrier, 16 MFMAs, barrier
+#define RN_PK_PHASE(READS, ISSUE, MH, NH, BF)                                                          \
+    phase_wait();                                                                                      \
+    READS                                                                                              \
+    if constexpr (!(DBG & 8)) { ISSUE }                                                                \
+    sync_mma_begin();                                                                                  \
+    if constexpr (DBG & 8) {                                                                           \
+        RN_PK_MMA_S(MH, NH, BF, 0)                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        ISSUE                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        RN_PK_MMA_S(MH, NH, BF, 1)                                                                     \
+    } else {                                                                                           \
+        RN_PK_MMA(MH, NH, BF)                                                                          \
+    }                                                                                                  \
+    sync_mma_end();
+
 #pragma unroll 1
     for (int u = 0; u < my_items * nk; ++u) {
         const char* sl = smem + (u & 1) * (4 * PK_HALF);
         // q0: At + Bl  (fragment reads first: their latency runs under the DMA issue)
-        phase_wait();
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl, wr * 64 + i * 16, s, lane);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) Bl[j][s] = pk_frag_b<BKC>(sl + PK_HALF, wc * 32, j, s, lane);
-        }
-        issue_h(H2{});
-        sync_mma_begin();
-        RN_PK_MMA(0, 0, Bl)
-        sync_mma_end();
+        RN_PK_PHASE(
+            _Pragma("unroll") for (int s = 0; s < 2; ++s) {
+                _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl, wr * 64 + i * 16, s, lane);
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) Bl[j][s] = pk_frag_b<BKC>(sl + PK_HALF, wc * 32, j, s, lane);
+            },
+            issue_h(H2{});, 0, 0, Bl)
         // q1: At + Br
-        phase_wait();
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) Br[j][s] = pk_frag_b<BKC>(sl + 2 * PK_HALF, wc * 32, j, s, lane);
-        issue_h(H3{});
-        sync_mma_begin();
-        RN_PK_MMA(0, 1, Br)
-        sync_mma_end();
-        // q2: Ab + Br
-        phase_wait();
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl + 3 * PK_HALF, wr * 64 + i * 16, s, lane);
-        cur_adv();
-        issue_h(H0{});
-        sync_mma_begin();
-        RN_PK_MMA(1, 1, Br)
-        sync_mma_end();
+        RN_PK_PHASE(
+            _Pragma("unroll") for (int s = 0; s < 2; ++s)
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) Br[j][s] = pk_frag_b<BKC>(sl + 2 * PK_HALF, wc * 32, j, s, lane);,
+            issue_h(H3{});, 0, 1, Br)
+        // q2: Ab + Br (the cursor moves on to K-tile u + 2)
+        RN_PK_PHASE(
+            _Pragma("unroll") for (int s = 0; s < 2; ++s)
+                _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl + 3 * PK_HALF, wr * 64 + i * 16, s, lane);,
+            cur_adv(); issue_h(H0{});, 1, 1, Br)
         // q3: Ab + Bl (all fragments already in registers)
-        phase_wait();
-        issue_h(H1{});
-        sync_mma_begin();
-        RN_PK_MMA(1, 0, Bl)
-        sync_mma_end();
+        RN_PK_PHASE(, issue_h(H1{});, 1, 0, Bl)
         if (++c_kt == nk) {
-            epilogue(c_m0, c_n0, c_tm, c_sid);
+            if constexpr (!(DBG & 4)) {
+                epilogue(c_m0, c_n0, c_tm, c_sid);
+            } else {  // keep the accumulators (and the MFMAs feeding them) alive
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[a][b][i][j]));
+            }
             since_epi = 0;
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -581,6 +593,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         }
     }
 #undef RN_PK_MMA
+#undef RN_PK_MMA_S
+#undef RN_PK_PHASE
     if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger barrier
     (void)nphase;
     (void)c_kb;
@@ -588,9 +602,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 }
 
 // Launch: persistent grid of min(items, 256 × blocks-per-CU) workgroups (1 per CU: 128 KiB LDS).
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32>
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0>
 void launch_pk_t(GemmArgs& a, hipStream_t st) {
-    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32>;
+    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG>;
     static int attr_dev = -1;  // the >64 KiB LDS opt-in, per device the process launches on
     int dev = 0;
     (void)hipGetDevice(&dev);

@@ -1,4 +1,6 @@
-"""``python -m replicann [train args...]`` → the training entrypoint (replicann_amd.training.main)."""
-from replicann_amd.training import main
+"""``python -m replicann train|eval|build [args]`` → :func:`replicann_amd.cli.main`."""
+import sys
 
-main()
+from replicann_amd.cli import main
+
+sys.exit(main())

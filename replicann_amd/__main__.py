@@ -1,4 +1,6 @@
-"""``python -m replicann_amd [train args...]`` → training entrypoint."""
-from .training import main
+"""``python -m replicann_amd train|eval|build [args]`` → :func:`replicann_amd.cli.main`."""
+import sys
 
-main()
+from .cli import main
+
+sys.exit(main())

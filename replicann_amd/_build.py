@@ -14,6 +14,8 @@ shared headers and the flags.
 
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import hashlib
 import os
 import shutil
@@ -83,15 +85,30 @@ def _compile(src: Path, hdr: str, torch_inc) -> Path:
     obj = BUILD / f"{src.stem}.{key}.o"
     if obj.exists():
         return obj
-    cmd = [_hipcc()] + flags + ["-c", str(src), "-o", str(obj) + ".tmp"]
+    tmp = f"{obj}.tmp.{os.getpid()}"
+    cmd = [_hipcc()] + flags + ["-c", str(src), "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
-    os.replace(str(obj) + ".tmp", obj)
+    os.replace(tmp, obj)
     return obj
 
 
 IO_OUT = Path(__file__).resolve().parent / "_io.so"
+
+
+@contextlib.contextmanager
+def _build_lock():
+    """Serialise builds across processes (every data-parallel rank may trigger one): an
+    exclusive flock on build/.lock; outputs are written to per-process tmp names and renamed."""
+    lock = ROOT / "build" / ".lock"
+    lock.parent.mkdir(parents=True, exist_ok=True)
+    with open(lock, "a+") as fh:
+        fcntl.flock(fh, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(fh, fcntl.LOCK_UN)
 
 
 def build_runtime(verbose: bool = True) -> Path:
@@ -104,12 +121,16 @@ def build_runtime(verbose: bool = True) -> Path:
     stamp = IO_OUT.with_suffix(".stamp")
     if IO_OUT.exists() and stamp.exists() and stamp.read_text() == key:
         return IO_OUT
-    cxx = os.environ.get("CXX") or shutil.which("g++") or "/opt/rocm/llvm/bin/clang++"
-    r = subprocess.run([cxx, *flags, *map(str, srcs), "-o", str(IO_OUT) + ".tmp"], capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"runtime build failed:\n{r.stderr[-6000:]}")
-    os.replace(str(IO_OUT) + ".tmp", IO_OUT)
-    stamp.write_text(key)
+    with _build_lock():
+        if IO_OUT.exists() and stamp.exists() and stamp.read_text() == key:  # another process built it
+            return IO_OUT
+        cxx = os.environ.get("CXX") or shutil.which("g++") or "/opt/rocm/llvm/bin/clang++"
+        tmp = f"{IO_OUT}.tmp.{os.getpid()}"
+        r = subprocess.run([cxx, *flags, *map(str, srcs), "-o", tmp], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"runtime build failed:\n{r.stderr[-6000:]}")
+        os.replace(tmp, IO_OUT)
+        stamp.write_text(key)
     if verbose:
         print(f"[replicann build] linked {IO_OUT}")
     return IO_OUT
@@ -120,6 +141,11 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     ``_io.so``). Returns the ``_C.so`` path."""
     build_runtime(verbose)
     BUILD.mkdir(parents=True, exist_ok=True)
+    with _build_lock():
+        return _build_locked(verbose, jobs)
+
+
+def _build_locked(verbose, jobs):
     torch_inc, torch_lib = _torch_paths()
     hdr = _headers_digest()
     srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "bindings").glob("*.cpp"))
@@ -132,13 +158,14 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
         if verbose:
             print(f"[replicann build] up to date: {OUT}")
         return OUT
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(OUT) + ".tmp",
+    tmp = f"{OUT}.tmp.{os.getpid()}"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", tmp,
            f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
            f"-Wl,-rpath,{torch_lib}"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
-    os.replace(str(OUT) + ".tmp", OUT)
+    os.replace(tmp, OUT)
     stamp.write_text(link_key)
     if verbose:
         print(f"[replicann build] linked {OUT} from {len(objs)} objects")

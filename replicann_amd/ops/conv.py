@@ -65,6 +65,7 @@ class _ConvImplicitFn(torch.autograd.Function):
             # that follows every ResNet conv reduces instead of re-reading y for its statistics
             y, part = ops.conv_fwd_implicit_stats(x, w, bias, stride, pad)
             y._rn_bn_partials = part
+            y._rn_bn_version = y._version  # partials describe THIS version of y (see norm.py)
         else:
             y = ops.conv_fwd_implicit(x, w, bias, stride, pad)
         ctx.save_for_backward(x, w)

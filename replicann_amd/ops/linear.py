@@ -117,6 +117,7 @@ def _notify(p):
     uses = getattr(p, "_rn_direct_uses", 1)
     if uses > 1:
         left = getattr(p, "_rn_pending", uses) - 1
+        p._rn_flat.contributed(p, left == 0)  # DDP reduces each contribution of a tied parameter
         if left > 0:
             p._rn_pending = left
             return

@@ -114,6 +114,8 @@ class _BatchNormFn(torch.autograd.Function):
         part = getattr(x, "_rn_bn_partials", None)
         if part is not None and (part.dim() != 2 or part.shape[1] != 2 * C):
             part = None
+        if part is not None and getattr(x, "_rn_bn_version", -1) != x._version:
+            part = None  # x was modified in place after the conv: recompute the statistics
         y, mean, rstd = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
                                                  momentum, eps, relu, r2, part)
         ctx.save_for_backward(x2, y, weight, bias, mean, rstd)

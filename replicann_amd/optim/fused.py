@@ -37,6 +37,9 @@ class _FlatOptimizer:
         self.max_grad_norm = max_grad_norm
         self.grad_scale = grad_scale  # e.g. 1/world_size for DDP SUM-reduced grads
         self.step_count = 0
+        # gradient the step reads: the flat bf16 .grad buffer, or (data parallel) the fp32
+        # all-reduced copy the DDP reducer owns (``DistributedDataParallel.grad_source``)
+        self.grad_source = None
         dev = flat.data.device
         self.master = flat.data.float() if flat.data.dtype != torch.float32 else flat.data
         # device state: [‖g‖², skipped flag, step t, lr, bc1, bc2, -, -]
@@ -48,12 +51,16 @@ class _FlatOptimizer:
     def native(self):
         return _ext.use_native(self.flat.data)
 
+    @property
+    def grad(self):
+        return self.grad_source if self.grad_source is not None else self.flat.grad
+
     def grad_norm(self):
         """Global L2 norm of the (scaled) gradient as a device tensor."""
         if self.native:
-            _ext.ops().sumsq(self.flat.grad, self.norm_buf)
+            _ext.ops().sumsq(self.grad, self.norm_buf)
         else:
-            self.norm_buf[0] = self.flat.grad.float().pow(2).sum()
+            self.norm_buf[0] = self.grad.float().pow(2).sum()
         return self.norm_buf[0].sqrt() * self.grad_scale
 
     def _wd_elementwise(self):
@@ -112,14 +119,14 @@ class FusedAdamW(_FlatOptimizer):
         if self.native:
             ops = _ext.ops()
             self._prep(lr, b1, b2)
-            ops.sumsq(self.flat.grad, self.norm_buf)
-            ops.adamw_step(self.flat.data, self.master, self.flat.grad, self.m, self.v, self.flat.wd_mask,
+            ops.sumsq(self.grad, self.norm_buf)
+            ops.adamw_step(self.flat.data, self.master, self.grad, self.m, self.v, self.flat.wd_mask,
                            self.norm_buf, b1, b2, self.eps, self.weight_decay, self.grad_scale, clip)
             return
         lr = self._host_lr(lr)
         bc1 = 1 - b1 ** self.step_count
         bc2 = 1 - b2 ** self.step_count
-        g = self.flat.grad.float() * self.grad_scale
+        g = self.grad.float() * self.grad_scale
         norm = g.pow(2).sum().sqrt()
         if not torch.isfinite(norm):
             return
@@ -165,12 +172,12 @@ class FusedSGD(_FlatOptimizer):
         if self.native:
             ops = _ext.ops()
             self._prep(lr)
-            ops.sumsq(self.flat.grad, self.norm_buf)
-            ops.sgd_step(self.flat.data, self.master, self.flat.grad, self.buf, self.flat.wd_mask,
+            ops.sumsq(self.grad, self.norm_buf)
+            ops.sgd_step(self.flat.data, self.master, self.grad, self.buf, self.flat.wd_mask,
                          self.norm_buf, self.momentum, self.weight_decay, self.nesterov, self.grad_scale, clip)
             return
         lr = self._host_lr(lr)
-        g = self.flat.grad.float() * self.grad_scale
+        g = self.grad.float() * self.grad_scale
         norm = g.pow(2).sum().sqrt()
         if not torch.isfinite(norm):
             return

@@ -1,22 +1,34 @@
-"""Data parallelism: bucketed in-place gradient all-reduce overlapped with backward — N15/N16.
+"""Data parallelism: bucketed gradient all-reduce overlapped with backward — N15/N16.
 
 One process per GPU, ``torch.distributed`` with backend ``"nccl"`` (= RCCL on
 ROCm) over xGMI; ``gloo`` for the CPU tests.  The reference has no
 parallelism at all; this is built MI355X-first:
 
-* gradients live in ONE flat buffer (:class:`~replicann_amd.utils.flat.FlatParams`);
-  a bucket is a contiguous slice of it, so the all-reduce runs IN PLACE on the
-  gradient memory — no bucket copy-in/copy-out kernels;
+* gradients are produced in ONE flat bf16 buffer (:class:`~replicann_amd.utils.flat.FlatParams`);
+  the reduction runs in **fp32**: when a bucket (a contiguous slice of that buffer)
+  is complete it is widened into the same slice of a flat fp32 reduction buffer and
+  all-reduced there, in place — the cross-rank sum never rounds to bf16 (summing 8
+  bf16 partials in a bf16 ring loses up to 3 bits).  The fused optimizer then reads
+  the fp32 sums directly (``grad_source``), so there is no narrowing pass either.
+  ``reduce_dtype=torch.bfloat16`` keeps the bf16-in-place variant (half the bytes);
 * buckets are formed in reverse parameter order (the order backward produces
-  gradients) and sized for point-to-point xGMI rings (default 64 MB of bf16:
-  large enough that RCCL's per-collective latency is amortised over 7 links,
-  small enough that the first bucket launches early in the backward);
-* a post-accumulate-grad hook per parameter counts arrivals; when a bucket is
-  complete its ``all_reduce(SUM, async_op=True)`` is issued at once — RCCL
-  runs it on its own HIP stream, ordered after the producing kernels, and it
-  overlaps the rest of the backward;
-* buckets are always LAUNCHED in index order (a ready bucket waits for its
-  predecessors) so every rank issues the same collective sequence;
+  gradients) and sized for point-to-point xGMI rings (default 64 MB of reduced
+  elements: large enough to amortise RCCL's per-collective latency over the 7
+  links, small enough that the first bucket launches early in the backward);
+* a post-accumulate-grad hook per parameter (and ``FlatParams.mark_ready`` for the
+  gradients kernels accumulate directly) counts arrivals; a complete bucket's
+  ``all_reduce(SUM, async_op=True)`` is issued at once — RCCL runs it on its own HIP
+  stream, ordered after the producing kernels, overlapping the rest of the backward;
+* **tied parameters are split**: a parameter with several direct gradient
+  contributions per backward (GPT-2's ``wte``: LM-head weight gradient at the START
+  of the backward, embedding scatter at the END) gets a bucket of its own, and EACH
+  contribution is reduced as soon as it exists — the first one into the reduction
+  buffer, later ones into side buffers that ``finish()`` adds in (the bf16 slice is
+  cleared between contributions).  Without the split the 38.6 M-element ``wte``
+  bucket waited for the embedding backward and ran fully exposed after it;
+* buckets are LAUNCHED in index order (a ready bucket waits for its predecessors) and
+  split contributions at their (deterministic) arrival, so every rank issues the same
+  collective sequence;
 * the 1/world averaging is NOT a separate pass: it is folded into the fused
   optimizer's ``grad_scale``;
 * ``finish()`` waits on the outstanding works (stream-ordered, no host sync),
@@ -30,6 +42,7 @@ parallelism at all; this is built MI355X-first:
 from __future__ import annotations
 
 import contextlib
+import time
 
 import torch
 import torch.distributed as dist
@@ -40,7 +53,8 @@ from ..utils.flat import FlatParams
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, flat: FlatParams, bucket_mb: float = 64.0,
-                 process_group=None, broadcast: bool = True, check_unused: bool = False):
+                 process_group=None, broadcast: bool = True, check_unused: bool = False,
+                 reduce_dtype=torch.float32, split_tied: bool = True):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -51,34 +65,49 @@ class DistributedDataParallel(nn.Module):
         self._works = []
         if broadcast and self.world > 1:
             self._broadcast_state()
-        # ---- bucket assignment (reverse layout order) ----
-        elem = flat.grad.element_size()
-        cap = max(1, int(bucket_mb * 1024 * 1024 / elem))
+        self.reduce_dtype = reduce_dtype
+        self.fp32 = reduce_dtype == torch.float32 and flat.grad.dtype != torch.float32
+        # the buffer the all-reduce runs on (and the optimizer reads): fp32 copy, or the grads themselves
+        self.reduce_buf = (torch.zeros(flat.numel, dtype=torch.float32, device=flat.grad.device)
+                           if self.fp32 else flat.grad)
+        # ---- bucket assignment (reverse layout order); split (tied) parameters alone ----
         segs = flat.segments()
+        self.split = {}  # id(p) -> [lo, hi, uses, side buffers]
+        if split_tied:
+            for p, off, n in segs:
+                uses = getattr(p, "_rn_direct_uses", 1)
+                if uses > 1 and flat.direct:
+                    sides = [torch.zeros(n, dtype=self.reduce_buf.dtype, device=flat.grad.device)
+                             for _ in range(uses - 1)]
+                    self.split[id(p)] = [off, off + n, uses, sides]
+        elem = self.reduce_buf.element_size()
+        cap = max(1, int(bucket_mb * 1024 * 1024 / elem))
         self.buckets = []  # (lo, hi, n_params)
         self.param_bucket = {}
         cur_hi = None
         cur_lo = None
         cur_n = 0
         for p, off, n in reversed(segs):
+            if id(p) in self.split:
+                continue
             end = off + ((n + 63) // 64) * 64
             if cur_hi is None:
                 cur_hi, cur_lo, cur_n = end, off, 0
-            elif cur_hi - off > cap and cur_n > 0:
+            elif (cur_hi - off > cap or cur_lo != off + ((n + 63) // 64) * 64) and cur_n > 0:
+                # a split parameter between two neighbours breaks contiguity: close the bucket
                 self.buckets.append([cur_lo, cur_hi, cur_n])
                 cur_hi, cur_lo, cur_n = end, off, 0
             cur_lo = off
             cur_n += 1
             self.param_bucket[id(p)] = len(self.buckets)
-        self.buckets.append([cur_lo, cur_hi, cur_n])
-        self._pending = [b[2] for b in self.buckets]
-        self._ready = [False] * len(self.buckets)
-        self._launched = [False] * len(self.buckets)
-        self._next = 0
-        self._seen = set()
-        self.launched_in_backward = 0  # buckets whose all-reduce was issued from a gradient hook (last step)
+        if cur_hi is not None:
+            self.buckets.append([cur_lo, cur_hi, cur_n])
+        self._split_params = {id(p): p for p, _, _ in segs if id(p) in self.split}
+        self._reset()
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p, _, _ in segs]
         flat.ready_hooks.append(self._hook)  # parameters whose grads are accumulated directly by kernels
+        flat.contribution_hooks.append(self._contribution)
+        self.comm_wait_ms = 0.0  # host time spent in finish() (last step): the exposed all-reduce tail
 
     # ------------------------------------------------------------------
     def _broadcast_state(self):
@@ -93,20 +122,54 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         self._works = []
         self._seen = set()
+        self._split_done = {k: 0 for k in self.split}  # contributions reduced this step
         self.launched_in_backward = 0
+
+    def _reduce_slice(self, lo, hi, dst=None):
+        """Widen (fp32 mode) and all-reduce grad[lo:hi]; ``dst`` overrides the target buffer."""
+        g = self.flat.grad[lo:hi]
+        if dst is None:
+            dst = self.reduce_buf[lo:hi]
+        if dst.data_ptr() != g.data_ptr():
+            dst.copy_(g)  # stream-ordered after the kernels that produced the gradient
+        self._works.append(dist.all_reduce(dst, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
     def _launch_ready(self, from_hook=False):
         while self._next < len(self.buckets) and self._ready[self._next]:
             self.launched_in_backward += int(from_hook)
             lo, hi, _ = self.buckets[self._next]
-            w = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-            self._works.append(w)
+            self._reduce_slice(lo, hi)
             self._launched[self._next] = True
             self._next += 1
+
+    def _contribution(self, p, final):
+        """A direct gradient contribution to a split parameter is complete (``final``: its last)."""
+        if not self._sync or self.world == 1 or id(p) not in self.split:
+            return
+        lo, hi, uses, sides = self.split[id(p)]
+        k = self._split_done[id(p)]
+        if k >= uses:
+            return
+        g = self.flat.grad[lo:hi]
+        if self.fp32:
+            # contribution 0 → the reduction buffer, later ones → side buffers (added in finish)
+            self._reduce_slice(lo, hi, None if k == 0 else sides[k - 1])
+            if not final:
+                g.zero_()  # the next contribution accumulates into a cleared slice
+        elif final:
+            self._reduce_slice(lo, hi)  # bf16 in place: only this contribution is left in the slice
+        else:
+            sides[k].copy_(g)
+            g.zero_()
+            self._works.append(dist.all_reduce(sides[k], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        self._split_done[id(p)] = k + 1
+        self.launched_in_backward += 1
 
     def _hook(self, p):
         if not self._sync or self.world == 1:
             return
+        if id(p) in self.split:
+            return  # handled per contribution
         if id(p) in self._seen:  # a parameter used twice accumulates twice: count once
             return
         self._seen.add(id(p))
@@ -122,22 +185,50 @@ class DistributedDataParallel(nn.Module):
             self._reset()
         return self.module(*args, **kwargs)
 
+    @property
+    def grad_source(self):
+        """The tensor holding the all-reduced (SUM over ranks) flat gradient after ``finish()``."""
+        return self.reduce_buf
+
+    reduced_grad = grad_source
+
     def finish(self):
         """Complete the gradient reduction (call after backward, before the optimizer)."""
         if not self._sync or self.world == 1:
             return
+        t0 = time.perf_counter()
         unused = [i for i, r in enumerate(self._ready) if not r]
         if unused and self.check_unused:
             names = [self.flat.names.get(id(p), "?") for p, _, _ in self.flat.segments()
-                     if id(p) not in self._seen]
+                     if id(p) not in self._seen and id(p) not in self.split]
             raise RuntimeError(f"parameters received no gradient this step: {names[:8]}")
         for i in unused:
             self._ready[i] = True
         self._launch_ready()
+        # split parameters: contributions that never arrived (e.g. autograd-accumulated on CPU,
+        # where both uses land in .grad at once) are reduced now, as one
+        for pid, (lo, hi, uses, sides) in self.split.items():
+            k = self._split_done[pid]
+            if k < uses:
+                # the contributions that never signalled (e.g. autograd accumulated both uses at
+                # once, CPU path) are all in the slice: reduce it as ONE contribution
+                if self.fp32 and k > 0:
+                    self._reduce_slice(lo, hi, sides[k - 1])
+                    unused_sides = sides[k:]
+                else:
+                    self._reduce_slice(lo, hi)  # fp32: contribution 0; bf16: in place, sides[:k] hold the rest
+                    unused_sides = sides[k:]
+                for s_ in unused_sides:
+                    s_.zero_()
+            self._split_done[pid] = uses
         for w in self._works:
             w.wait()
+        for pid, (lo, hi, uses, sides) in self.split.items():
+            for s in sides:
+                self.reduce_buf[lo:hi].add_(s)
         assert all(self._launched), "a gradient bucket was never reduced"
         self._works = []
+        self.comm_wait_ms = (time.perf_counter() - t0) * 1e3
 
     @contextlib.contextmanager
     def no_sync(self):

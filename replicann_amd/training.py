@@ -1,5 +1,5 @@
-"""Training / evaluation entrypoints (N21) — ``replicann_amd.train(...)``,
-``replicann_amd.evaluate(...)`` and ``python -m replicann_amd`` (``train`` sub-command).
+"""Training / evaluation entrypoints (N21) — ``replicann.train(...)``,
+``replicann.evaluate(...)`` and ``python -m replicann train|eval`` (``replicann_amd.cli``).
 
 The reference has no training code at all; this API is
 defined here and frozen.  One step:
@@ -29,7 +29,7 @@ from .utils.checkpoint import load_checkpoint, save_checkpoint
 from .utils.data import SyntheticImages, SyntheticLM, SyntheticMNIST
 from .utils.token_data import TokenFileLM
 from .utils.flat import FlatParams
-from .utils.metrics import MetricsLogger, is_rank0, phase
+from .utils.metrics import MetricsLogger, PhaseTimer, is_rank0, phase
 
 MODEL_KINDS = {
     "gpt2-small": "lm", "gpt2-medium": "lm", "gpt2-medium-fp8": "lm", "gpt2-tiny": "lm",
@@ -88,6 +88,7 @@ class TrainConfig:
     data: str | None = None       # LM token shards (comma-separated paths / globs); None = synthetic
     data_dtype: str = "uint16"    # uint16 | uint32 shard element type
     data_mode: str = "train"      # train (random windows) | eval (non-overlapping windows)
+    phase_timing: bool = True     # device ms per phase (incl. comm wait) on logged eager steps
     model_kwargs: dict = field(default_factory=dict)
 
 
@@ -114,34 +115,55 @@ class Trainer:
         else:
             self.opt = FusedSGD(self.flat, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
                                 max_grad_norm=cfg.max_grad_norm, grad_scale=gs)
+        if self.ddp is not None:
+            self.opt.grad_source = self.ddp.grad_source  # fp32 all-reduced gradients
         self.opt.set_schedule(cfg.warmup_steps, max(cfg.steps, 1), cfg.min_lr_ratio)
         self.step_idx = 0
         self._graph = None
+        self._resume_state = None
         if cfg.resume:
-            self.step_idx, _ = load_checkpoint(cfg.resume, self.model, self.opt)
+            self.step_idx, _, self._resume_state = load_checkpoint(cfg.resume, self.model, self.opt)
             if self.ddp is not None:
                 self.ddp._broadcast_state()
         self.data = self._make_data()
         self.logger = MetricsLogger(cfg.metrics_path)
+        # per-phase device times (forward / backward / allreduce_wait / optimizer) of logged eager steps
+        self.timer = PhaseTimer(enabled=cfg.phase_timing)
 
     # ------------------------------------------------------------------
     def _make_data(self):
         c = self.cfg
         seed = c.seed * 1000 + self.rank
+        saved = (self._resume_state or {}).get("data") if c.data_mode == "train" else None
         if self.kind == "lm":
             vocab = self.model.config.vocab_size
             if c.data:
                 paths = sorted(p for pat in c.data.split(",") for p in (glob.glob(pat) or [pat]))
+                # the stream position: the cursor saved with the checkpoint (any grad_accum), else
+                # step × grad_accum for checkpoints that predate it; evaluation always starts at
+                # window 0, so two checkpoints of one run are scored on the same windows
+                if c.data_mode != "train":
+                    start = 0
+                elif saved is not None and "batch_index" in saved:
+                    start = int(saved["batch_index"])
+                else:
+                    start = self.step_idx * c.grad_accum
                 return TokenFileLM(paths, c.batch_size, c.seq_len, self.device, seed=c.seed, rank=self.rank,
                                    world=self.world, mode=c.data_mode, dtype=c.data_dtype,
-                                   start_batch=self.step_idx * c.grad_accum, vocab=vocab)
-            return SyntheticLM(c.batch_size, c.seq_len, vocab, self.device, seed=seed)
-        if self.kind == "image":
+                                   start_batch=start, vocab=vocab)
+            src = SyntheticLM(c.batch_size, c.seq_len, vocab, self.device, seed=seed)
+        elif self.kind == "image":
             m = self.model
             size = m.config.image_size if hasattr(m, "config") else c.image_size
             classes = m.config.num_classes if hasattr(m, "config") else m.fc.out_features
-            return SyntheticImages(c.batch_size, size, 3, classes, self.device, self.dtype, seed=seed)
-        return SyntheticMNIST(c.batch_size, self.device, seed=seed)
+            src = SyntheticImages(c.batch_size, size, 3, classes, self.device, self.dtype, seed=seed)
+        else:
+            src = SyntheticMNIST(c.batch_size, self.device, seed=seed)
+        if saved is not None:
+            src.load_state_dict(saved)
+        elif self.step_idx and c.data_mode == "train":
+            src.load_state_dict({"i": self.step_idx * c.grad_accum})
+        return src
 
     @property
     def net(self):
@@ -167,18 +189,20 @@ class Trainer:
         c = self.cfg
         self.opt.zero_grad()
         loss = None
+        t = self.timer
         for micro, (x, y) in enumerate(batches):
             sync_ctx = (self.ddp.no_sync() if (self.ddp is not None and micro < len(batches) - 1)
                         else contextlib.nullcontext())
             with sync_ctx:
-                with phase("forward"):
+                with phase("forward"), t("forward"):
                     loss = self.net(x, y)
-                with phase("backward"):
+                with phase("backward"), t("backward"):
                     (loss / c.grad_accum if c.grad_accum > 1 else loss).backward()
         if self.ddp is not None:
-            with phase("allreduce_wait"):
+            # device time the compute stream waits for the last all-reduces: the exposed comm
+            with phase("allreduce_wait"), t("allreduce_wait"):
                 self.ddp.finish()
-        with phase("optimizer"):
+        with phase("optimizer"), t("optimizer"):
             self.opt.step(lr)
         return loss.detach()
 
@@ -208,7 +232,7 @@ class Trainer:
         count = self.opt.step_count
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), self.timer.paused():
             for _ in range(2):
                 self._step_body(self._static)
         torch.cuda.current_stream().wait_stream(s)
@@ -218,7 +242,7 @@ class Trainer:
         torch.cuda.synchronize()
         del snap
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g), self.timer.paused():
             self._static_loss = self._step_body(self._static)
         self.opt.step_count = count  # capture only recorded the step; replays count themselves
         self._graph = g
@@ -243,9 +267,17 @@ class Trainer:
             self.step_idx += 1
             return self._static_loss
         batches = [next(self.data) for _ in range(c.grad_accum)]
-        loss = self._step_body(batches, lr)
+        # phase timing only on the steps that get logged (events + one sync there)
+        logged = (self.step_idx + 1) % c.log_every == 0 or self.step_idx + 1 >= c.steps
+        with self.timer.step(active=logged):
+            loss = self._step_body(batches, lr)
         self.step_idx += 1
         return loss
+
+    def save(self, path):
+        """Checkpoint (collective under DDP): model, optimizer, step, config, and every rank's RNG
+        states and data cursor."""
+        save_checkpoint(path, self.model, self.opt, self.step_idx, asdict(self.cfg), data=self.data)
 
     def lr_at(self, i):
         c = self.cfg
@@ -262,11 +294,14 @@ class Trainer:
             if i % c.log_every == 0 or i >= c.steps:
                 lv = float(loss)
                 dt = time.time() - t0
+                extra = self.timer.summary()  # forward_ms, backward_ms, allreduce_wait_ms (comm wait), optimizer_ms
+                if self.ddp is not None:
+                    extra["comm_host_ms"] = round(self.ddp.comm_wait_ms, 3)
                 self.logger.log(step=i, loss=round(lv, 5), lr=round(float(self.opt._host_lr(None)), 8),
-                                **self._throughput(i - start, dt))
+                                **self._throughput(i - start, dt), **extra)
                 last = lv
         if c.checkpoint:
-            save_checkpoint(c.checkpoint, self.model, self.opt, c.steps, asdict(c))
+            self.save(c.checkpoint)
         return {"final_loss": last, "steps": c.steps, "wall_s": time.time() - t0}
 
 
@@ -281,26 +316,35 @@ def train(config: TrainConfig | None = None, model=None, **kw):
 
 @torch.no_grad()
 def evaluate(model, data, steps=10):
-    """Mean loss (and accuracy for classifiers) over ``steps`` batches."""
+    """Mean loss (and accuracy for classifiers) over ``steps`` batches per rank; under
+    data parallelism the sums are all-reduced, so every rank returns the mean over ALL
+    ranks' batches (each rank reads its own round-robin share of the eval stream)."""
     was = model.training
     model.eval()
-    tot, acc, n = 0.0, 0.0, 0
+    dev = next(model.parameters()).device
+    sums = torch.zeros(3, dtype=torch.float64, device=dev)  # Σ loss·n, Σ correct, Σ n
     for _ in range(steps):
         x, y = next(data)
         out = model(x)
         if out.dim() == 3:  # LM logits
             lf = out.float().reshape(-1, out.shape[-1])
-            tot += float(torch.nn.functional.cross_entropy(lf, y.reshape(-1)))
+            yy = y.reshape(-1)
+            sums[0] += torch.nn.functional.cross_entropy(lf, yy, reduction="sum").double()
+            sums[2] += yy.numel()
         else:
-            tot += float(torch.nn.functional.cross_entropy(out.float(), y))
-            acc += float((out.argmax(-1) == y).float().mean())
-        n += 1
+            sums[0] += torch.nn.functional.cross_entropy(out.float(), y, reduction="sum").double()
+            sums[1] += (out.argmax(-1) == y).sum().double()
+            sums[2] += y.numel()
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(sums)
     model.train(was)
-    return {"loss": tot / n, "accuracy": acc / n}
+    tot, cor, n = (float(v) for v in sums.cpu())
+    return {"loss": tot / max(n, 1), "accuracy": cor / max(n, 1)}
 
 
 def eval_main(argv=None):
-    """``python -m replicann.eval``: mean loss (+ accuracy) of a model — random init, or a
+    """``python -m replicann eval``: mean loss (+ accuracy) of a model — random init, or a
     checkpoint written by ``train(checkpoint=...)`` — over synthetic batches, or over ``--data`` token shards in eval order."""
     ap = argparse.ArgumentParser(description="replicann evaluation entrypoint")
     ap.add_argument("--model", default="gpt2-small")

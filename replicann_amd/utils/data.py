@@ -50,6 +50,12 @@ class SyntheticLM:
     def __iter__(self):
         return self
 
+    def state_dict(self):
+        return {"i": self.i}
+
+    def load_state_dict(self, sd):
+        self.i = int(sd["i"])
+
 
 class SyntheticImages:
     """Random NHWC images + labels."""
@@ -67,6 +73,12 @@ class SyntheticImages:
 
     def __iter__(self):
         return self
+
+    def state_dict(self):
+        return {"i": self.i}
+
+    def load_state_dict(self, sd):
+        self.i = int(sd["i"])
 
 
 class SyntheticMNIST:
@@ -90,3 +102,9 @@ class SyntheticMNIST:
 
     def __iter__(self):
         return self
+
+    def state_dict(self):
+        return {"i": self.i}
+
+    def load_state_dict(self, sd):
+        self.i = int(sd["i"])

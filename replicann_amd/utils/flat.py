@@ -58,6 +58,7 @@ class FlatParams:
         # autograd's AccumulateGrad add.
         self.direct = direct
         self.ready_hooks = []
+        self.contribution_hooks = []  # (param, final) per direct contribution of a multi-use parameter
         for p in self.params:
             p._rn_flat = self
         # per-64-element-granule weight-decay flag (matrices decay; vectors don't)
@@ -80,6 +81,10 @@ class FlatParams:
     def mark_ready(self, p):
         for h in self.ready_hooks:
             h(p)
+
+    def contributed(self, p, final):
+        for h in self.contribution_hooks:
+            h(p, final)
 
     def segments(self):
         """[(param, offset, numel)] in layout order."""

@@ -1,9 +1,12 @@
 """Rank-0 logging + JSONL metrics and profiling hooks.
 
 ``MetricsLogger`` appends one JSON object per logged step (loss, samples/s,
-tokens/s, MFU, peak HBM).  ``phase()`` wraps a step phase in a
-``torch.profiler.record_function`` range so ``torch.profiler`` / rocprofv3
-traces show fwd / bwd / allreduce-wait / optimizer separately.
+tokens/s, MFU, peak HBM, and the per-phase device milliseconds of that step).
+``phase()`` wraps a step phase in a ``torch.profiler.record_function`` range so
+``torch.profiler`` / rocprofv3 traces show fwd / bwd / allreduce-wait / optimizer
+separately; ``PhaseTimer`` measures the same phases with device events on the
+steps that get logged (``allreduce_wait_ms`` = how long the compute stream waited
+for the gradient all-reduce after the backward: the exposed communication).
 """
 
 from __future__ import annotations
@@ -41,6 +44,64 @@ class MetricsLogger:
         if self.path:
             with open(self.path, "a") as f:
                 f.write(line + "\n")
+
+
+class PhaseTimer:
+    """Device-event timing of named step phases, only on steps marked active (the event
+    records are cheap, the read-back needs one sync, done when the step is logged)."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+        self._active = False
+        self._paused = 0
+        self._ev = []
+
+    @contextlib.contextmanager
+    def step(self, active=True):
+        self._active = self.enabled and active
+        self._ev = []
+        try:
+            yield
+        finally:
+            self._active = False
+
+    @contextlib.contextmanager
+    def paused(self):  # graph capture / warm-up: no events
+        self._paused += 1
+        try:
+            yield
+        finally:
+            self._paused -= 1
+
+    @contextlib.contextmanager
+    def __call__(self, name):
+        if not self._active or self._paused:
+            yield
+            return
+        cuda = torch.cuda.is_available() and torch.cuda.is_initialized()
+        if cuda:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            yield
+            e.record()
+        else:
+            s = time.perf_counter()
+            yield
+            e = time.perf_counter()
+        self._ev.append((name, s, e))
+
+    def summary(self):
+        """{phase}_ms of the last timed step (summed over micro-batches); {} if none."""
+        out = {}
+        for name, s, e in self._ev:
+            if isinstance(s, float):
+                ms = (e - s) * 1e3
+            else:
+                e.synchronize()
+                ms = s.elapsed_time(e)
+            out[f"{name}_ms"] = round(out.get(f"{name}_ms", 0.0) + ms, 3)
+        self._ev = []
+        return out
 
 
 @contextlib.contextmanager

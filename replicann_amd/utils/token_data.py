@@ -29,9 +29,9 @@ def _lib():
     global _LIB
     if _LIB is None:
         from .. import _build
-        path = _build.IO_OUT
-        if not path.exists():
-            _build.build_runtime(verbose=False)
+        # always through the hash-checked builder (cheap when up to date): a stale _io.so built
+        # from older loader sources must never be dlopen'ed with the current argtypes
+        path = _build.build_runtime(verbose=False)
         lib = ctypes.CDLL(str(path))
         lib.rn_loader_create.restype = ctypes.c_void_p
         lib.rn_loader_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -118,6 +118,10 @@ class TokenFileLM:
         else:
             t = buf.clone()
         return t[:, :-1], t[:, 1:]
+
+    def state_dict(self):
+        """Resume cursor (the trainer's checkpoints store it per rank)."""
+        return {"batch_index": int(self.batch_index), "paths": list(self.paths)}
 
     def close(self):
         if getattr(self, "_h", None):

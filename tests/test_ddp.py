@@ -54,16 +54,17 @@ def _worker(rank, world, port, bucket_mb, q):
         flat.zero_grad()
         ddp(x, y).backward()
         ddp.finish()
-        grad_avg = flat.grad.clone() / world
+        grad_avg = ddp.grad_source.clone() / world
         # 2) no_sync accumulation over two half-batches, then a synced one
         flat.zero_grad()
         with ddp.no_sync():
             ddp(x[:4], y[:4]).backward()
         ddp(x[4:], y[4:]).backward()
         ddp.finish()
-        grad_acc = flat.grad.clone() / world
+        grad_acc = ddp.grad_source.clone() / world
         # 3) optimizer keeps ranks identical
         opt = FusedAdamW(flat, lr=1e-2, grad_scale=1 / world)
+        opt.grad_source = ddp.grad_source
         for _ in range(3):
             flat.zero_grad()
             ddp(x, y).backward()
@@ -112,3 +113,128 @@ def test_ddp_gloo(world, bucket_mb):
         torch.testing.assert_close(grad_avg, ref_grad, atol=1e-6, rtol=1e-5)
         torch.testing.assert_close(grad_acc, ref_grad * 2, atol=1e-6, rtol=1e-5)  # sum of 2 half-batch means
         torch.testing.assert_close(params, res[0][3], atol=0, rtol=0)
+
+
+# ---------------------------------------------------------------- tied weights, split reduction
+class _DirectHead(torch.autograd.Function):
+    """y = h·Wᵀ whose backward accumulates dW straight into the flat .grad view and signals the
+    contribution (what the GEMM epilogue + ops.linear._notify do on the GPU path)."""
+
+    @staticmethod
+    def forward(ctx, h, w):
+        ctx.save_for_backward(h, w)
+        return h @ w.t()
+
+    @staticmethod
+    def backward(ctx, gy):
+        from replicann_amd.ops.linear import _notify
+        h, w = ctx.saved_tensors
+        g2, h2 = gy.reshape(-1, gy.shape[-1]), h.reshape(-1, h.shape[-1])
+        w.grad.add_((g2.t() @ h2).to(w.grad.dtype))
+        _notify(w)
+        return gy @ w, None
+
+
+class _DirectEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w):
+        ctx.save_for_backward(ids)
+        ctx.w = w
+        return w[ids]
+
+    @staticmethod
+    def backward(ctx, g):
+        from replicann_amd.ops.linear import _notify
+        (ids,) = ctx.saved_tensors
+        ctx.w.grad.index_add_(0, ids.reshape(-1), g.reshape(-1, g.shape[-1]).to(ctx.w.grad.dtype))
+        _notify(ctx.w)
+        return None, None
+
+
+class TiedNet(torch.nn.Module):
+    """Token embedding tied to the output head (GPT-2's wte): two direct gradient contributions,
+    the head's at the start of the backward and the embedding's at the end."""
+
+    def __init__(self):
+        super().__init__()
+        self.wte = torch.nn.Parameter(torch.randn(40, 16) * 0.3)
+        self.wte._rn_shared = True
+        self.wte._rn_direct_uses = 2
+        self.mid = torch.nn.Linear(16, 16)
+        self.tail = torch.nn.Linear(16, 16)
+
+    def forward(self, ids, y):
+        h = _DirectEmbed.apply(ids, self.wte)
+        h = self.tail(torch.relu(self.mid(h)))
+        logits = _DirectHead.apply(h, self.wte)
+        return torch.nn.functional.cross_entropy(logits.float().reshape(-1, 40), y.reshape(-1))
+
+
+def _tied_data(world):
+    g = torch.Generator().manual_seed(3)
+    return torch.randint(0, 40, (world * 4, 6), generator=g), torch.randint(0, 40, (world * 4, 6), generator=g)
+
+
+def _tied_worker(rank, world, port, dtype_name, reduce_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from replicann_amd.parallel import DistributedDataParallel
+        from replicann_amd.utils.flat import FlatParams
+        dtype, rdt = getattr(torch, dtype_name), getattr(torch, reduce_name)
+        torch.manual_seed(0)
+        net = TiedNet().to(dtype)
+        flat = FlatParams(net)
+        ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_dtype=rdt)
+        X, Y = _tied_data(world)
+        x, y = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
+        res = []
+        for _ in range(2):  # twice: the per-step split state must reset
+            flat.zero_grad()
+            ddp(x, y).backward()
+            launched = ddp.launched_in_backward
+            ddp.finish()
+            res.append((ddp.grad_source.float() / world).numpy())
+        q.put((rank, res, launched, len(ddp.buckets), ddp.grad_source.dtype == torch.float32))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype_name,reduce_name", [("float32", "float32"), ("bfloat16", "float32"),
+                                                    ("bfloat16", "bfloat16")])
+def test_ddp_tied_split_gloo(dtype_name, reduce_name):
+    """A tied parameter's two contributions are all-reduced separately (the head's during the
+    backward) and summed in finish(); result = single-process gradient of the whole batch, for the
+    fp32 reduction buffer (bf16 grads widened) and the bf16 in-place mode."""
+    from replicann_amd.utils.flat import FlatParams
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tied_worker, args=(r, world, port, dtype_name, reduce_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dtype = getattr(torch, dtype_name)
+    torch.manual_seed(0)
+    net = TiedNet().to(dtype)
+    flat = FlatParams(net)
+    X, Y = _tied_data(world)
+    flat.zero_grad()
+    # per-rank mean losses averaged == mean over the concatenated batch (equal shard sizes)
+    net(X, Y).backward()
+    ref = flat.grad.float()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    for rank, grads, launched, nb, is_fp32 in res:
+        assert nb >= 2
+        assert is_fp32 == (reduce_name == "float32" or dtype == torch.float32)
+        # the head contribution + every regular bucket + the embedding contribution, all in backward
+        assert launched == nb + 2, (launched, nb)
+        for g in grads:
+            g = torch.from_numpy(g)
+            err = ((g - ref).norm() / ref.norm()).item()
+            assert err < tol, (rank, err)
+    torch.testing.assert_close(torch.from_numpy(res[0][1][1]), torch.from_numpy(res[1][1][1]), atol=0, rtol=0)

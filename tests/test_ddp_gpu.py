@@ -60,7 +60,7 @@ def _worker(rank, world, port, q):
         torch.cuda.synchronize()
         # numpy is pickled by value (a CPU tensor would travel as a shared-memory fd
         # that can vanish when this worker exits before the parent unpickles it)
-        q.put((rank, (flat.grad.float() / world).cpu().numpy(), hooked, len(ddp.buckets)))
+        q.put((rank, (ddp.grad_source.float() / world).cpu().numpy(), hooked, len(ddp.buckets)))
     finally:
         dist.destroy_process_group()
 
@@ -89,7 +89,8 @@ def test_ddp_native_path_two_ranks_one_gpu():
     ref = flat.grad.float().cpu()
     for rank, g, hooked, nb in res:
         assert nb > 2
-        assert hooked == nb, f"rank {rank}: only {hooked}/{nb} buckets were launched during the backward"
+        # every bucket + both contributions of the tied wte (LM head, embedding) during the backward
+        assert hooked == nb + 2, f"rank {rank}: only {hooked}/{nb}+2 reductions were launched during the backward"
         err = (g - ref).norm() / ref.norm()
         assert err < 2e-2, f"rank {rank}: rel err {err}"
     torch.testing.assert_close(res[0][1], res[1][1], atol=0, rtol=0)
