@@ -27,7 +27,8 @@ using c10::optional;
 extern "C" {
 void rn_act_fwd(const void*, void*, long, int, hipStream_t);
 void rn_act_bwd(const void*, const void*, void*, long, int, hipStream_t);
-void rn_dropout(const void*, void*, long, float, uint64_t, hipStream_t);
+void rn_dropout(const void*, void*, long, float, uint64_t, const uint64_t*, hipStream_t);
+void rn_rng_next(void*, void*, hipStream_t);
 void rn_add(const void*, const void*, void*, long, int, hipStream_t);
 void rn_bias_act_grad(const void*, const void*, void*, float*, void*, float*, int, int, int, int, int, hipStream_t);
 int rn_bias_act_grad_splits(int, int);
@@ -57,10 +58,10 @@ int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, fl
 int rn_gemm_cfg_bm(int);
 long rn_gemm_colpart_rows(int, int);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
-                int, int, float, int, float, uint64_t, hipStream_t);
+                int, int, float, int, float, uint64_t, const uint64_t*, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
                 void*, void*, void*, float*, float*, float*, const long*, int, int, int, int, int, float, int, float,
-                uint64_t, float*, hipStream_t);
+                uint64_t, const uint64_t*, float*, hipStream_t);
 void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
 int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
@@ -370,11 +371,23 @@ Tensor act_bwd(const Tensor& dy, const Tensor& x, int64_t kind) {
     rn_act_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), dy.numel(), (int)kind, cur_stream());
     return dx;
 }
-Tensor dropout_fwd(const Tensor& x, double p, int64_t seed) {
+// seed_buf: optional 1-element int64 DEVICE tensor (from rng_next) — the kernel reads its seed there,
+// so a captured hipGraph replays with a fresh draw each step
+const uint64_t* seed_ptr(const optional<Tensor>& sb) {
+    if (!(sb && sb->defined())) return nullptr;
+    TORCH_CHECK(sb->scalar_type() == at::kLong && sb->numel() >= 1 && sb->is_cuda(), "seed_buf: 1-element int64 GPU tensor");
+    return (const uint64_t*)sb->data_ptr();
+}
+Tensor dropout_fwd(const Tensor& x, double p, int64_t seed, const optional<Tensor>& seed_buf) {
     CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
     Tensor y = at::empty_like(x);
-    rn_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint64_t)seed, cur_stream());
+    rn_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint64_t)seed, seed_ptr(seed_buf), cur_stream());
     return y;
+}
+void rng_next(const Tensor& state, const Tensor& out) {
+    TORCH_CHECK(state.scalar_type() == at::kLong && out.scalar_type() == at::kLong && state.is_cuda() && out.is_cuda());
+    GUARD(state);
+    rn_rng_next(state.data_ptr(), out.data_ptr(), cur_stream());
 }
 Tensor add_act(const Tensor& a, const Tensor& b, bool relu) {
     CHECK_BF16(a); CHECK_CONTIG(a); CHECK_CONTIG(b); GUARD(a);
@@ -566,7 +579,8 @@ void strides_bth(const Tensor& t, std::vector<long>& s) {
     s.push_back(t.stride(0)); s.push_back(t.stride(1)); s.push_back(t.stride(2));
 }
 std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& bias,
-                                    double scale, bool causal, double p, int64_t seed) {
+                                    double scale, bool causal, double p, int64_t seed,
+                                    const optional<Tensor>& seed_buf) {
     CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); GUARD(q);
     const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3), Tk = k.size(1);
     Tensor o = at::empty({B, Tq, H, D}, q.options());
@@ -581,13 +595,14 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
     if (B * H * Tq == 0) return {o, lse};
     int rc = rn_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                          bias && bias->defined() ? bias->data_ptr<float>() : nullptr, bias_b, s.data(), B, H, Tq, Tk, D,
-                         (float)scale, causal, (float)p, (uint64_t)seed, cur_stream());
+                         (float)scale, causal, (float)p, (uint64_t)seed, seed_ptr(seed_buf), cur_stream());
     TORCH_CHECK(rc == 0, "attention: unsupported shape D=", D, " Tk=", Tk);
     return {o, lse};
 }
 void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                    const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
-                   const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad = {}) {
+                   const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad = {},
+                   const optional<Tensor>& seed_buf = {}) {
     GUARD(q);
     const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3), Tk = k.size(1);
     std::vector<long> s;
@@ -614,7 +629,8 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
                          bias && bias->defined() ? bias->data_ptr<float>() : nullptr, bias_b, dq.data_ptr(), dk.data_ptr(),
                          dv.data_ptr(), delta.data_ptr<float>(), dk32.defined() ? dk32.data_ptr<float>() : nullptr,
                          dv32.defined() ? dv32.data_ptr<float>() : nullptr, s.data(), B, H, Tq, Tk, D, (float)scale,
-                         causal, (float)p, (uint64_t)seed, want_bg ? bsum.data_ptr<float>() : nullptr, cur_stream());
+                         causal, (float)p, (uint64_t)seed, seed_ptr(seed_buf), want_bg ? bsum.data_ptr<float>() : nullptr,
+                         cur_stream());
     TORCH_CHECK(rc == 0, "attention backward: unsupported shape D=", D);
     if (want_bg) {
         const int C = 3 * H * D;
@@ -625,17 +641,19 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
 }
 std::tuple<Tensor, Tensor, Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
                                             const Tensor& o, const Tensor& lse, const optional<Tensor>& bias,
-                                            double scale, bool causal, double p, int64_t seed) {
+                                            double scale, bool causal, double p, int64_t seed,
+                                            const optional<Tensor>& seed_buf) {
     Tensor dq = at::empty(q.sizes(), q.options());
     Tensor dk = at::empty(k.sizes(), k.options());
     Tensor dv = at::empty(v.sizes(), v.options());
-    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv);
+    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, {}, seed_buf);
     return {dq, dk, dv};
 }
 void attn_bwd_out(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                   const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
-                  const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad) {
-    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, qkv_bias_grad);
+                  const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad,
+                  const optional<Tensor>& seed_buf) {
+    attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, qkv_bias_grad, seed_buf);
 }
 
 // ------------------------------------------------------------------ implicit-GEMM conv
@@ -885,7 +903,8 @@ TORCH_LIBRARY(replicann, m) {
     m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias, Tensor(a!)? db_accum=None) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
-    m.def("dropout_fwd(Tensor x, float p, int seed) -> Tensor");
+    m.def("dropout_fwd(Tensor x, float p, int seed, Tensor? seed_buf=None) -> Tensor");
+    m.def("rng_next(Tensor(a!) state, Tensor(b!) out) -> ()");
     m.def("add_act(Tensor a, Tensor b, bool relu) -> Tensor");
     m.def("softmax_fwd(Tensor x, float scale) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y, float scale) -> Tensor");
@@ -904,12 +923,13 @@ TORCH_LIBRARY(replicann, m) {
           "float b1, float b2, float eps, float wd, float gscale, float clip) -> ()");
     m.def("sgd_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) buf, Tensor wdm, Tensor(e!) state, "
           "float mom, float wd, bool nesterov, float gscale, float clip) -> ()");
-    m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? bias, float scale, bool causal, float p, int seed) -> (Tensor, Tensor)");
+    m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? bias, float scale, bool causal, float p, int seed, "
+          "Tensor? seed_buf=None) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
-          "bool causal, float p, int seed) -> (Tensor, Tensor, Tensor)");
+          "bool causal, float p, int seed, Tensor? seed_buf=None) -> (Tensor, Tensor, Tensor)");
     m.def("attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
           "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, "
-          "Tensor(d!)? qkv_bias_grad=None) -> ()");
+          "Tensor(d!)? qkv_bias_grad=None, Tensor? seed_buf=None) -> ()");
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("conv_fwd_implicit(Tensor x, Tensor w, Tensor? bias, int S, int P) -> Tensor");
     m.def("conv_fwd_implicit_stats(Tensor x, Tensor w, Tensor? bias, int S, int P) -> (Tensor, Tensor)");
@@ -941,6 +961,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("act_fwd", &act_fwd);
     m.impl("act_bwd", &act_bwd);
     m.impl("dropout_fwd", &dropout_fwd);
+    m.impl("rng_next", &rng_next);
     m.impl("add_act", &add_act);
     m.impl("softmax_fwd", &softmax_fwd);
     m.impl("softmax_bwd", &softmax_bwd);

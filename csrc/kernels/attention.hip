@@ -47,6 +47,9 @@ struct AttnArgs {
     int causal, bias_b;
     float scale, p_drop;
     uint64_t seed;
+    // optional device seed (graph-capturable dropout: drawn on the device per call, see ops/rng.py);
+    // replaces `seed` when set
+    const uint64_t* seed_ptr;
     float* dk32; float* dv32;  // generic bwd scratch
     // optional [B * ceil(T/64)][3 * H * 64] fp32: per-64-row-block column sums of dQ | dK | dV
     // (the packed-QKV projection's bias gradient, reduced later) — fast path, self-attention
@@ -291,6 +294,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
         for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+    if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
     for (int t = 0; t < nkv; ++t) {
         vm_wait_all();   // this wave's DMA of tile t landed ...
         __syncthreads(); // ... and every wave's; every wave also finished tile t-1 (its buffer is free)
@@ -721,6 +725,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
         for (int jd = 0; jd < 4; ++jd) { dvacc[u][jd] = (f32x4){0, 0, 0, 0}; dkacc[u][jd] = (f32x4){0, 0, 0, 0}; }
 
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+    if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
     // Tiles split into masked (causal diagonal of this block's keys, ragged Tq / Tk) and unmasked
     // ones, each class in its own loop: a per-wave `continue` or a runtime mask branch inside one
     // loop makes hipcc carry the accumulators through a phi (a VGPR copy block every tile).
@@ -937,6 +942,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+    if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
     // masked (diagonal / ragged) and unmasked tiles in separate loops, see the dK/dV kernel
     auto masked_tile = [&](int t) {
         return (t * 64 + 64 > p.Tk) || (qb * QB + QB > p.Tq) || (CAUSAL && t * 64 + 63 > qb * QB + off);
@@ -1098,6 +1104,7 @@ __global__ void __launch_bounds__(256) attn_fwd_generic_k(AttnArgs p) {
     sum = block_sum(sum, red);
     const float inv = sum > 0.f ? 1.f / sum : 0.f;
     const float rd = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+    if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
     for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
         float pv = sc[kj] * inv;
         if (p.p_drop > 0.f) pv = hash_uniform(p.seed, drop_idx(p, b, h, qi, kj)) >= p.p_drop ? pv * rd : 0.f;
@@ -1133,6 +1140,7 @@ __global__ void __launch_bounds__(256) attn_bwd_generic_k(AttnArgs p) {
     dl = block_sum(dl, red);
     const float L = p.lse[((long)b * p.H + h) * p.Tq + qi] * (p.lse_log2 ? LN2 : 1.f);
     const float rd = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+    if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
     for (int kj = threadIdx.x; kj < p.Tk; kj += 256) {
         const bf16* kp = p.k + b * p.k_sb + (long)kj * p.k_st + h * p.k_sh;
         const bf16* vp = p.v + b * p.v_sb + (long)kj * p.v_st + h * p.v_sh;
@@ -1197,8 +1205,9 @@ extern "C" {
 // strides in elements: [b, t, h] for q, k, v, o ; d is contiguous
 int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* bias, int bias_b,
                 const long* strides, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
-                uint64_t seed, hipStream_t st) {
+                uint64_t seed, const uint64_t* seed_ptr, hipStream_t st) {
     AttnArgs a = {};
+    a.seed_ptr = seed_ptr;
     a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = lse; a.bias = bias;
     a.q_sb = strides[0]; a.q_st = strides[1]; a.q_sh = strides[2];
     a.k_sb = strides[3]; a.k_st = strides[4]; a.k_sh = strides[5];
@@ -1236,8 +1245,9 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
 int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                 const float* bias, int bias_b, void* dq, void* dk, void* dv, float* delta, float* dk32, float* dv32,
                 const long* s, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
-                uint64_t seed, float* bsum, hipStream_t st) {
+                uint64_t seed, const uint64_t* seed_ptr, float* bsum, hipStream_t st) {
     AttnArgs a = {};
+    a.seed_ptr = seed_ptr;
     a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = (float*)lse;
     a.bias = bias; a.dout = (const bf16*)dout; a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.delta = delta;
     a.q_sb = s[0]; a.q_st = s[1]; a.q_sh = s[2]; a.k_sb = s[3]; a.k_st = s[4]; a.k_sh = s[5];

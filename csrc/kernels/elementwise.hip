@@ -43,7 +43,8 @@ __global__ void __launch_bounds__(TPB) act_bwd_k(const bf16* __restrict__ dy, co
 }
 
 __global__ void __launch_bounds__(TPB) dropout_k(const bf16* __restrict__ x, bf16* __restrict__ y, long n,
-                                                 float p, uint64_t seed) {
+                                                 float p, uint64_t seed, const uint64_t* __restrict__ seed_ptr) {
+    if (seed_ptr) seed = *seed_ptr;  // device-drawn seed (graph-capturable dropout)
     const float keep = 1.f / (1.f - p);
     long n8 = n / 8;
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n8; i += (long)gridDim.x * TPB) {
@@ -150,8 +151,22 @@ void rn_act_bwd(const void* dy, const void* x, void* dx, long n, int kind, hipSt
     else act_bwd_k<ACT_RELU><<<g, TPB, 0, st>>>((const bf16*)dy, (const bf16*)x, (bf16*)dx, n);
 }
 
-void rn_dropout(const void* x, void* y, long n, float p, uint64_t seed, hipStream_t st) {
-    dropout_k<<<ew_grid(n / 8 + 1), TPB, 0, st>>>((const bf16*)x, (bf16*)y, n, p, seed);
+void rn_dropout(const void* x, void* y, long n, float p, uint64_t seed, const uint64_t* seed_ptr, hipStream_t st) {
+    dropout_k<<<ew_grid(n / 8 + 1), TPB, 0, st>>>((const bf16*)x, (bf16*)y, n, p, seed, seed_ptr);
+}
+
+// Device RNG stream for dropout seeds (ops/rng.py): out[0] = splitmix64(state[0]); state[0] += γ.
+// One thread; stream-ordered, so a captured hipGraph draws a fresh seed at every replay.
+__global__ void rng_next_k(uint64_t* __restrict__ state, uint64_t* __restrict__ out) {
+    uint64_t z = state[0] + 0x9E3779B97F4A7C15ull;
+    state[0] = z;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    out[0] = z ^ (z >> 31);
+}
+
+void rn_rng_next(void* state, void* out, hipStream_t st) {
+    rng_next_k<<<1, 1, 0, st>>>((uint64_t*)state, (uint64_t*)out);
 }
 
 void rn_add(const void* a, const void* b, void* y, long n, int relu, hipStream_t st) {

@@ -75,20 +75,20 @@ def softmax(x, dim=-1, scale=1.0):
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
-        y = _ext.ops().dropout_fwd(x.contiguous(), p, seed)
-        ctx.p, ctx.seed = p, seed
+    def forward(ctx, x, p, seed_buf):
+        y = _ext.ops().dropout_fwd(x.contiguous(), p, 0, seed_buf)
+        ctx.p, ctx.seed_buf = p, seed_buf
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        return _ext.ops().dropout_fwd(gy.contiguous(), ctx.p, ctx.seed), None, None
+        return _ext.ops().dropout_fwd(gy.contiguous(), ctx.p, 0, ctx.seed_buf), None, None
 
 
 def dropout(x, p, training=True):
     if not training or p == 0.0:
         return x
     if _ext.use_native(x):
-        seed = int(torch.randint(0, 2**62, (1,)).item())
-        return _DropoutFn.apply(x, float(p), seed)
+        from .rng import next_seed
+        return _DropoutFn.apply(x, float(p), next_seed(x.device))  # seed drawn on the device
     return F.dropout(x, p, True)

@@ -78,7 +78,8 @@ def attention_reference(q, k, v, scale, causal=False, bias=None, dropout_p=0.0, 
 class _AttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, bias, scale, causal, dropout_p, seed):
-        o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, seed)
+        # seed: None, or a 1-element int64 device tensor (ops/rng.py) the kernels read
+        o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, 0, seed)
         ctx.save_for_backward(q, k, v, o, lse, bias)
         ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed = scale, causal, dropout_p, seed
         return o
@@ -87,7 +88,7 @@ class _AttnFn(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse, bias = ctx.saved_tensors
         dq, dk, dv = _ext.ops().attn_bwd(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
-                                         ctx.dropout_p, ctx.seed)
+                                         ctx.dropout_p, 0, ctx.seed)
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -103,7 +104,8 @@ def attention(q, k, v, *, scale=None, causal=False, bias=None, mask=None, dropou
     p = dropout_p if training else 0.0
     if _ext.use_native(q):
         b3 = _bias_3d(bias, B, Tq, Tk)
-        seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+        from .rng import next_seed
+        seed = next_seed(q.device) if p > 0 else None  # drawn on the device: graph-capturable
         return _AttnFn.apply(q, k, v, b3, float(scale), bool(causal), float(p), seed)
     return attention_reference(q, k, v, scale, causal, bias, p, training)
 
@@ -114,7 +116,7 @@ class _AttnPackedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, bias, scale, causal, dropout_p, seed, producer_bias):
         q, k, v = qkv.unbind(2)
-        o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, seed)
+        o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, 0, seed)
         ctx.save_for_backward(qkv, o, lse, bias)
         ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed = scale, causal, dropout_p, seed
         ctx.producer_bias = producer_bias
@@ -131,7 +133,7 @@ class _AttnPackedFn(torch.autograd.Function):
         B, T, _, H, D = qkv.shape
         pb_acc = _direct_grad(pb) if (pb is not None and D == 64 and pb.numel() == 3 * H * D) else None
         _ext.ops().attn_bwd_out(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
-                                ctx.dropout_p, ctx.seed, dq, dk, dv, pb_acc)
+                                ctx.dropout_p, 0, dq, dk, dv, pb_acc, ctx.seed)
         if pb_acc is not None:  # Σ_rows dQKV reduced in the kernels: the c_attn bias gradient
             pb._rn_bias_done = True
             _notify(pb)
@@ -154,7 +156,8 @@ def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dro
     p = dropout_p if training else 0.0
     if _ext.use_native(qkv):
         b3 = _bias_3d(bias, B, T, T)
-        seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+        from .rng import next_seed
+        seed = next_seed(qkv.device) if p > 0 else None
         return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed, producer_bias)
     q, k, v = qkv.unbind(2)
     return attention_reference(q, k, v, scale, causal, bias, p, training)

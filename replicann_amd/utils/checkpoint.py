@@ -30,6 +30,8 @@ def rank_state(data=None):
     st = {"rng_cpu": torch.get_rng_state()}
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         st["rng_cuda"] = torch.cuda.get_rng_state()
+        from ..ops import rng as dev_rng
+        st["rng_dropout"] = {str(k): v for k, v in dev_rng.state_dict().items()}  # device dropout streams
     if data is not None and hasattr(data, "state_dict"):
         st["data"] = data.state_dict()
     return st
@@ -81,4 +83,7 @@ def load_checkpoint(path, model, optimizer=None, strict=True, map_location="cpu"
             torch.set_rng_state(cpu)
         if mine is not None and "rng_cuda" in mine and torch.cuda.is_available():
             torch.cuda.set_rng_state(mine["rng_cuda"])
+        if mine is not None and mine.get("rng_dropout") and torch.cuda.is_available():
+            from ..ops import rng as dev_rng
+            dev_rng.load_state_dict(mine["rng_dropout"])
     return sd.get("step", 0), sd.get("config", {}), mine

@@ -1,0 +1,41 @@
+"""Deterministic weights / inputs shared by scripts/gen_reference_fixtures.py (which runs the
+reference's own code from /root/reference/src on the CPU, fp32) and tests/test_reference_parity_gpu.py
+(which runs the native bf16 GPU path on the GPU box, where the reference is not mounted)."""
+
+import torch
+
+CASES = [  # name, block, n_heads, E, T, extra ctor kwargs
+    ("enc_h12_e768", "TransformerEncoder", 12, 768, 128, {}),
+    ("enc_h8_e256", "TransformerEncoder", 8, 256, 96, {}),
+    ("enc_h4_e512", "TransformerEncoder", 4, 512, 64, {}),
+    ("dec_h12_e768", "TransformerDecoder", 12, 768, 128, {"context_size": 256}),
+    ("dec_h8_e256", "TransformerDecoder", 8, 256, 80, {"context_size": 256}),
+]
+CROSS = ("xdec_h12_e768", 12, 768, 96, 64)  # name, H, E, T_src, T_tgt
+
+
+def det_state_dict(module, seed):
+    """Weights drawn from a seeded generator in state_dict key order (independent of either
+    implementation's init); LayerNorms near identity, buffers (the decoder mask) kept."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, v in module.state_dict().items():
+        if k.endswith("_attn_mask"):
+            sd[k] = v.clone()
+        elif k.endswith("ln.weight"):
+            sd[k] = 1.0 + 0.1 * torch.randn(v.shape, generator=g)
+        elif k.endswith("bias"):
+            sd[k] = 0.02 * torch.randn(v.shape, generator=g)
+        else:
+            sd[k] = torch.randn(v.shape, generator=g) * (v.shape[-1] ** -0.5)
+    return sd
+
+
+def det_input(shape, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g) * 0.5
+
+
+def det_grad(shape, seed):
+    g = torch.Generator().manual_seed(seed + 7)
+    return torch.randn(shape, generator=g)

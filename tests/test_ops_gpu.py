@@ -684,3 +684,39 @@ def test_conv_bn_fused_statistics(cuda, monkeypatch, fused, N, HW, C, OC):
     assert rel_err(rm, rmf) < 2e-2 and rel_err(rv, rvf) < 2e-2
     for t, tf in ((x, xf), (w, wf), (g, gf), (b, bf_)):
         assert rel_err(t.grad, tf.grad) < 3e-2
+
+
+def test_dropout_device_seeds_graph_capture(cuda):
+    """Device-drawn dropout seeds (ops/rng.py): a captured hipGraph of a train-mode reference
+    TransformerDecoder step (head dropout 0.1 + block dropout) replays with FRESH masks every replay,
+    and replays reproduce eager steps started from the same device RNG state bit for bit."""
+    import replicann_amd.arch.transformer as T
+    from replicann_amd.ops import rng
+    torch.manual_seed(0)
+    m = T.TransformerDecoder(4, 256, context_size=64, p_dropout=0.1).cuda().to(torch.bfloat16).train()
+    x = bf(2, 64, 256)
+
+    def step():
+        return m(x).float().sum()
+
+    _ = step()  # warm-up (autotuner, lazy allocations) outside the capture
+    torch.cuda.synchronize()
+    st0 = rng.state_dict()
+    eager = [step().item() for _ in range(3)]
+    rng.load_state_dict(st0)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()  # side-stream warm-up required before capture
+    torch.cuda.current_stream().wait_stream(s)
+    rng.load_state_dict(st0)
+    with torch.cuda.graph(g):
+        out = step()
+    rng.load_state_dict(st0)  # the capture did not run the kernels, but reset anyway
+    replays = []
+    for _ in range(3):
+        g.replay()
+        replays.append(out.item())
+    assert len(set(replays)) == 3, "each replay must draw new dropout masks"
+    assert replays == eager, (replays, eager)
