@@ -621,8 +621,8 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
     const int nblk = (Tq + 63) / 64;
     if (want_bg) {
         CHECK_BF16(*qkv_bias_grad);
-        TORCH_CHECK(qkv_bias_grad->numel() == 3L * H * D && qkv_bias_grad->is_contiguous() && D == 64 && Tq == Tk,
-                    "qkv bias gradient: packed self-attention with head_dim 64 only");
+        TORCH_CHECK(qkv_bias_grad->numel() == 3L * H * D && qkv_bias_grad->is_contiguous() && rn_attn_is_fast(D) &&
+                    Tq == Tk, "qkv bias gradient: packed self-attention with head_dim 32, 64 or 128 only");
         bsum = at::empty({(int64_t)B * nblk, 3L * H * D}, q.options().dtype(at::kFloat));
     }
     int rc = rn_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),

@@ -4,7 +4,8 @@
 // (q, k, v are usually views into one packed QKV GEMM output).  LSE is saved as
 // [B][H][Tq] fp32 (natural log).
 //
-// Fast path D = 64 (GPT-2 small/medium, ViT-B/16), all v_mfma_f32_16x16x32_bf16:
+// MFMA path, head size D ∈ {32, 64, 128} (D = 64: GPT-2 small/medium, ViT-B/16; 32 / 128: the
+// reference blocks' E // n_heads at e.g. 256/8 and 512/4), all v_mfma_f32_16x16x32_bf16:
 //   * every product is arranged so that the softmax row index (the query for
 //     fwd / dQ, the key for dK/dV) sits on lane&15 and the reduced index sits in
 //     accumulator registers: the accumulator tile is then directly the next
@@ -13,18 +14,19 @@
 //     operands ({4g..4g+3} ∪ {16+4g..16+4g+3} for lane group g);
 //   * the other operand of those products is a column slice of a row-major LDS
 //     tile, read with ds_read_b64_tr_b16 (hardware transpose);
-//   * LDS tiles are [64 rows][64 bf16] (128-B rows) staged by LDS-DMA
-//     (buffer_load … lds) with the 16-B chunk XOR swizzle c ^ (((r>>1)&3)<<1),
-//     which is conflict-free for BOTH the ds_read_b128 row reads and the
-//     transposed reads (one image serves both);
+//   * LDS tiles are [64 rows][D bf16] staged by LDS-DMA (buffer_load … lds) with a
+//     per-D 16-B chunk XOR swizzle (swz<D>) that is conflict-free for BOTH the
+//     ds_read_b128 row reads and the transposed reads (one image serves both);
 //   * online softmax in exp2 domain; causal tiles above the diagonal are
 //     skipped, diagonal tiles masked; heaviest causal blocks launch first;
 //   * dropout on P by a stateless counter hash, regenerated in the backward;
 //   * backward = dQ kernel (one workgroup per 64 queries, loops over keys; also
 //     emits delta = rowsum(dO·O) from registers) + dK/dV kernel (one workgroup
 //     per 64 keys, loops over queries): no atomics, bitwise deterministic.
-// Generic path (any D ≤ 256, used by the reference-parity blocks with small
-// head sizes): straightforward per-query-row kernels with fp32 scores in LDS.
+// D = 64 has extra tuned variants (split-loop forward with MFMA row sums, two query / key
+// groups per wave in the backward); D = 32 / 128 use the single-loop forward and one group.
+// Generic path (odd head sizes ≤ 256 only): per-query-row kernels with fp32 scores in LDS
+// and fp32 atomics for dK/dV (not bitwise deterministic).
 #include "common.h"
 
 #include <cstdlib>
@@ -59,24 +61,42 @@ struct AttnArgs {
     int lse_log2;
 };
 
-// Sum a wave-tile's [16 rows][64 cols] accumulator (lane holds row lane&15, cols 16jd+4g+r)
+// LDS tile geometry for head size D ∈ {32, 64, 128}: [64 rows][D bf16] = RB-byte rows, 16-B chunks
+// XOR-swizzled per row.  Each swizzle is a permutation of the row's chunks that (a) makes the
+// 16 rows of a ds_read_b128 row fragment (same logical chunk) land in 16 distinct 16-B bank slots
+// and (b) keeps the 32-B chunk pairs of a ds_read_b64_tr_b16 column fragment (8 rows per pass) in
+// 8 distinct 32-B slots; all three repeat with period 16 in the row, which FragOff relies on.
+//   D = 64  (128-B rows, 2 per bank line): c ^ (((r>>1)&3)<<1)
+//   D = 128 (256-B rows):                  c ^ (((r&7)<<1) | ((r>>3)&1))
+//   D = 32  (64-B rows, 4 per bank line):  c ^ ((((r>>2)&1)<<1) | ((r>>3)&1))
+template <int D = 64>
+RN_DEV int swz(int r) {
+    if constexpr (D == 64) return ((r >> 1) & 3) << 1;
+    else if constexpr (D == 128) return ((r & 7) << 1) | ((r >> 3) & 1);
+    else return (((r >> 2) & 1) << 1) | ((r >> 3) & 1);
+}
+template <int D> constexpr int kRB = 2 * D;        // bytes per tile row
+template <int D> constexpr int kTB = 64 * 2 * D;   // bytes per 64-row tile
+template <int D> constexpr int kNS = D / 32;       // 32-wide k-steps over the head dim
+template <int D> constexpr int kNJ = D / 16;       // 16-wide output column blocks over the head dim
+
+// Sum a wave-tile's [16 rows][D cols] accumulator (lane holds row lane&15, cols 16jd+4g+r)
 // over the 64 rows of the 4 waves via LDS and write one partial row: out[col].
-RN_DEV void block_colsum64(const f32x4 (&acc)[4], float mul, float* lds, float* out, int wave, int lane) {
+template <int D = 64>
+RN_DEV void block_colsum64(const f32x4 (&acc)[kNJ<D>], float mul, float* lds, float* out, int wave, int lane) {
     const int g = lane >> 4, c = lane & 15;
     __syncthreads();  // LDS tiles no longer read by any wave
 #pragma unroll
-    for (int jd = 0; jd < 4; ++jd)
+    for (int jd = 0; jd < kNJ<D>; ++jd)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) lds[(wave * 16 + c) * 65 + jd * 16 + 4 * g + r] = acc[jd][r] * mul;
+        for (int r = 0; r < 4; ++r) lds[(wave * 16 + c) * (D + 1) + jd * 16 + 4 * g + r] = acc[jd][r] * mul;
     __syncthreads();
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < D) {
         float t = 0.f;
-        for (int row = 0; row < 64; ++row) t += lds[row * 65 + threadIdx.x];
+        for (int row = 0; row < 64; ++row) t += lds[row * (D + 1) + threadIdx.x];
         out[threadIdx.x] = t;
     }
 }
-
-RN_DEV int swz(int r) { return ((r >> 1) & 3) << 1; }
 
 RN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
     const uint64_t bp = (uint64_t)base;
@@ -85,34 +105,21 @@ RN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
 }
 
-// Stage rows [r0, r0+64) (valid < rlim) of a [T][stride] bf16 matrix (64 cols at `base`)
-// into a swizzled 8 KiB LDS tile.  8 DMA instructions; each of the 4 waves issues 2.
-RN_DEV void stage64(const bf16* base, long st, int r0, int rlim, char* lds, int wave, int lane) {
-    __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int ins = wave * 2 + i;
-        const int r = ins * 8 + (lane >> 3);
-        const int cg = (lane & 7) ^ swz(r);
-        const bool ok = (r0 + r) < rlim;
-        const uint32_t voff = ok ? (uint32_t)((((long)(r0 + r)) * st + cg * 8) * 2) : 0xFFFFFFF0u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
-    }
-}
-
 // row fragment: 8 bf16 of row `row`, columns 32*s + 8*(lane>>4) .. +7
+template <int D = 64>
 RN_DEV s16x8 rowfrag(const char* t, int row, int s, int lane) {
     const int chunk = s * 4 + (lane >> 4);
-    return *reinterpret_cast<const s16x8*>(t + row * 128 + ((chunk ^ swz(row)) << 4));
+    return *reinterpret_cast<const s16x8*>(t + row * kRB<D> + ((chunk ^ swz<D>(row)) << 4));
 }
 
 // column fragment: column c0 + (lane&15), rows {rb + 4g + 0..3} ∪ {rb + 16 + 4g + 0..3}
+template <int D = 64>
 RN_DEV s16x8 colfrag(const char* t, int rb, int c0, int lane) {
     const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
     const int ch = (c0 >> 3) + (p >> 1);
     const int r0 = rb + 4 * g + qq, r1 = r0 + 16;
-    const char* a0 = t + r0 * 128 + ((ch ^ swz(r0)) << 4) + (p & 1) * 8;
-    const char* a1 = t + r1 * 128 + ((ch ^ swz(r1)) << 4) + (p & 1) * 8;
+    const char* a0 = t + r0 * kRB<D> + ((ch ^ swz<D>(r0)) << 4) + (p & 1) * 8;
+    const char* a1 = t + r1 * kRB<D> + ((ch ^ swz<D>(r1)) << 4) + (p & 1) * 8;
     s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
     s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
     s16x8 r;
@@ -125,32 +132,37 @@ RN_DEV s16x8 colfrag(const char* t, int rb, int c0, int lane) {
 // site reads row X*16 + (lane&15) (rowfrag) or rows 32*ks + … / columns 16*jd + … (colfrag) with
 // X, ks, jd compile-time: the XOR swizzle then depends on the lane only, so the address is
 // base + per-lane offset + an immediate, instead of ~50 recomputed VALU address ops per tile.
-struct FragOff {
-    uint32_t rf[2];  // rowfrag, k-step s
-    uint32_t cf[4];  // colfrag, column block jd
+template <int D = 64>
+struct FragOffT {
+    uint32_t rf[kNS<D>];  // rowfrag, k-step s
+    uint32_t cf[kNJ<D>];  // colfrag, column block jd
 };
-RN_DEV FragOff make_fragoff(int lane) {
-    FragOff f;
+using FragOff = FragOffT<64>;
+template <int D = 64>
+RN_DEV FragOffT<D> make_fragoff(int lane) {
+    FragOffT<D> f;
     const int g = lane >> 4, c = lane & 15;
-    const int swc = swz(c);
+    const int swc = swz<D>(c);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) f.rf[s] = c * 128 + ((((4 * s) + g) ^ swc) << 4);
+    for (int s = 0; s < kNS<D>; ++s) f.rf[s] = c * kRB<D> + ((((4 * s) + g) ^ swc) << 4);
     const int qq = c >> 2, pp = c & 3;
     const int r0 = 4 * g + qq;
-    const int swr = swz(r0);
+    const int swr = swz<D>(r0);
 #pragma unroll
-    for (int jd = 0; jd < 4; ++jd) f.cf[jd] = r0 * 128 + (((2 * jd + (pp >> 1)) ^ swr) << 4) + (pp & 1) * 8;
+    for (int jd = 0; jd < kNJ<D>; ++jd) f.cf[jd] = r0 * kRB<D> + (((2 * jd + (pp >> 1)) ^ swr) << 4) + (pp & 1) * 8;
     return f;
 }
-// == rowfrag(t, X * 16 + (lane & 15), s, lane)
-RN_DEV s16x8 rowfragx(const char* t, int X, int s, const FragOff& f) {
-    return *reinterpret_cast<const s16x8*>(t + X * 2048 + f.rf[s]);
+// == rowfrag<D>(t, X * 16 + (lane & 15), s, lane)
+template <int D>
+RN_DEV s16x8 rowfragx(const char* t, int X, int s, const FragOffT<D>& f) {
+    return *reinterpret_cast<const s16x8*>(t + X * 16 * kRB<D> + f.rf[s]);
 }
-// == colfrag(t, 32 * ks, 16 * jd, lane)
-RN_DEV s16x8 colfragx(const char* t, int ks, int jd, const FragOff& f) {
-    const char* a0 = t + ks * 4096 + f.cf[jd];
+// == colfrag<D>(t, 32 * ks, 16 * jd, lane)
+template <int D>
+RN_DEV s16x8 colfragx(const char* t, int ks, int jd, const FragOffT<D>& f) {
+    const char* a0 = t + ks * 32 * kRB<D> + f.cf[jd];
     s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-    s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 2048));
+    s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 16 * kRB<D>));
     s16x8 r;
     r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
     r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
@@ -215,13 +227,17 @@ RN_DEV void dma16_async(const u32x4& rs_, uint32_t voff, uint32_t lds) {
 }
 #pragma clang diagnostic pop
 
-// stage64 with compiler-invisible DMA (2 instructions per wave).
+// Stage rows [r0, r0+64) (valid < rlim) of a [T][stride] bf16 matrix (D cols at the resource's
+// base) into a swizzled LDS tile, by compiler-invisible LDS-DMA: D/8 16-B instructions in all,
+// D/32 per wave; instruction `ins` fills rows ins·(512/D) .. +512/D (1 KiB of LDS).
+template <int D = 64>
 RN_DEV void stage64_async(const u32x4& rs, long st, int r0, int rlim, const char* lds, int wave, int lane) {
+    constexpr int CPR = D / 8, RPI = 64 / CPR;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int ins = wave * 2 + i;
-        const int r = ins * 8 + (lane >> 3);
-        const int cg = (lane & 7) ^ swz(r);
+    for (int i = 0; i < D / 32; ++i) {
+        const int ins = wave * (D / 32) + i;
+        const int r = ins * RPI + lane / CPR;
+        const int cg = (lane % CPR) ^ swz<D>(r);
         const bool ok = (r0 + r) < rlim;
         const uint32_t voff = ok ? (uint32_t)((((long)(r0 + r)) * st + cg * 8) * 2) : 0xFFFFFFF0u;
         dma16_async(rs, voff, lds_addr(lds + ins * 1024));
@@ -245,8 +261,12 @@ RN_DEV float sum4groups(float x) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <bool CAUSAL, bool BIAS, bool DROP>
-__global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
+// D = 32 / 64 / 128 (template); at D = 64 the default for bias / dropout, D = 32 / 128 for everything.
+// QI: 16-query fragments per wave (block = 64·QI queries); 1 at D = 128 to fit the O accumulators.
+// The bias / dropout variants run at occupancy ≤ 2: the per-score loads / hash need the registers.
+template <bool CAUSAL, bool BIAS, bool DROP, int D = 64, int OCC = 3, int QI = 2>
+__global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) attn_fwd64_k(AttnArgs p) {
+    constexpr int NS = kNS<D>, NJ = kNJ<D>, TB = kTB<D>, QBLK = 64 * QI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -255,7 +275,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     const int nqb = gridDim.y;
     const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
     const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-    const int q0 = qb * 128 + wave * 32;
+    const int q0 = qb * QBLK + wave * 16 * QI;
     const int off = p.Tk - p.Tq;  // causal: key j visible to query i iff j <= i + off
     const float sl2 = p.scale * LOG2E;
     const float xs = BIAS ? 1.f : sl2;  // units of the running max m: log2-scaled with bias, raw without
@@ -265,33 +285,38 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
 
     int kv_end = p.Tk;
-    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    if (CAUSAL) kv_end = min(p.Tk, qb * QBLK + QBLK + off);
     const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
-#define Kt(i) (smem + (i) * 16384)
-#define Vt(i) (smem + 8192 + (i) * 16384)
+#define Kt(i) (smem + (i) * 2 * TB)
+#define Vt(i) (smem + TB + (i) * 2 * TB)
     if (nkv > 0) {  // first tile in flight while Q is loaded
-        stage64_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
-        stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+        stage64_async<D>(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64_async<D>(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
 
-    s16x8 qf[2][2];
+    s16x8 qf[QI][NS];
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi)
+    for (int qi = 0; qi < QI; ++qi)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int row = q0 + qi * 16 + c;
             qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
         }
     // Re-define qf through an (empty) asm so the compiler's wait for these loads happens
     // here, once: otherwise it re-waits vmcnt(0) inside the loop at their first use,
     // which would also drain the in-flight K/V prefetch.
-    asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]));
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-    f32x4 oacc[2][4];
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi)
+    for (int qi = 0; qi < QI; ++qi)
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(qf[qi][s]));
+    float m[QI], l[QI];
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) { m[qi] = -INFINITY; l[qi] = 0.f; }
+    f32x4 oacc[QI][NJ];
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi)
+#pragma unroll
+        for (int jd = 0; jd < NJ; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
@@ -300,29 +325,31 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
         __syncthreads(); // ... and every wave's; every wave also finished tile t-1 (its buffer is free)
         const int cur = t & 1;
         if (t + 1 < nkv) {
-            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
-            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
+            stage64_async<D>(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(cur ^ 1), wave, lane);
+            stage64_async<D>(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(cur ^ 1), wave, lane);
         }
         const int kv0 = t * 64;
         // wave-uniform skip: this wave's queries all precede the tile
-        if (CAUSAL && kv0 > q0 + 31 + off) continue;
+        if (CAUSAL && kv0 > q0 + 16 * QI - 1 + off) continue;
         const char* kt = Kt(cur);
         const char* vt = Vt(cur);
-        f32x4 sacc[2][4];
+        f32x4 sacc[QI][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            s16x8 a0 = rowfrag(kt, j * 16 + c, 0, lane);
-            s16x8 a1 = rowfrag(kt, j * 16 + c, 1, lane);
+            s16x8 a[NS];
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) {
+            for (int s = 0; s < NS; ++s) a[s] = rowfrag<D>(kt, j * 16 + c, s, lane);
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) {
                 f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                z = MFMA(a0, qf[qi][0], z, 0, 0, 0);
-                sacc[qi][j] = MFMA(a1, qf[qi][1], z, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) z = MFMA(a[s], qf[qi][s], z, 0, 0, 0);
+                sacc[qi][j] = z;
             }
         }
         if constexpr (BIAS) {  // x = s·scale·log2e + bias·log2e
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) {
+            for (int qi = 0; qi < QI; ++qi) {
                 const int qg = q0 + qi * 16 + c;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -348,7 +375,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
         if ((kv0 + 64 > p.Tk) || (CAUSAL && kv0 + 63 > q0 + off)) {
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) {
+            for (int qi = 0; qi < QI; ++qi) {
                 const int qg = q0 + qi * 16 + c;
                 const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
 #pragma unroll
@@ -359,7 +386,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
             }
         }
 #pragma unroll
-        for (int qi = 0; qi < 2; ++qi) {
+        for (int qi = 0; qi < QI; ++qi) {
             const int qg = q0 + qi * 16 + c;
             float tmax = -INFINITY;
 #pragma unroll
@@ -387,19 +414,19 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
                 }
             l[qi] = l[qi] * alpha + ls;
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alpha;
+            for (int jd = 0; jd < NJ; ++jd) oacc[qi][jd] *= alpha;
         }
         // O^T[d][q] += V^T[d][kv] * P^T[kv][q]
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            s16x8 pb[2];
+            s16x8 pb[QI];
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
+            for (int qi = 0; qi < QI; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
-                s16x8 a = colfrag(vt, 32 * s, 16 * jd, lane);
+            for (int jd = 0; jd < NJ; ++jd) {
+                s16x8 a = colfrag<D>(vt, 32 * s, 16 * jd, lane);
 #pragma unroll
-                for (int qi = 0; qi < 2; ++qi) oacc[qi][jd] = MFMA(a, pb[qi], oacc[qi][jd], 0, 0, 0);
+                for (int qi = 0; qi < QI; ++qi) oacc[qi][jd] = MFMA(a, pb[qi], oacc[qi][jd], 0, 0, 0);
             }
         }
     }
@@ -408,13 +435,13 @@ __global__ void __launch_bounds__(256, 3) attn_fwd64_k(AttnArgs p) {
     // epilogue
     bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
+    for (int qi = 0; qi < QI; ++qi) {
         const float lt = sum4groups(l[qi]);
         const int qg = q0 + qi * 16 + c;
         const float inv = lt > 0.f ? 1.f / lt : 0.f;
         if (qg < p.Tq) {
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
+            for (int jd = 0; jd < NJ; ++jd) {
                 bf16x4 o4 = {(bf16)(oacc[qi][jd][0] * inv), (bf16)(oacc[qi][jd][1] * inv),
                              (bf16)(oacc[qi][jd][2] * inv), (bf16)(oacc[qi][jd][3] * inv)};
                 *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
@@ -663,12 +690,13 @@ __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
 // dK, dV: grid (B*H, ceil(Tk/(64·KG))); key group u (< KG) of wave w owns keys
 // kb·64·KG + 64·u + 16w + (lane&15).  KG = 2: every Q / dO fragment read from LDS feeds both key
 // groups' MFMAs and each wave carries two independent S → P → dS chains (as in the dQ kernel).
-template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 3, int KG = 1>
-__global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
+template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 3, int KG = 1, int D = 64>
+__global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) attn_bwd_dkdv64_k(AttnArgs p) {
+    constexpr int NS = kNS<D>, NJ = kNJ<D>, TB = kTB<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const FragOff fo = make_fragoff(lane);
+    const FragOffT<D> fo = make_fragoff<D>(lane);
     constexpr int KB = 64 * KG;  // keys per block
     // grid (B*H, key blocks): low key blocks see the most queries under causal and, with the block
     // index varying slowest, launch first across ALL heads (longest-first)
@@ -692,14 +720,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     int qt0 = 0;
     if (CAUSAL) qt0 = max(0, (kb * KB - off)) / 64;
     const int nqt = (p.Tq + 63) / 64;
-    // buffer i: Q tile [0, 8K), dO tile [8K, 16K), lse [16K, 17K), delta [17K, 18K)
-#define Qt(i) (smem + (i) * 18432)
-#define Ot(i) (smem + 8192 + (i) * 18432)
-#define Lt(i) (smem + 16384 + (i) * 18432)
-#define Dt(i) (smem + 17408 + (i) * 18432)
+    // buffer i: Q tile [0, TB), dO tile [TB, 2TB), lse [2TB, 2TB + 1K), delta [2TB + 1K, 2TB + 2K)
+#define Qt(i) (smem + (i) * (2 * TB + 2048))
+#define Ot(i) (smem + TB + (i) * (2 * TB + 2048))
+#define Lt(i) (smem + 2 * TB + (i) * (2 * TB + 2048))
+#define Dt(i) (smem + 2 * TB + 1024 + (i) * (2 * TB + 2048))
     auto stage = [&](int qt, int buf) {
-        stage64_async(qrs, p.q_st, qt * 64, p.Tq, Qt(buf), wave, lane);
-        stage64_async(ors, p.do_st, qt * 64, p.Tq, Ot(buf), wave, lane);
+        stage64_async<D>(qrs, p.q_st, qt * 64, p.Tq, Qt(buf), wave, lane);
+        stage64_async<D>(ors, p.do_st, qt * 64, p.Tq, Ot(buf), wave, lane);
         if (wave < 2) {  // lanes 0-15 carry 64 floats; the rest land as zeros past them
             const int r = qt * 64 + lane * 4;
             const uint32_t voff = (lane < 16 && r < p.Tq) ? (uint32_t)(r * 4) : 0xFFFFFFF0u;
@@ -708,21 +736,22 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
     };
     if (qt0 < nqt) stage(qt0, 0);
 
-    s16x8 kf[KG][2], vf[KG][2];
+    s16x8 kf[KG][NS], vf[KG][NS];
 #pragma unroll
     for (int u = 0; u < KG; ++u) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             kf[u][s] = gload16(kbase + (long)kvl[u] * p.k_st + s * 32 + g * 8, kvl[u] < p.Tk);
             vf[u][s] = gload16(vbase + (long)kvl[u] * p.v_st + s * 32 + g * 8, kvl[u] < p.Tk);
         }
-        asm volatile("" : "+v"(kf[u][0]), "+v"(kf[u][1]), "+v"(vf[u][0]), "+v"(vf[u][1]));  // wait here, not in the loop
+#pragma unroll
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(kf[u][s]), "+v"(vf[u][s]));  // wait here, not in the loop
     }
-    f32x4 dvacc[KG][4], dkacc[KG][4];
+    f32x4 dvacc[KG][NJ], dkacc[KG][NJ];
 #pragma unroll
     for (int u = 0; u < KG; ++u)
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) { dvacc[u][jd] = (f32x4){0, 0, 0, 0}; dkacc[u][jd] = (f32x4){0, 0, 0, 0}; }
+        for (int jd = 0; jd < NJ; ++jd) { dvacc[u][jd] = (f32x4){0, 0, 0, 0}; dkacc[u][jd] = (f32x4){0, 0, 0, 0}; }
 
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
@@ -748,8 +777,12 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
         f32x4 pq[KG][4], dsq[KG][4];
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
-            const s16x8 a0 = rowfragx(qt_, qi, 0, fo), a1 = rowfragx(qt_, qi, 1, fo);
-            const s16x8 o0 = rowfragx(ot_, qi, 0, fo), o1 = rowfragx(ot_, qi, 1, fo);
+            s16x8 af[NS], of[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                af[s] = rowfragx(qt_, qi, s, fo);
+                of[s] = rowfragx(ot_, qi, s, fo);
+            }
             // lane holds S[q = q0 + 16qi + 4g + r][kv]
             const int ql = qi * 16 + 4 * g;
             const float4 l4 = *reinterpret_cast<const float4*>(lt_ + ql);
@@ -758,10 +791,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
 #pragma unroll
             for (int u = 0; u < KG; ++u) {
                 f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
-                sa = MFMA(a0, kf[u][0], sa, 0, 0, 0);
-                sa = MFMA(a1, kf[u][1], sa, 0, 0, 0);
-                da = MFMA(o0, vf[u][0], da, 0, 0, 0);
-                da = MFMA(o1, vf[u][1], da, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) sa = MFMA(af[s], kf[u][s], sa, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) da = MFMA(of[s], vf[u][s], da, 0, 0, 0);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int qg = q0 + ql + r;
@@ -807,7 +840,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
                 sb[u] = pack_p(dsq[u][2 * ks], dsq[u][2 * ks + 1]);
             }
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
+            for (int jd = 0; jd < NJ; ++jd) {
                 const s16x8 ao = colfragx(ot_, ks, jd, fo);
 #pragma unroll
                 for (int u = 0; u < KG; ++u) dvacc[u][jd] = MFMA(ao, pb[u], dvacc[u][jd], 0, 0, 0);
@@ -846,14 +879,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
 #undef Lt
 #undef Dt
     if (p.bsum) {  // dK / dV column partials for the QKV bias gradient; row = (b, 64-key block)
-        const int E = p.H * 64, nb64 = (p.Tk + 63) / 64;
+        const int E = p.H * D, nb64 = (p.Tk + 63) / 64;
 #pragma unroll
         for (int u = 0; u < KG; ++u) {
             const int blk = kb * KG + u;
             if (blk < nb64) {  // block-uniform
-                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * 64;
-                block_colsum64(dkacc[u], p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
-                block_colsum64(dvacc[u], 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
+                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * D;
+                block_colsum64<D>(dkacc[u], p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
+                block_colsum64<D>(dvacc[u], 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
             }
         }
     }
@@ -863,7 +896,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
             bf16* dkp = p.dk + b * p.dk_sb + (long)kvl[u] * p.dk_st + h * p.dk_sh;
             bf16* dvp = p.dv + b * p.dv_sb + (long)kvl[u] * p.dv_st + h * p.dv_sh;
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
+            for (int jd = 0; jd < NJ; ++jd) {
                 bf16x4 k4 = {(bf16)(dkacc[u][jd][0] * p.scale), (bf16)(dkacc[u][jd][1] * p.scale),
                              (bf16)(dkacc[u][jd][2] * p.scale), (bf16)(dkacc[u][jd][3] * p.scale)};
                 bf16x4 v4 = {(bf16)dvacc[u][jd][0], (bf16)dvacc[u][jd][1], (bf16)dvacc[u][jd][2],
@@ -879,12 +912,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64_k(AttnArgs p) {
 // qb·64·QG + 64·qg + 16w + (lane&15).  With QG = 2 every K / V fragment read from LDS feeds
 // the MFMAs of two query groups (half the LDS reads per MFMA) and each wave carries two
 // independent dependency chains (S → P → dS → dQ) for the scheduler to interleave.
-template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 2, int QG = 1>
+template <bool CAUSAL, bool BIAS, bool DROP, int OCC = 2, int QG = 1, int D = 64>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
+    constexpr int NS = kNS<D>, NJ = kNJ<D>, TB = kTB<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const FragOff fo = make_fragoff(lane);
+    const FragOffT<D> fo = make_fragoff<D>(lane);
     constexpr int QB = 64 * QG;  // queries per block
     const int nqb = gridDim.y;  // grid (B*H, query blocks): heaviest blocks of every head first
     const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
@@ -899,14 +933,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
     int qgl[QG];
     bool qok[QG];
-    s16x8 qf[QG][2], df[QG][2];
+    s16x8 qf[QG][NS], df[QG][NS];
     float lse2[QG], dl[QG];
 #pragma unroll
     for (int u = 0; u < QG; ++u) {
         qgl[u] = qb * QB + 64 * u + wave * 16 + c;
         qok[u] = qgl[u] < p.Tq;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             qf[u][s] = gload16(qbase + (long)qgl[u] * p.q_st + s * 32 + g * 8, qok[u]);
             df[u][s] = gload16(dobase + (long)qgl[u] * p.do_st + s * 32 + g * 8, qok[u]);
         }
@@ -916,7 +950,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         const bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
         float part = 0.f;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             s16x8 of = gload16(obase + (long)qgl[u] * p.o_st + s * 32 + g * 8, qok[u]);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
@@ -924,22 +958,24 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         }
         dl[u] = sum4groups(part);
         if (qok[u] && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qgl[u]] = dl[u];
-        asm volatile("" : "+v"(qf[u][0]), "+v"(qf[u][1]), "+v"(df[u][0]), "+v"(df[u][1]), "+v"(dl[u]));  // loads retired here
+#pragma unroll
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(qf[u][s]), "+v"(df[u][s]));
+        asm volatile("" : "+v"(dl[u]));  // loads retired here
     }
-    f32x4 dqacc[QG][4];
+    f32x4 dqacc[QG][NJ];
 #pragma unroll
     for (int u = 0; u < QG; ++u)
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) dqacc[u][jd] = (f32x4){0, 0, 0, 0};
+        for (int jd = 0; jd < NJ; ++jd) dqacc[u][jd] = (f32x4){0, 0, 0, 0};
 
     int kv_end = p.Tk;
     if (CAUSAL) kv_end = min(p.Tk, qb * QB + QB + off);
     const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
-#define Kt(i) (smem + (i) * 16384)
-#define Vt(i) (smem + 8192 + (i) * 16384)
+#define Kt(i) (smem + (i) * 2 * TB)
+#define Vt(i) (smem + TB + (i) * 2 * TB)
     if (nkv > 0) {
-        stage64_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
-        stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+        stage64_async<D>(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage64_async<D>(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
     const float rd = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
     if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
@@ -951,8 +987,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         vm_wait_all();
         __syncthreads();
         if (t + 1 < nkv) {
-            stage64_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt((t & 1) ^ 1), wave, lane);
-            stage64_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
+            stage64_async<D>(krs, p.k_st, (t + 1) * 64, p.Tk, Kt((t & 1) ^ 1), wave, lane);
+            stage64_async<D>(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
         }
     };
     auto body = [&](int t, auto masked_c, auto buf_c) {
@@ -964,15 +1000,19 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         f32x4 dsv[QG][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const s16x8 k0 = rowfragx(kt, j, 0, fo), k1 = rowfragx(kt, j, 1, fo);
-            const s16x8 v0 = rowfragx(vt, j, 0, fo), v1 = rowfragx(vt, j, 1, fo);
+            s16x8 kr[NS], vr[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                kr[s] = rowfragx(kt, j, s, fo);
+                vr[s] = rowfragx(vt, j, s, fo);
+            }
 #pragma unroll
             for (int u = 0; u < QG; ++u) {
                 f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
-                sa = MFMA(k0, qf[u][0], sa, 0, 0, 0);
-                sa = MFMA(k1, qf[u][1], sa, 0, 0, 0);
-                da = MFMA(v0, df[u][0], da, 0, 0, 0);
-                da = MFMA(v1, df[u][1], da, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) sa = MFMA(kr[s], qf[u][s], sa, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) da = MFMA(vr[s], df[u][s], da, 0, 0, 0);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int kvj = kv0 + j * 16 + 4 * g + r;
@@ -1009,7 +1049,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
 #pragma unroll
             for (int u = 0; u < QG; ++u) sb[u] = pack_p(dsv[u][2 * ks], dsv[u][2 * ks + 1]);
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
+            for (int jd = 0; jd < NJ; ++jd) {
                 const s16x8 kc = colfragx(kt, ks, jd, fo);
 #pragma unroll
                 for (int u = 0; u < QG; ++u) dqacc[u][jd] = MFMA(kc, sb[u], dqacc[u][jd], 0, 0, 0);
@@ -1042,13 +1082,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
 #undef Kt
 #undef Vt
     if (p.bsum) {  // dQ column partials; row = (b, 64-query block) — the dK/dV kernel's row layout
-        const int E = p.H * 64, nb64 = (p.Tq + 63) / 64;
+        const int E = p.H * D, nb64 = (p.Tq + 63) / 64;
 #pragma unroll
         for (int u = 0; u < QG; ++u) {
             const int blk = qb * QG + u;
             if (blk < nb64) {  // block-uniform
-                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * 64;
-                block_colsum64(dqacc[u], p.scale, reinterpret_cast<float*>(smem), row, wave, lane);
+                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * D;
+                block_colsum64<D>(dqacc[u], p.scale, reinterpret_cast<float*>(smem), row, wave, lane);
             }
         }
     }
@@ -1057,7 +1097,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         if (qok[u]) {
             bf16* dqp = p.dq + b * p.dq_sb + (long)qgl[u] * p.dq_st + h * p.dq_sh;
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
+            for (int jd = 0; jd < NJ; ++jd) {
                 bf16x4 q4 = {(bf16)(dqacc[u][jd][0] * p.scale), (bf16)(dqacc[u][jd][1] * p.scale),
                              (bf16)(dqacc[u][jd][2] * p.scale), (bf16)(dqacc[u][jd][3] * p.scale)};
                 *reinterpret_cast<bf16x4*>(dqp + jd * 16 + 4 * g) = q4;
@@ -1198,6 +1238,38 @@ __global__ void scatter_kv_k(AttnArgs p) {
         }                                                                                              \
     } while (0)
 
+// RN_DISPATCH3 with trailing template arguments after <CAUSAL, BIAS, DROP>; kernels above 64 KiB of
+// dynamic LDS are opted in on every launch (D = 128 only; the call is a host-side attribute write)
+#define RN_DISPATCH3V(KERN, grid, lds, st, args, ...)                                                 \
+    do {                                                                                               \
+        const bool c_ = args.causal, b_ = args.bias != nullptr, d_ = args.p_drop > 0.f;              \
+        auto k_ = c_ ? (b_ ? (d_ ? KERN<true, true, true, __VA_ARGS__> : KERN<true, true, false, __VA_ARGS__>)      \
+                           : (d_ ? KERN<true, false, true, __VA_ARGS__> : KERN<true, false, false, __VA_ARGS__>))    \
+                     : (b_ ? (d_ ? KERN<false, true, true, __VA_ARGS__> : KERN<false, true, false, __VA_ARGS__>)    \
+                           : (d_ ? KERN<false, false, true, __VA_ARGS__> : KERN<false, false, false, __VA_ARGS__>)); \
+        if ((lds) > 65536) (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize, (lds)); \
+        k_<<<grid, 256, lds, st>>>(args);                                                              \
+    } while (0)
+
+// MFMA path for head sizes 32 / 128 (one kernel family, templated on D): forward = the bias/dropout
+// capable single-loop kernel, backward = dQ (+delta) then dK/dV, one 64-row group per wave.
+template <int D>
+void attn_fwd_mfma(AttnArgs& a, hipStream_t st) {
+    constexpr int QBLK = D == 128 ? 64 : 128;
+    dim3 grid(a.B * a.H, (a.Tq + QBLK - 1) / QBLK);
+    RN_DISPATCH3V(attn_fwd64_k, grid, 4 * kTB<D>, st, a, D, (D == 128 ? 2 : 3), (D == 128 ? 1 : 2));
+}
+template <int D>
+void attn_bwd_mfma(AttnArgs& a, hipStream_t st) {
+    dim3 g2(a.B * a.H, (a.Tq + 63) / 64);
+    dim3 g1(a.B * a.H, (a.Tk + 63) / 64);
+    RN_DISPATCH3V(attn_bwd_dq64_k, g2, 4 * kTB<D>, st, a, 2, 1, D);
+    RN_DISPATCH3V(attn_bwd_dkdv64_k, g1, 2 * (2 * kTB<D> + 2048), st, a, (D == 128 ? 1 : 3), 1, D);
+}
+
+// the MFMA kernels' requirements: D ∈ {32, 64, 128} and 16-B aligned rows (strides in elements)
+bool mfma_head(int D) { return D == 32 || D == 64 || D == 128; }
+
 }  // namespace
 
 extern "C" {
@@ -1215,8 +1287,11 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     a.o_sb = strides[9]; a.o_st = strides[10]; a.o_sh = strides[11];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
     a.scale = scale; a.p_drop = p_drop; a.seed = seed;
-    const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
-    if (fast) {
+    const bool fast = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
+    if (fast && D != 64) {
+        if (D == 32) attn_fwd_mfma<32>(a, st);
+        else attn_fwd_mfma<128>(a, st);
+    } else if (fast) {
         dim3 grid(B * H, (Tq + 127) / 128);
         // REPLICANN_ATTN_FWD=1 selects the original single-loop kernel, 2 the split-loop v2, 3 (default)
         // v2 with the LEAN softmax bookkeeping (read per call so one process can A/B them); no bias /
@@ -1256,14 +1331,17 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     a.dk_sb = s[18]; a.dk_st = s[19]; a.dk_sh = s[20]; a.dv_sb = s[21]; a.dv_st = s[22]; a.dv_sh = s[23];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
     a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.dk32 = dk32; a.dv32 = dv32; a.bsum = bsum;
-    const bool fast = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) &&
+    const bool fast = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) &&
                       (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
                       (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
     if (bsum && !(fast && Tq == Tk)) return -2;  // bias partials: fast self-attention path only
     // the forward chose its path with its own stride test: lse is base 2 iff that one was fast
-    a.lse_log2 = (D == 64) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
+    a.lse_log2 = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast && !a.lse_log2) return -1;  // cannot happen (the backward test is stricter); never mix units
-    if (fast) {
+    if (fast && D != 64) {
+        if (D == 32) attn_bwd_mfma<32>(a, st);
+        else attn_bwd_mfma<128>(a, st);
+    } else if (fast) {
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2(B * H, (Tq + 63) / 64);
         dim3 g1(B * H, (Tk + 63) / 64);
@@ -1299,6 +1377,6 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     return 0;
 }
 
-int rn_attn_is_fast(int D) { return D == 64; }
+int rn_attn_is_fast(int D) { return mfma_head(D); }
 
 }  // extern "C"

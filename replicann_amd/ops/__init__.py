@@ -2,7 +2,7 @@
 CPU tensors → plain ATen with the same math.  No other backends."""
 
 from .activation import dropout, gelu, relu, softmax
-from .attention import attention, attention_packed, attention_reference, mask_to_bias
+from .attention import attention, attention_is_mfma, attention_packed, attention_reference, mask_to_bias
 from .conv import conv2d_nhwc
 from .embedding import embedding
 from .fp8 import Fp8State, dequantize_fp8, linear_fp8, quantize_fp8
@@ -12,7 +12,7 @@ from .norm import batch_norm_nhwc, layer_norm
 from .pool import avgpool_nhwc, maxpool_nhwc
 
 __all__ = [
-    "attention", "attention_packed", "attention_reference", "mask_to_bias", "avgpool_nhwc",
+    "attention", "attention_is_mfma", "attention_packed", "attention_reference", "mask_to_bias", "avgpool_nhwc",
     "batch_norm_nhwc", "conv2d_nhwc", "cross_entropy", "dropout", "embedding", "gelu", "gemm",
     "layer_norm", "linear", "mlp", "linear_cross_entropy", "linear_fp8", "Fp8State", "quantize_fp8", "dequantize_fp8", "maxpool_nhwc", "relu", "softmax", "ACT_GELU", "ACT_NONE", "ACT_RELU",
 ]

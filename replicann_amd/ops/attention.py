@@ -27,6 +27,15 @@ import torch
 from .. import _ext
 
 
+MFMA_HEAD_DIMS = (32, 64, 128)
+
+
+def attention_is_mfma(head_dim: int) -> bool:
+    """True if ``head_dim`` runs on the MFMA flash kernels (deterministic, no atomics); other head
+    sizes take the generic per-query-row kernels (fp32 atomics in the backward)."""
+    return int(head_dim) in MFMA_HEAD_DIMS
+
+
 def mask_to_bias(mask, dtype=torch.float32):
     """Reference mask semantics → additive bias.
 
@@ -131,7 +140,7 @@ class _AttnPackedFn(torch.autograd.Function):
         dq, dk, dv = dqkv.unbind(2)
         pb = ctx.producer_bias
         B, T, _, H, D = qkv.shape
-        pb_acc = _direct_grad(pb) if (pb is not None and D == 64 and pb.numel() == 3 * H * D) else None
+        pb_acc = _direct_grad(pb) if (pb is not None and attention_is_mfma(D) and pb.numel() == 3 * H * D) else None
         _ext.ops().attn_bwd_out(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
                                 ctx.dropout_p, 0, dq, dk, dv, pb_acc, ctx.seed)
         if pb_acc is not None:  # Σ_rows dQKV reduced in the kernels: the c_attn bias gradient

@@ -9,8 +9,8 @@ int64 device tensor — to the kernel, which reads its seed from there; the back
 same ``out``.  Replaying a captured step therefore draws fresh masks every step, and eager and
 graph runs started from the same state produce identical masks.
 
-The per-device state is seeded from torch's CPU generator (``torch.manual_seed`` governs it) and
-travels in checkpoints (``state_dict`` / ``load_state_dict``).
+The per-device state is seeded by ``manual_seed`` (the Trainer passes its run seed and rank), else
+from torch's CPU generator, and travels in checkpoints (``state_dict`` / ``load_state_dict``).
 """
 
 from __future__ import annotations
@@ -20,13 +20,21 @@ import torch
 from .. import _ext
 
 _STATES: dict[int, torch.Tensor] = {}
+_BASE: list = [None]  # manual_seed() value: streams created later derive from it too
+
+
+def _derive(seed: int, idx: int) -> int:
+    return (int(seed) * 0x9E3779B1 + idx) & ((1 << 62) - 1)
 
 
 def _state(device: torch.device) -> torch.Tensor:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _STATES.get(idx)
     if st is None:
-        seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+        if _BASE[0] is not None:
+            seed = _derive(_BASE[0], idx)
+        else:
+            seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
         st = torch.tensor([seed], dtype=torch.int64, device=torch.device("cuda", idx))
         _STATES[idx] = st
     return st
@@ -39,6 +47,14 @@ def next_seed(device) -> torch.Tensor:
     out = torch.empty(1, dtype=torch.int64, device=st.device)
     _ext.ops().rng_next(st, out)
     return out
+
+
+def state_tensors(device=None) -> list:
+    """The live per-device state tensors (restored in place around graph-capture warm-ups: a
+    captured graph holds their addresses); ``device`` creates that device's stream first."""
+    if device is not None:
+        _state(torch.device(device))
+    return list(_STATES.values())
 
 
 def state_dict() -> dict:
@@ -56,6 +72,8 @@ def load_state_dict(sd: dict) -> None:
 
 
 def manual_seed(seed: int) -> None:
-    """Reset every device stream to a value derived from ``seed`` (tests)."""
+    """Reset every device stream (and any created later) to a value derived from ``seed``
+    (``Trainer`` calls it with the run's seed, so eager and graph runs draw the same masks)."""
+    _BASE[0] = int(seed)
     for i, s in _STATES.items():
-        s.fill_(int(seed) * 0x9E3779B1 + i)
+        s.fill_(_derive(seed, i))

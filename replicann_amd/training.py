@@ -36,6 +36,7 @@ MODEL_KINDS = {
     "vit-b16": "image", "vit-tiny": "image",
     "resnet18": "image", "resnet18-tiny": "image",
     "mlp": "mnist",
+    "refblock-lm": "lm",  # the reference's TransformerDecoder blocks (head dropout 0.1) as a token model
 }
 
 
@@ -58,6 +59,8 @@ def build_model(name, **kw):
         return models.ResNet18(num_classes=10, widths=(16, 32, 64, 128), **kw)
     if name == "mlp":
         return models.MLP(**kw)
+    if name == "refblock-lm":
+        return models.RefBlockLM(**kw)
     raise ValueError(f"unknown model {name!r}; known: {sorted(MODEL_KINDS)}")
 
 
@@ -99,6 +102,9 @@ class Trainer:
             backend="gloo" if cfg.device == "cpu" else None)
         self.device = torch.device(cfg.device) if cfg.device else dev
         torch.manual_seed(cfg.seed)
+        if self.device.type == "cuda":
+            from .ops import rng as dev_rng
+            dev_rng.manual_seed(cfg.seed * 1000 + self.rank)  # device dropout streams (ops/rng.py)
         self.kind = MODEL_KINDS.get(cfg.model, "lm")
         self.model = model if model is not None else build_model(cfg.model, **cfg.model_kwargs)
         dtype = torch.bfloat16 if (cfg.dtype == "bf16" and self.device.type == "cuda") else torch.float32
@@ -228,7 +234,8 @@ class Trainer:
         follows exactly the same step sequence as eager mode."""
         c = self.cfg
         self._static = [tuple(t.clone() for t in next(self.data)) for _ in range(c.grad_accum)]
-        state = self.opt.state_tensors() + [b for b in self.model.buffers()]
+        from .ops import rng as dev_rng
+        state = self.opt.state_tensors() + [b for b in self.model.buffers()] + dev_rng.state_tensors(self.device)
         snap = [t.clone() for t in state]
         count = self.opt.step_count
         s = torch.cuda.Stream()

@@ -40,14 +40,19 @@ def test_gemm_bitwise(cuda, split):
     assert same(a, b)
 
 
-def test_attention_fwd_bwd_bitwise(cuda):
+@pytest.mark.parametrize("D,drop", [(32, 0.0), (64, 0.0), (128, 0.0), (32, 0.1), (64, 0.1), (128, 0.1)])
+def test_attention_fwd_bwd_bitwise(cuda, D, drop):
+    """Every MFMA head size, with and without in-kernel dropout (device seed stream reset per run)."""
+    from replicann_amd.ops import rng
     torch.manual_seed(1)
-    qkv = bf(4, 512, 3, 12, 64).requires_grad_()
-    g = bf(4, 512, 12, 64)
+    H = 768 // D
+    qkv = bf(4, 512, 3, H, D).requires_grad_()
+    g = bf(4, 512, H, D)
 
     def run():
         qkv.grad = None
-        o = ops.attention_packed(qkv, causal=True)
+        rng.manual_seed(5)
+        o = ops.attention_packed(qkv, causal=True, dropout_p=drop, training=drop > 0)
         o.backward(g)
         return o.detach().clone(), qkv.grad.clone()
 

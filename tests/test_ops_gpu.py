@@ -316,7 +316,39 @@ def test_attention_bias_additive(cuda):
     _attn_check(2, T, 2, 64, False, bias=bias)
 
 
-@pytest.mark.parametrize("D", [4, 32, 48])
+@pytest.mark.parametrize("D", [32, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_mfma_d(cuda, D, causal):
+    """Head sizes 32 / 128 on the MFMA kernels (templated on D; no fp32 atomics): several key tiles,
+    ragged T, Tq != Tk (causal offset / ragged key blocks), additive bias."""
+    assert ops.attention_is_mfma(D)
+    torch.manual_seed(90 + D)
+    _attn_check(2, 320, 3, D, causal)
+    _attn_check(1, 100, 2, D, causal, Tk=260)
+    if not causal:
+        _attn_check(1, 130, 2, D, False, Tk=70)
+        T = 96
+        _attn_check(2, T, 2, D, False, bias=torch.tril(torch.ones(T, T, device="cuda")).unsqueeze(0))
+
+
+@pytest.mark.parametrize("D", [32, 128])
+def test_attention_packed_qkv_bias_grad_d(cuda, D):
+    """The in-kernel Σ_rows dQKV partials at head sizes 32 / 128."""
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(12)
+    B, H, T = 2, 2, 200
+    mod = torch.nn.Module()
+    mod.pb = torch.nn.Parameter(torch.zeros(3 * H * D, device="cuda").bfloat16())
+    flat = FlatParams(mod)
+    flat.zero_grad()
+    qkv = bf(B, T, 3, H, D).requires_grad_()
+    o = ops.attention_packed(qkv, causal=True, producer_bias=mod.pb)
+    o.backward(bf(B, T, H, D))
+    assert mod.pb._rn_bias_done
+    assert rel_err(mod.pb.grad, qkv.grad.float().reshape(B * T, 3 * H * D).sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("D", [4, 48, 80])
 def test_attention_generic_d(cuda, D):
     torch.manual_seed(9)
     _attn_check(2, 40, 3, D, True)
@@ -359,9 +391,10 @@ def test_attention_packed_qkv_bias_grad(cuda, monkeypatch, causal, T, dq, dkdv):
     assert rel_err(mod.pb.grad, ref) < 1e-2
 
 
-def test_attention_dropout_unbiased(cuda):
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_attention_dropout_unbiased(cuda, D):
     torch.manual_seed(11)
-    B, T, H, D = 4, 128, 4, 64
+    B, T, H = 4, 128, 4
     q, k, v = bf(B, T, H, D), bf(B, T, H, D), bf(B, T, H, D)
     o0 = ops.attention(q, k, v, causal=True)
     outs = torch.stack([ops.attention(q, k, v, causal=True, dropout_p=0.1, training=True).float() for _ in range(16)])
