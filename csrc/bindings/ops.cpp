@@ -49,7 +49,7 @@ int rn_norm_ws_floats();
 void rn_sumsq(const void*, long, int, float*, float*, hipStream_t);
 void rn_opt_prep(float*, float, float, float, float, int, float, float, float, hipStream_t);
 int rn_adamw(void*, float*, const void*, int, float*, float*, const uint8_t*, float*, long, float, float, float, float,
-             float, float, hipStream_t);
+             float, float, int, hipStream_t);
 void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, long, float, float, int, float, float,
             hipStream_t);
 long rn_gemm_ws_floats(int, int, int);
@@ -556,13 +556,14 @@ void opt_prep(const Tensor& state, double base_lr, double warmup, double total, 
 }
 void adamw_step(const Tensor& p, const Tensor& master, const Tensor& g, const Tensor& m, const Tensor& v,
                 const Tensor& wdm, const Tensor& state, double b1, double b2, double eps, double wd, double gscale,
-                double clip) {
+                double clip, bool stochastic_round) {
     CHECK_BF16(p); GUARD(p);
     TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat);
     TORCH_CHECK(p.numel() == master.numel() && p.numel() == g.numel() && wdm.numel() * 64 >= p.numel());
     int rc = rn_adamw(p.data_ptr(), master.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16,
                       m.data_ptr<float>(), v.data_ptr<float>(), wdm.data_ptr<uint8_t>(), state.data_ptr<float>(),
-                      p.numel(), (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale, (float)clip, cur_stream());
+                      p.numel(), (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale, (float)clip,
+                      stochastic_round ? 1 : 0, cur_stream());
     TORCH_CHECK(rc == 0, "adamw: flat buffer length must be a multiple of 8");
 }
 void sgd_step(const Tensor& p, const Tensor& master, const Tensor& g, const Tensor& buf, const Tensor& wdm,
@@ -920,7 +921,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("opt_prep(Tensor(a!) state, float base_lr, float warmup, float total, float min_ratio, bool cosine, "
           "float lr_override, float b1, float b2) -> ()");
     m.def("adamw_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) m, Tensor(d!) v, Tensor wdm, Tensor(e!) state, "
-          "float b1, float b2, float eps, float wd, float gscale, float clip) -> ()");
+          "float b1, float b2, float eps, float wd, float gscale, float clip, bool stochastic_round=False) -> ()");
     m.def("sgd_step(Tensor(a!) p, Tensor(b!) master, Tensor g, Tensor(c!) buf, Tensor wdm, Tensor(e!) state, "
           "float mom, float wd, bool nesterov, float gscale, float clip) -> ()");
     m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? bias, float scale, bool causal, float p, int seed, "

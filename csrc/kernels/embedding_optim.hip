@@ -150,12 +150,40 @@ RN_DEV float clip_coef(const float* normbuf, float grad_scale, float clip) {
     return (clip > 0.f && nrm > clip) ? clip / (nrm + 1e-6f) : 1.f;
 }
 
-// AdamW over the flat buffer, 8 elements per lane.
-template <typename GT>
+// fp32 → bf16 with stochastic rounding: add 16 random low bits, truncate (unbiased: E[bf16] = w).
+// The bits hash (element index, optimizer step): deterministic for a given step, fresh every step,
+// and graph-capturable (the step count lives in device memory).
+RN_DEV uint32_t sr_hash(uint32_t x) {
+    x ^= x >> 16; x *= 0x7FEB352Du;
+    x ^= x >> 15; x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+RN_DEV void store8_sr(bf16* dst, const float (&w)[8], long e, uint32_t step) {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        uint32_t h[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t bits = __float_as_uint(w[j + u]);
+            const uint32_t r = sr_hash((uint32_t)(e + j + u) ^ (step * 0x9E3779B9u)) & 0xFFFFu;
+            // finite values only (inf / nan keep nearest rounding's upper half unchanged)
+            h[u] = ((bits & 0x7F800000u) == 0x7F800000u) ? (bits >> 16) : ((bits + r) >> 16);
+        }
+        o[j / 2] = h[0] | (h[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// AdamW over the flat buffer, 8 elements per lane.  SR: stochastic rounding of the bf16 weight copy
+// (the fp32 master is exact either way).
+template <typename GT, bool SR>
 __global__ void __launch_bounds__(256) adamw_k(bf16* __restrict__ p, float* __restrict__ master,
                                                const GT* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
                                                const uint8_t* __restrict__ wdm, float* __restrict__ normbuf, long n,
                                                float b1, float b2, float eps, float wd, float grad_scale, float clip) {
+    const uint32_t step = (uint32_t)normbuf[2];
     const float coef = clip_coef(normbuf, grad_scale, clip);
     const float lr = normbuf[3], bc1 = normbuf[4], bc2 = normbuf[5];
     if (coef < 0.f) {
@@ -194,7 +222,8 @@ __global__ void __launch_bounds__(256) adamw_k(bf16* __restrict__ p, float* __re
         vv[1] = make_float4(vf[4], vf[5], vf[6], vf[7]);
         ww[0] = make_float4(wf[0], wf[1], wf[2], wf[3]);
         ww[1] = make_float4(wf[4], wf[5], wf[6], wf[7]);
-        store8(p + e, wf);
+        if constexpr (SR) store8_sr(p + e, wf, e, step);
+        else store8(p + e, wf);
     }
 }
 
@@ -299,16 +328,15 @@ void rn_opt_prep(float* state, float base_lr, float warmup, float total, float m
 }
 
 int rn_adamw(void* p, float* master, const void* g, int g_bf16, float* m, float* v, const uint8_t* wdm,
-             float* state, long n, float b1, float b2, float eps, float wd, float grad_scale, float clip,
+             float* state, long n, float b1, float b2, float eps, float wd, float grad_scale, float clip, int sr,
              hipStream_t st) {
     if (n % 8) return -1;
     int gb = grid_for(n / 8);
-    if (g_bf16)
-        adamw_k<bf16><<<gb, 256, 0, st>>>((bf16*)p, master, (const bf16*)g, m, v, wdm, state, n, b1, b2, eps, wd,
-                                          grad_scale, clip);
-    else
-        adamw_k<float><<<gb, 256, 0, st>>>((bf16*)p, master, (const float*)g, m, v, wdm, state, n, b1, b2, eps, wd,
-                                           grad_scale, clip);
+#define RN_ADAMW(GT, SRV) \
+    adamw_k<GT, SRV><<<gb, 256, 0, st>>>((bf16*)p, master, (const GT*)g, m, v, wdm, state, n, b1, b2, eps, wd, grad_scale, clip)
+    if (g_bf16) { if (sr) RN_ADAMW(bf16, true); else RN_ADAMW(bf16, false); }
+    else { if (sr) RN_ADAMW(float, true); else RN_ADAMW(float, false); }
+#undef RN_ADAMW
     return 0;
 }
 

@@ -103,10 +103,16 @@ class _FlatOptimizer:
 
 
 class FusedAdamW(_FlatOptimizer):
+    """AdamW on the flat buffer (fp32 master, moments).  ``stochastic_round``: the bf16 weight copy
+    the forward reads is written with stochastic rounding (unbiased), so updates smaller than half a
+    bf16 ulp of the weight — every update at warm-up learning rates for |w| ≳ 4e-3 — still move the
+    weights the model computes with in expectation instead of being rounded away."""
+
     def __init__(self, flat: FlatParams, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
-                 max_grad_norm=1.0, grad_scale=1.0):
+                 max_grad_norm=1.0, grad_scale=1.0, stochastic_round=False):
         super().__init__(flat, lr, weight_decay, max_grad_norm, grad_scale)
         self.betas, self.eps = betas, eps
+        self.stochastic_round = bool(stochastic_round)
         self.m = torch.zeros_like(self.master)
         self.v = torch.zeros_like(self.master)
 
@@ -121,7 +127,8 @@ class FusedAdamW(_FlatOptimizer):
             self._prep(lr, b1, b2)
             ops.sumsq(self.grad, self.norm_buf)
             ops.adamw_step(self.flat.data, self.master, self.grad, self.m, self.v, self.flat.wd_mask,
-                           self.norm_buf, b1, b2, self.eps, self.weight_decay, self.grad_scale, clip)
+                           self.norm_buf, b1, b2, self.eps, self.weight_decay, self.grad_scale, clip,
+                           self.stochastic_round)
             return
         lr = self._host_lr(lr)
         bc1 = 1 - b1 ** self.step_count

@@ -92,6 +92,7 @@ class TrainConfig:
     data_dtype: str = "uint16"    # uint16 | uint32 shard element type
     data_mode: str = "train"      # train (random windows) | eval (non-overlapping windows)
     phase_timing: bool = True     # device ms per phase (incl. comm wait) on logged eager steps
+    stochastic_round: bool = True  # AdamW writes the bf16 weight copy with stochastic rounding
     model_kwargs: dict = field(default_factory=dict)
 
 
@@ -117,7 +118,8 @@ class Trainer:
         gs = 1.0 / self.world
         if cfg.optimizer == "adamw":
             self.opt = FusedAdamW(self.flat, lr=cfg.lr, weight_decay=cfg.weight_decay,
-                                  max_grad_norm=cfg.max_grad_norm, grad_scale=gs)
+                                  max_grad_norm=cfg.max_grad_norm, grad_scale=gs,
+                                  stochastic_round=cfg.stochastic_round)
         else:
             self.opt = FusedSGD(self.flat, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
                                 max_grad_norm=cfg.max_grad_norm, grad_scale=gs)

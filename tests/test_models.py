@@ -12,11 +12,11 @@ def _lm_batch(cfg, B=2, T=32, dev="cpu"):
     return x[:, :-1], x[:, 1:]
 
 
-@pytest.mark.parametrize("name", ["gpt2-tiny", "vit-tiny", "resnet18-tiny", "mlp"])
+@pytest.mark.parametrize("name", ["gpt2-tiny", "vit-tiny", "resnet18-tiny", "mlp", "refblock-lm"])
 def test_model_cpu_fwd_bwd(name):
     torch.manual_seed(0)
     m = build_model(name)
-    if name.startswith("gpt2"):
+    if name.startswith("gpt2") or name == "refblock-lm":
         x, y = _lm_batch(m.config)
     elif name == "mlp":
         x, y = torch.rand(4, 784), torch.randint(0, 10, (4,))
@@ -27,6 +27,20 @@ def test_model_cpu_fwd_bwd(name):
     assert torch.isfinite(loss)
     loss.backward()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters() if p.requires_grad)
+
+
+def test_refblock_lm_trains_and_keeps_reference_layout():
+    """The reference-block token model: its blocks are the reference's TransformerDecoder (state_dict
+    keys as in the reference), head dropout 0.1 is active in train mode, and the loss falls."""
+    m = build_model("refblock-lm", n_layer=1, n_head=4, n_embd=64, block_size=32)
+    keys = [k for k in m.state_dict() if k.startswith("blocks.0.")]
+    assert "blocks.0._attn._heads.0._query.weight" in keys and "blocks.0._attn_mask" in keys
+    tr = Trainer(TrainConfig(model="refblock-lm", steps=30, batch_size=8, seq_len=32, lr=3e-3, device="cpu",
+                             log_every=1000, model_kwargs=dict(n_layer=1, n_head=4, n_embd=64, block_size=32)))
+    first = float(tr.step())
+    assert tr.model.training and tr.model.blocks[0]._attn._heads[0]._dropout.p == 0.1
+    out = tr.run()
+    assert out["final_loss"] < first
 
 
 def test_gpt2_param_count():

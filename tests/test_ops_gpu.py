@@ -467,6 +467,27 @@ def test_fused_adamw_matches_cpu(cuda):
     assert torch.equal(before, og.master) and og.norm_buf[1].item() == 1.0
 
 
+def test_adamw_stochastic_rounding_unbiased(cuda):
+    """The bf16 weight copy under stochastic rounding: a master value a quarter bf16 ulp above 1.0
+    rounds up for ~1/4 of the elements (nearest rounding: never), deterministically per step."""
+    from replicann_amd.optim import FusedAdamW
+    from replicann_amd.utils.flat import FlatParams
+    lin = torch.nn.Linear(1024, 1024, bias=False).cuda().to(torch.bfloat16)
+    flat = FlatParams(lin)
+    outs = []
+    for sr in (True, True, False):
+        opt = FusedAdamW(flat, lr=0.0, weight_decay=0.0, max_grad_norm=0.0, stochastic_round=sr)
+        opt.master.fill_(1.0 + 2.0 ** -9)
+        flat.grad.zero_()
+        opt.step()
+        outs.append(flat.data.float().clone())
+    up = (outs[0] > 1.0).float().mean().item()
+    assert 0.24 < up < 0.26, up
+    assert abs(outs[0].mean().item() - (1.0 + 2.0 ** -9)) < 2e-4
+    assert torch.equal(outs[0], outs[1])  # same step count -> same bits
+    assert (outs[2] == 1.0).all()
+
+
 # ----------------------------------------------------------------- conv / bn / pool
 @pytest.mark.parametrize("cfg", [(3, 7, 2, 3), (16, 3, 1, 1), (16, 1, 2, 0), (8, 3, 2, 1), (3, 16, 16, 0)])
 def test_conv2d(cuda, cfg):
