@@ -192,7 +192,9 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         CHECK_BF16(*preact);
         TORCH_CHECK(preact->size(0) == M && preact->size(1) == N && preact->stride(0) == c.stride(0));
     }
-    const bool act_bwd = act == 3 || act == 4;  // fused activation backward: out = (A·B) ⊙ act'(preact)
+    // fused activation backward: out = (A·B) ⊙ act'(preact); 6: out = (A·B) ⊙ preact (preact holds gelu'(h),
+    // written by the act-5 forward)
+    const bool act_bwd = act == 3 || act == 4 || act == 6;
     // bias_grad (act-backward only): Σ_rows of the output accumulated into it — from per-M-tile
     // column partials the epilogue writes (configs that support it), else one reduction pass
     const bool want_bg = bias_grad && bias_grad->defined();

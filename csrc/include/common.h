@@ -103,23 +103,45 @@ RN_DEV float gelu_grad_f(float x) {
     return s + 2.f * x * s * (1.f - s) * c * (1.f + 0.134145f * x2);
 }
 
-enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU_BWD = 3, ACT_GELU_BWD = 4 };
+// gelu(x) and gelu'(x) sharing one exp + rcp
+RN_DEV float gelu_and_grad_f(float x, float& d) {
+    const float c = 0.7978845608028654f;
+    const float x2 = x * x;
+    const float s = fast_sigmoid(2.f * c * (x + 0.044715f * x2 * x));
+    d = s + 2.f * x * s * (1.f - s) * c * (1.f + 0.134145f * x2);
+    return x * s;
+}
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU_BWD = 3, ACT_GELU_BWD = 4, ACT_GELU_D = 5, ACT_MUL_BWD = 6 };
 // *_BWD (GEMM epilogue only): out = acc · act'(aux) with aux = the saved pre-activation,
 // i.e. the activation backward fused into the dgrad GEMM that produces dY·W.
-constexpr bool act_fwd(int a) { return a == ACT_RELU || a == ACT_GELU; }
-constexpr bool act_bwd(int a) { return a == ACT_RELU_BWD || a == ACT_GELU_BWD; }
+// ACT_GELU_D: GELU whose forward epilogue saves gelu'(h) instead of h (computed with the same
+// exp / rcp as gelu(h)); its backward ACT_MUL_BWD is then one multiply per element, out = acc · aux,
+// instead of re-deriving gelu'(h) (exp, rcp and ~10 FMAs) in the dgrad epilogue.
+constexpr bool act_fwd(int a) { return a == ACT_RELU || a == ACT_GELU || a == ACT_GELU_D; }
+constexpr bool act_bwd(int a) { return a == ACT_RELU_BWD || a == ACT_GELU_BWD || a == ACT_MUL_BWD; }
 
 template <int ACT>
 RN_DEV float act_f(float x) {
     if constexpr (ACT == ACT_RELU) return fmaxf(x, 0.f);
-    else if constexpr (ACT == ACT_GELU) return gelu_f(x);
+    else if constexpr (ACT == ACT_GELU || ACT == ACT_GELU_D) return gelu_f(x);
     else return x;
 }
 template <int ACT>
 RN_DEV float act_grad_f(float x) {
     if constexpr (ACT == ACT_RELU || ACT == ACT_RELU_BWD) return x > 0.f ? 1.f : 0.f;
     else if constexpr (ACT == ACT_GELU || ACT == ACT_GELU_BWD) return gelu_grad_f(x);
+    else if constexpr (ACT == ACT_MUL_BWD) return x;
     else return 1.f;
+}
+// forward epilogue with a pre-activation buffer: returns act(h), *pre = what the buffer stores
+template <int ACT>
+RN_DEV float act_fwd_pre(float h, float& pre) {
+    if constexpr (ACT == ACT_GELU_D) return gelu_and_grad_f(h, pre);
+    else {
+        pre = h;
+        return act_f<ACT>(h);
+    }
 }
 
 #define HIP_CHECK_LAUNCH() (void)hipGetLastError()

@@ -643,9 +643,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                 bool changed = false;
                 if constexpr (act_fwd(ACT)) {
                     if (two_out) {
-                        *reinterpret_cast<s16x8*>(p.pre + goff) = v;
+                        float pv[8];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) f[t] = act_f<ACT>(f[t]);
+                        for (int t = 0; t < 8; ++t) f[t] = act_fwd_pre<ACT>(f[t], pv[t]);
+                        if constexpr (ACT == ACT_GELU_D) store8(p.pre + goff, pv);
+                        else *reinterpret_cast<s16x8*>(p.pre + goff) = v;
                         changed = true;
                     }
                 }
@@ -750,15 +752,16 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                         if (n + t < p.N) v[t] = (float)(bf16)v[t] * act_grad_f<ACT>((float)pp[t]);
                 }
                 if constexpr (act_fwd(ACT)) {
+                    float pv[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v[t] = act_fwd_pre<ACT>(v[t], pv[t]);
                     if (p.pre) {
                         bf16* pp = p.pre + (long)m * p.ldc + n;
                         if (full) {
-                            bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+                            bf16x4 o = {(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
                             *reinterpret_cast<bf16x4*>(pp) = o;
-                        } else for (int t = 0; t < 4 && n + t < p.N; ++t) pp[t] = (bf16)v[t];
+                        } else for (int t = 0; t < 4 && n + t < p.N; ++t) pp[t] = (bf16)pv[t];
                     }
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) v[t] = act_f<ACT>(v[t]);
                 }
                 if (p.res) {
                     const bf16* rp = p.res + (long)m * p.ldc + n;
@@ -813,8 +816,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
             float x = v[t];
             if (p.bias) x += (float)p.bias[n];
             if constexpr (act_fwd(ACT)) {
-                if (p.pre) p.pre[(long)m * p.ldc + n] = (bf16)x;
-                x = act_f<ACT>(x);
+                float pv;
+                x = act_fwd_pre<ACT>(x, pv);
+                if (p.pre) p.pre[(long)m * p.ldc + n] = (bf16)pv;
             }
             if constexpr (act_bwd(ACT)) x = (float)(bf16)x * act_grad_f<ACT>((float)p.pre[(long)m * p.ldc + n]);
             if (p.res) x += (float)p.res[(long)m * p.ldc + n];
@@ -862,9 +866,13 @@ void launch_cfg(GemmArgs& a, bool ak, bool bk, int act, hipStream_t st) {
     if (act == ACT_GELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_GELU, NS>(a, st);           \
     else if (act == ACT_RELU) launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_RELU, NS>(a, st);      \
     else launch_t<BM, BN, WM, WN, PIPE, AKv, BKv, ACT_NONE, NS>(a, st);
-    if (ak && bk) { RN_L(true, true) }
+    if (ak && bk) {
+        if (act == ACT_GELU_D) launch_t<BM, BN, WM, WN, PIPE, true, true, ACT_GELU_D, NS>(a, st);
+        else { RN_L(true, true) }
+    }
     else if (ak && !bk) {  // dgrad layout: also the fused activation-backward epilogues
         if (act == ACT_GELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_GELU_BWD, NS>(a, st);
+        else if (act == ACT_MUL_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_MUL_BWD, NS>(a, st);
         else if (act == ACT_RELU_BWD) launch_t<BM, BN, WM, WN, PIPE, true, false, ACT_RELU_BWD, NS>(a, st);
         else { RN_L(true, false) }
     }

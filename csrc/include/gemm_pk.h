@@ -389,10 +389,20 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                         // the activation is applied to the bf16-rounded value the backward sees
                         const u32x4 pu = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
                                           pk_pack2(v[6], v[7])};
-                        pk_st16(pu, prs, off(mh, i, nh, 2));
-                        if (p.pre) pk_unpack8(pu, v);
+                        if constexpr (ACT == ACT_GELU_D) {  // store gelu'(h) of the bf16-rounded h
+                            pk_unpack8(pu, v);
+                            float d[8];
 #pragma unroll
-                        for (int c = 0; c < 8; ++c) v[c] = act_f<ACT>(v[c]);
+                            for (int c = 0; c < 8; ++c) v[c] = gelu_and_grad_f(v[c], d[c]);
+                            pk_st16((u32x4){pk_pack2(d[0], d[1]), pk_pack2(d[2], d[3]), pk_pack2(d[4], d[5]),
+                                            pk_pack2(d[6], d[7])},
+                                    prs, off(mh, i, nh, 2));
+                        } else {
+                            pk_st16(pu, prs, off(mh, i, nh, 2));
+                            if (p.pre) pk_unpack8(pu, v);
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) v[c] = act_f<ACT>(v[c]);
+                        }
                     }
                     if (auxp) {
                         float ax[8];

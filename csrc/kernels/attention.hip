@@ -59,7 +59,26 @@ struct AttnArgs {
     // lse units: the D = 64 forward kernels store log2(Σ exp) in base-2 units (the backward then
     // needs one FMA per score, exp2(s·scale·log2e − lse2)); the generic forward stores natural log.
     int lse_log2;
+    // block order (1-D grid of B·H·nblk blocks): 0 = head-interleaved (block L: head L % (B·H), the
+    // heaviest causal blocks of all heads first); 1 = XCD-grouped — each XCD (blocks b, b+8, …, dealt
+    // round-robin) works through a contiguous range of heads, all blocks of a head back to back
+    int xcd_map;
 };
+
+// (bh, block) of this workgroup; `reverse`: the head's heaviest (last) causal block first
+RN_DEV void blk_map(const AttnArgs& p, int nblk, bool reverse, int& bh, int& blk) {
+    const int BH = p.B * p.H, L = blockIdx.x, n = BH * nblk;
+    int i;
+    if (p.xcd_map && (n & 7) == 0) {
+        const int w = (L & 7) * (n >> 3) + (L >> 3);
+        bh = w / nblk;
+        i = w - bh * nblk;
+    } else {
+        bh = L % BH;
+        i = L / BH;
+    }
+    blk = reverse ? nblk - 1 - i : i;
+}
 
 // LDS tile geometry for head size D ∈ {32, 64, 128}: [64 rows][D bf16] = RB-byte rows, 16-B chunks
 // XOR-swizzled per row.  Each swizzle is a permutation of the row's chunks that (a) makes the
@@ -272,9 +291,9 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // grid (B*H, blocks): the block index varies SLOWEST, so under causal masking every head's
     // heaviest query block is dispatched before any lighter one (longest-first over the grid)
-    const int nqb = gridDim.y;
-    const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
-    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+    int bh, qb;
+    blk_map(p, (p.Tq + QBLK - 1) / QBLK, CAUSAL, bh, qb);
+    const int b = bh / p.H, h = bh % p.H;
     const int q0 = qb * QBLK + wave * 16 * QI;
     const int off = p.Tk - p.Tq;  // causal: key j visible to query i iff j <= i + off
     const float sl2 = p.scale * LOG2E;
@@ -475,9 +494,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     const FragOff fo = make_fragoff(lane);
     // grid (B*H, blocks): the block index varies SLOWEST, so under causal masking every head's
     // heaviest query block is dispatched before any lighter one (longest-first over the grid)
-    const int nqb = gridDim.y;
-    const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
-    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+    int bh, qb;
+    blk_map(p, (p.Tq + 127) / 128, CAUSAL, bh, qb);
+    const int b = bh / p.H, h = bh % p.H;
     const int q0 = qb * 128 + wave * 32;
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
@@ -700,8 +719,9 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
     constexpr int KB = 64 * KG;  // keys per block
     // grid (B*H, key blocks): low key blocks see the most queries under causal and, with the block
     // index varying slowest, launch first across ALL heads (longest-first)
-    const int kb = blockIdx.y;
-    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+    int bh, kb;
+    blk_map(p, (p.Tk + KB - 1) / KB, false, bh, kb);  // low key blocks see the most queries: first
+    const int b = bh / p.H, h = bh % p.H;
     const int kvw = kb * KB + wave * 16;  // this wave's first key (group 0)
     int kvl[KG];
 #pragma unroll
@@ -920,9 +940,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const FragOffT<D> fo = make_fragoff<D>(lane);
     constexpr int QB = 64 * QG;  // queries per block
-    const int nqb = gridDim.y;  // grid (B*H, query blocks): heaviest blocks of every head first
-    const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
-    const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+    int bh, qb;
+    blk_map(p, (p.Tq + QB - 1) / QB, CAUSAL, bh, qb);  // heaviest blocks of every head first
+    const int b = bh / p.H, h = bh % p.H;
     const int qw_last = qb * QB + 64 * (QG - 1) + wave * 16;  // this wave's first query of its LAST group
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
@@ -1256,15 +1276,24 @@ __global__ void scatter_kv_k(AttnArgs p) {
 template <int D>
 void attn_fwd_mfma(AttnArgs& a, hipStream_t st) {
     constexpr int QBLK = D == 128 ? 64 : 128;
-    dim3 grid(a.B * a.H, (a.Tq + QBLK - 1) / QBLK);
+    dim3 grid(a.B * a.H * ((a.Tq + QBLK - 1) / QBLK));
     RN_DISPATCH3V(attn_fwd64_k, grid, 4 * kTB<D>, st, a, D, (D == 128 ? 2 : 3), (D == 128 ? 1 : 2));
 }
 template <int D>
 void attn_bwd_mfma(AttnArgs& a, hipStream_t st) {
-    dim3 g2(a.B * a.H, (a.Tq + 63) / 64);
-    dim3 g1(a.B * a.H, (a.Tk + 63) / 64);
+    dim3 g2(a.B * a.H * ((a.Tq + 63) / 64));
+    dim3 g1(a.B * a.H * ((a.Tk + 63) / 64));
     RN_DISPATCH3V(attn_bwd_dq64_k, g2, 4 * kTB<D>, st, a, 2, 1, D);
     RN_DISPATCH3V(attn_bwd_dkdv64_k, g1, 2 * (2 * kTB<D> + 2048), st, a, (D == 128 ? 1 : 3), 1, D);
+}
+
+// REPLICANN_ATTN_XCD=1 selects the XCD-grouped block order.  Measured slower (GPT-2-small causal
+// B64: fwd 0.177 -> 0.199 ms, bwd 0.571 -> 0.597 ms): a head's 8 query blocks then read the same K/V
+// tiles at the same moment, and the head-interleaved default (heaviest blocks of every head first)
+// balances the causal load better.  Kept for A/B on other shapes.
+int xcd_order() {
+    const char* e = std::getenv("REPLICANN_ATTN_XCD");
+    return e ? std::atoi(e) : 0;
 }
 
 // the MFMA kernels' requirements: D ∈ {32, 64, 128} and 16-B aligned rows (strides in elements)
@@ -1287,12 +1316,13 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     a.o_sb = strides[9]; a.o_st = strides[10]; a.o_sh = strides[11];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
     a.scale = scale; a.p_drop = p_drop; a.seed = seed;
+    a.xcd_map = xcd_order();
     const bool fast = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast && D != 64) {
         if (D == 32) attn_fwd_mfma<32>(a, st);
         else attn_fwd_mfma<128>(a, st);
     } else if (fast) {
-        dim3 grid(B * H, (Tq + 127) / 128);
+        dim3 grid(B * H * ((Tq + 127) / 128));
         // REPLICANN_ATTN_FWD=1 selects the original single-loop kernel, 2 the split-loop v2, 3 (default)
         // v2 with the LEAN softmax bookkeeping (read per call so one process can A/B them); no bias /
         // dropout in v2/v3, 3 blocks per CU
@@ -1331,6 +1361,7 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     a.dk_sb = s[18]; a.dk_st = s[19]; a.dk_sh = s[20]; a.dv_sb = s[21]; a.dv_st = s[22]; a.dv_sh = s[23];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
     a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.dk32 = dk32; a.dv32 = dv32; a.bsum = bsum;
+    a.xcd_map = xcd_order();
     const bool fast = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) &&
                       (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
                       (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
@@ -1343,14 +1374,14 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         else attn_bwd_mfma<128>(a, st);
     } else if (fast) {
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
-        dim3 g2(B * H, (Tq + 63) / 64);
-        dim3 g1(B * H, (Tk + 63) / 64);
+        dim3 g2(B * H * ((Tq + 63) / 64));
+        dim3 g1(B * H * ((Tk + 63) / 64));
         // REPLICANN_ATTN_DQ: 2 (default) = two 64-query groups per wave (plain causal / non-causal;
         // bwd -11 % at GPT-2-small shapes), 1 = one
         const char* eq = std::getenv("REPLICANN_ATTN_DQ");
         const int dqv = eq ? std::atoi(eq) : 2;
         if (dqv >= 2 && !bias && p_drop == 0.f) {
-            dim3 g2b(B * H, (Tq + 127) / 128);
+            dim3 g2b(B * H * ((Tq + 127) / 128));
             if (causal) attn_bwd_dq64_k<true, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
             else attn_bwd_dq64_k<false, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
         } else {
@@ -1361,7 +1392,7 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         const char* ek = std::getenv("REPLICANN_ATTN_DKDV");
         const int kvv = ek ? std::atoi(ek) : 2;
         if (kvv >= 2 && !bias && p_drop == 0.f) {
-            dim3 g1b(B * H, (Tk + 127) / 128);
+            dim3 g1b(B * H * ((Tk + 127) / 128));
             if (causal) attn_bwd_dkdv64_k<true, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
             else attn_bwd_dkdv64_k<false, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
         } else {

@@ -145,6 +145,7 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     a.split = 1; a.k_per_split = ((K / 2) + 63) / 64 * 64; a.out_f32 = 0; a.accumulate = 0;
     using namespace rn_gemm_detail;
     if (act == ACT_GELU) launch_fp8_t<256, 192, 2, 4, ACT_GELU>(a, st);
+    else if (act == ACT_GELU_D) launch_fp8_t<256, 192, 2, 4, ACT_GELU_D>(a, st);
     else if (act == ACT_RELU) launch_fp8_t<256, 192, 2, 4, ACT_RELU>(a, st);
     else launch_fp8_t<256, 192, 2, 4, ACT_NONE>(a, st);
     return 0;

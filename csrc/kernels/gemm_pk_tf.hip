@@ -12,6 +12,7 @@ void rn_gemm_launch_pk_tf(GemmArgs& a, int act, hipStream_t st) {
         if (act == ACT_GELU) splitk_reduce_k<ACT_GELU><<<g, 256, 0, st>>>(a);
         else if (act == ACT_RELU) splitk_reduce_k<ACT_RELU><<<g, 256, 0, st>>>(a);
         else if (act == ACT_GELU_BWD) splitk_reduce_k<ACT_GELU_BWD><<<g, 256, 0, st>>>(a);
+        else if (act == ACT_MUL_BWD) splitk_reduce_k<ACT_MUL_BWD><<<g, 256, 0, st>>>(a);
         else if (act == ACT_RELU_BWD) splitk_reduce_k<ACT_RELU_BWD><<<g, 256, 0, st>>>(a);
         else splitk_reduce_k<ACT_NONE><<<g, 256, 0, st>>>(a);
         return;
@@ -21,6 +22,7 @@ void rn_gemm_launch_pk_tf(GemmArgs& a, int act, hipStream_t st) {
         case ACT_GELU: launch_pk_t<true, false, ACT_GELU, false, false>(a, st); break;
         case ACT_RELU: launch_pk_t<true, false, ACT_RELU, false, false>(a, st); break;
         case ACT_GELU_BWD: launch_pk_t<true, false, ACT_GELU_BWD, false, false>(a, st); break;
+        case ACT_MUL_BWD: launch_pk_t<true, false, ACT_MUL_BWD, false, false>(a, st); break;
         case ACT_RELU_BWD: launch_pk_t<true, false, ACT_RELU_BWD, false, false>(a, st); break;
         default: launch_pk_t<true, false, ACT_NONE, false, false>(a, st); break;
     }

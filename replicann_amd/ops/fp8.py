@@ -16,7 +16,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
-from .linear import _act_ref
+from .linear import _act_ref, _pre_ref
 
 E4M3_MAX = 448.0
 
@@ -75,7 +75,7 @@ def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State):
     if bias is not None:
         h = h + bias.float()
     if preact is not None:
-        preact.copy_(h)
+        preact.copy_(_pre_ref(h, act))
     y = _act_ref(h, act)
     if res2 is not None:
         y = y + res2.float()

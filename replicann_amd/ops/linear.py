@@ -18,6 +18,7 @@ CPU tensors take the plain ATen path (same math, fp32 accumulation).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -25,14 +26,24 @@ import torch.nn.functional as F
 from .. import _ext
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+# GEMM-epilogue-only codes: 5 = GELU whose pre-activation buffer receives gelu'(h) instead of h;
+# 6 = its fused backward, out = (A·B) ⊙ pre (one multiply; see csrc/include/common.h)
+ACT_GELU_D, ACT_MUL_BWD = 5, 6
 _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU}
 
 
 def _act_ref(h: torch.Tensor, act: int) -> torch.Tensor:
     if act == ACT_RELU:
         return F.relu(h)
-    if act == ACT_GELU:
+    if act in (ACT_GELU, ACT_GELU_D):
         return F.gelu(h, approximate="tanh")
+    return h
+
+
+def _pre_ref(h: torch.Tensor, act: int) -> torch.Tensor:
+    """What the forward epilogue writes into the pre-activation buffer."""
+    if act == ACT_GELU_D:
+        return _act_grad_ref(torch.ones_like(h), h, ACT_GELU)
     return h
 
 
@@ -71,8 +82,10 @@ def gemm(a, b, *, ta=False, tb=False, bias=None, residual=None, act=ACT_NONE, pr
         h = h * alpha.float()
     if bias is not None:
         h = h + bias.float()
-    if preact is not None:
-        preact.copy_(h)
+    if act == ACT_MUL_BWD:
+        h = h * preact.float()
+    elif preact is not None:
+        preact.copy_(_pre_ref(h, act))
     y = _act_ref(h, act)
     if residual is not None:
         y = y + residual.float()
@@ -215,6 +228,13 @@ def linear(x, weight, bias=None, act=None, residual=None, fp8=None):
 # fused two-layer MLP: y = act(x·W1ᵀ + b1)·W2ᵀ + b2 (+ residual)
 # --------------------------------------------------------------------------
 ACT_BWD = {ACT_RELU: 3, ACT_GELU: 4}  # GEMM epilogue codes: out = (A·B) ⊙ act'(pre)
+# The MLP's GELU saves gelu'(h) (forward epilogue code 5) and its dgrad multiplies by it (code 6)
+# (REPLICANN_MLP_GELU=pre: save h and re-derive gelu'(h) in the dgrad epilogue — A/B only)
+if os.environ.get("REPLICANN_MLP_GELU", "deriv") == "pre":
+    _MLP_FWD_ACT, _MLP_BWD_ACT = {ACT_RELU: ACT_RELU, ACT_GELU: ACT_GELU}, dict(ACT_BWD)
+else:
+    _MLP_FWD_ACT = {ACT_RELU: ACT_RELU, ACT_GELU: ACT_GELU_D}
+    _MLP_BWD_ACT = {ACT_RELU: 3, ACT_GELU: ACT_MUL_BWD}
 
 
 def _bias_grad(g2, bias, native):
@@ -258,10 +278,10 @@ class _MLPFn(torch.autograd.Function):
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
         if fp8 is not None:  # (state of layer 1, state of layer 2): e4m3 forward GEMMs
             from .fp8 import fp8_forward
-            u = fp8_forward(x2, w1, b1, None, act, pre, fp8[0])
+            u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0])
             y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
         else:
-            u = ops.gemm(x2, w1, False, True, b1, None, act, pre, None, False, 0, False, None, -1)
+            u = ops.gemm(x2, w1, False, True, b1, None, _MLP_FWD_ACT[act], pre, None, False, 0, False, None, -1)
             y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)
         ctx.save_for_backward(x2, w1, pre, u, w2)
         ctx.b1, ctx.b2, ctx.act, ctx.shp, ctx.has_res = b1, b2, act, shp, residual is not None
@@ -281,7 +301,7 @@ class _MLPFn(torch.autograd.Function):
             b1_acc = _direct_grad(b1)
         # dH = (dY·W2) ⊙ act'(pre); with a flat-buffer b1 its gradient Σ_rows dH comes from the
         # same GEMM's epilogue (per-tile column partials + one small reduction)
-        dh = ops.gemm(gy2, w2, False, False, None, None, ACT_BWD[ctx.act], pre, None, False, 0, False, None, -1,
+        dh = ops.gemm(gy2, w2, False, False, None, None, _MLP_BWD_ACT[ctx.act], pre, None, False, 0, False, None, -1,
                       b1_acc)
         if b1_acc is not None:
             _notify(b1)

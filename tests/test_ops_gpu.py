@@ -108,6 +108,32 @@ def test_gemm_epilogue(cuda, act, cfg):
         assert rel_err(pre, h) < 1e-2
 
 
+def _gelu_grad(h):
+    hf = h.float().requires_grad_()
+    (g,) = torch.autograd.grad(F.gelu(hf, approximate="tanh"), hf, torch.ones_like(hf))
+    return g
+
+
+@pytest.mark.parametrize("cfg,split", [(-1, 0), (0, 0), (1, 0), (6, 0), (9, 0), (9, 3), (0, 4)])
+def test_gemm_gelu_saved_derivative(cuda, cfg, split):
+    """Epilogue code 5 (forward: y = gelu(h), pre = gelu'(h)) and code 6 (dgrad: out = (dY·W) ⊙ pre),
+    the pair the fused MLP uses; against fp32 math."""
+    torch.manual_seed(21)
+    M, N, K = 520, 776, 384
+    a, w, bias = bf(M, K), bf(N, K, scale=0.1), bf(N)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    out = torch.ops.replicann.gemm(a, w, False, True, bias, None, 5, pre, None, False, split, False, None, cfg, None)
+    h = a.float() @ w.float().t() + bias.float()
+    assert rel_err(out, F.gelu(h, approximate="tanh")) < 1e-2
+    assert rel_err(pre, _gelu_grad(h)) < 1e-2
+    dy, w2 = bf(M, K), bf(K, N, scale=0.1)
+    bg = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+    dh = torch.ops.replicann.gemm(dy, w2, False, False, None, None, 6, pre, None, False, split, False, None, cfg, bg)
+    ref = (dy.float() @ w2.float()).bfloat16().float() * pre.float()
+    assert rel_err(dh, ref) < 1e-2
+    assert rel_err(bg.float(), dh.float().sum(0)) < 2e-2
+
+
 @pytest.mark.parametrize("split,cfg", [(2, 0), (4, 1), (8, -1), (3, 2), (4, 9), (7, 9)])
 def test_gemm_splitk_fp32_accumulate(cuda, split, cfg):
     torch.manual_seed(2)
