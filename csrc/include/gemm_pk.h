@@ -169,7 +169,10 @@ constexpr int pk_epi_stores() {
 }
 
 // DBG (timing-only ablation builds: gemm_pk_dbg.hip, cfg 90 + DBG; outputs are wrong): bit 0
-// skips the main-loop operand DMA, bit 1 the counted vmcnt waits, bit 2 the epilogue body.
+// skips the main-loop operand DMA, bit 1 the counted vmcnt waits, bit 2 the epilogue body, bit 3
+// issues the DMA between the two k-steps' MFMAs, bit 4 issues every main-loop DMA instruction with
+// an out-of-range offset (same instructions, no memory traffic, no LDS writes), bit 5 issues each
+// half-tile's DMA with the SAME descriptor every phase (no per-phase descriptor rebuild).
 template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     constexpr int BM = 256, BN = 256;
@@ -268,6 +271,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         const bf16* base = isA ? (H == 3 ? ca + a_half : ca) : (H == 2 ? cb + b_half : cb);
         const int mnl = isA ? (H == 3 ? cml - 128 : cml) : (H == 2 ? cnl - 128 : cnl);
         const u32x4 rs = rsrc_sgpr(base);
+        if constexpr (DBG & 16) {
+            if (in_loop) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) dma16_at(rs, 0xFFFFFFF0u, dst + i * 1024);
+                return;
+            }
+        }
         if (mnl >= 128 && ckl >= BK) {  // interior half-tile: no per-lane checks
 #pragma unroll
             for (int i = 0; i < 2; ++i) dma16_at(rs, isA ? a_off[i] : b_off[i], dst + i * 1024);

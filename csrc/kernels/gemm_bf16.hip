@@ -144,7 +144,7 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
         if (split < 0) split = ch.split;
     }
     if (cfg == 9 && !pk_ok(N, ldc, out_f32, act)) cfg = 1;  // shapes the persistent kernel does not take
-    if (cfg >= 90 && cfg < 100) {  // timing-only ablation builds of cfg 9 (wrong outputs)
+    if (cfg >= 90 && cfg < 110) {  // timing-only ablation builds of cfg 9 (wrong outputs)
         GemmArgs d = {};
         d.A = (const bf16*)A; d.B = (const bf16*)B; d.C = C; d.M = M; d.N = N; d.K = K;
         d.lda = lda; d.ldb = ldb; d.ldc = ldc; d.split = 1; d.k_per_split = (K + BK - 1) / BK * BK;
