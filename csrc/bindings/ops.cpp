@@ -246,6 +246,10 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         (void)hipStreamIsCapturing(cur_stream(), &cap);
         if (!hit && autotune_enabled() && cap == hipStreamCaptureStatusNone) {
             Tensor scratch = at::empty({M, N}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
+            // forward activations time WITH their pre-activation / derivative store (a scratch copy): the
+            // second output is a large part of the epilogue, and configs differ most in the epilogue
+            const bool act_fwd_pre = !act_bwd && act != 0 && preact && preact->defined();
+            Tensor scratch_pre = act_fwd_pre ? at::empty({M, N}, a.options()) : Tensor();
             const bool plain = !(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
                                !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
             const int ncfg = (plain && lib_candidate()) ? 7 : 6;
@@ -274,16 +278,15 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                     if (cfgs[ci] == kLibCfg && sp > 1) break;
                     auto run = [&]() {
                         if (cfgs[ci] == kLibCfg) { lib_gemm(A, B, ta, tb, scratch); return 0; }
-                        // fwd activations: skip the pre-activation store while timing; bwd ones read it
                         return rn_gemm(A.data_ptr(), B.data_ptr(), scratch.data_ptr(), optr(bias), optr(residual),
-                                       act_bwd ? preact->data_ptr() : nullptr,
+                                       act_bwd ? preact->data_ptr() : (act_fwd_pre ? scratch_pre.data_ptr() : nullptr),
                                        tws.data_ptr<float>(), alpha && alpha->defined() ? alpha->data_ptr<float>() : nullptr,
                                        (int)M, (int)N, (int)Kp, A.stride(0), B.stride(0), scratch.stride(0), ta, tb, (int)act,
                                        sp, out_fp32, 0, cfgs[ci], cur_stream(), cp);
                     };
                     if (run() != 0) continue;
                     (void)hipEventRecord(e0, cur_stream());
-                    for (int r = 0; r < 3; ++r) run();
+                    for (int r = 0; r < 5; ++r) run();
                     (void)hipEventRecord(e1, cur_stream());
                     (void)hipEventSynchronize(e1);
                     float ms = 0.f;
@@ -299,7 +302,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             }
             if (std::getenv("REPLICANN_GEMM_VERBOSE"))
                 std::fprintf(stderr, "[replicann gemm tune] M=%ld N=%ld K=%ld ta=%d tb=%d act=%ld -> cfg %d split %d (%.3f ms)\n",
-                             (long)M, (long)N, (long)Kp, (int)ta, (int)tb, (long)act, best_cfg, best_split, best_ms / 3);
+                             (long)M, (long)N, (long)Kp, (int)ta, (int)tb, (long)act, best_cfg, best_split, best_ms / 5);
             cfg = best_cfg;
             split = best_split;
         }

@@ -238,6 +238,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     const bf16* ca = p.A;
     const bf16* cb = p.B;
     int cml = 0, cnl = 0, ckl = 0, ckt = 0, cli = 0, ct = 0;
+    // bit H: half-tile H of the K-tile being issued is interior (no per-lane range checks);
+    // recomputed once per K-tile instead of in every phase's DMA issue
+    uint32_t intr = 0;
+    auto cur_intr = [&]() {
+        const bool kf = ckl >= BK;
+        intr = kf ? ((cml >= 128 ? 1u : 0u) | (cnl >= 128 ? 2u : 0u) | (cnl >= 256 ? 4u : 0u) | (cml >= 256 ? 8u : 0u))
+                  : 0u;
+    };
     bool in_loop = false;
     auto cur_set = [&]() {
         int m0, n0, kb, ke, tm;
@@ -247,6 +255,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         cml = p.M - m0;
         cnl = p.N - n0;
         ckl = ke - kb;
+        cur_intr();
     };
     auto cur_adv = [&]() {
         ++ct;
@@ -254,11 +263,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             ca += a_step;
             cb += b_step;
             ckl -= BK;
+            if (ckl < BK) intr = 0u;  // ragged last K-tile
             return;
         }
         ckt = 0;
         if (++cli < my_items) cur_set();
-        else cml = cnl = ckl = 0;
+        else {
+            cml = cnl = ckl = 0;
+            intr = 0u;
+        }
     };
     const uint32_t lds0 = lds_addr(smem) + wave * 2048;  // this wave's 2 KiB of every slot
     auto issue_h = [&](auto hc) {
@@ -278,7 +291,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                 return;
             }
         }
-        if (mnl >= 128 && ckl >= BK) {  // interior half-tile: no per-lane checks
+        if (intr & (1u << H)) {  // interior half-tile: no per-lane checks
 #pragma unroll
             for (int i = 0; i < 2; ++i) dma16_at(rs, isA ? a_off[i] : b_off[i], dst + i * 1024);
         } else {
