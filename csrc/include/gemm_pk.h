@@ -381,6 +381,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                     for (int nh = 0; nh < 2; ++nh)
                         aux[i][nh] = __builtin_amdgcn_raw_buffer_load_b128(ars, off(mh, i, nh, 2), 0, 0);
+                // retire them HERE, in the branch that issued them (vmcnt(0); this epilogue drains the
+                // operand DMA anyway): with the wait left to the separately-branched consumers below,
+                // the compiler's wait insertion assumed the loads could still be pending at the main
+                // loop's head and put vmcnt(2) + vmcnt(0) into every K-tile's first phase
+                __builtin_amdgcn_s_waitcnt(0x0F70);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
