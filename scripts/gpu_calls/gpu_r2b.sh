@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 GPU call: parity vs recorded reference outputs, then GEMM PMC record (cfg 9 vs hipBLASLt).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 set -e

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 GPU call: attention head sizes 32/128 (MFMA) tests + determinism + refblock graph/dropout,
 # then attention A/B timings per head size.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 set -e

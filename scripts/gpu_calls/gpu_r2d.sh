@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 GPU call: full GPU test suite, GPT-2-small native-vs-fp32 100-step trajectory, N=1 bench.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 set -e

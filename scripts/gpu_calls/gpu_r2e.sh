@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 GPU call: stochastic-rounding test, trajectory with SR (b16, b64) and without (b16).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 set -e

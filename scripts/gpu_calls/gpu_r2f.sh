@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 GPU call: GPT-2-medium bf16 vs fp8 benches + kernel stats of the fp8 step.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof_fp8
 set -e

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 GPU call: GELU saved-derivative epilogues — tests + bench A/B (REPLICANN_MLP_GELU=pre = old path).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 set -e

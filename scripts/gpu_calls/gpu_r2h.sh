@@ -1,6 +1,6 @@
 #!/bin/bash
 # cfg 9 ablations (timing only, wrong outputs): 91 no DMA, 92 no vmcnt waits, 94 no epilogue, 98 DMA between k-steps
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 set -e
 for s in "8192 8192 8192 nt" "65536 2304 768 nt" "65536 768 3072 nt" "65536 768 50304 nn"; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # spread (deferred per-quadrant) epilogue in cfg 9: GEMM tests, per-shape A/B, bench A/B
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 set -e
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_ops_gpu.py tests/test_determinism_gpu.py tests/test_convergence_gpu.py > gpurun_out/spread_tests.log 2>&1

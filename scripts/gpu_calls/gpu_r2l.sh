@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 status call: benches of every BASELINE config + a GPT-2-small step kernel breakdown.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof_r2
 set -e
