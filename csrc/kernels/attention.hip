@@ -1328,10 +1328,7 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         // dropout in v2/v3, 3 blocks per CU
         const char* ev = std::getenv("REPLICANN_ATTN_FWD");
         const int var = ev ? std::atoi(ev) : 3;  // 3 = v2 + LEAN softmax bookkeeping
-        if (var == 5) {  // single-loop kernel, 4 query fragments (64 queries) per wave, occupancy 2
-            dim3 g5(B * H * ((Tq + 191) / 192));
-            RN_DISPATCH3V(attn_fwd64_k, g5, 32768, st, a, 64, 2, 3);
-        } else if (!bias && p_drop == 0.f && var >= 3) {
+        if (!bias && p_drop == 0.f && var >= 3) {
             if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
             else attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
         } else if (!bias && p_drop == 0.f && var == 2) {
