@@ -47,6 +47,10 @@ def main():
                          "global batch on 8 GPUs, sized for 288 GB HBM; 512 images ViT, 256 ResNet)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--ddp", default="auto", choices=["auto", "on"],
+                    help="on: run the data-parallel step (buckets, fp32 widening, collectives) even on 1 GPU")
+    ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch"],
+                    help="collective back-end: native RCCL communicator (csrc/comm) or torch.distributed")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra torch.profiler steps (not timed)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="capture the whole training step as one hipGraph (auto: on for 1 process)")
@@ -68,7 +72,7 @@ def main():
                       optimizer="adamw" if not args.model.startswith("resnet") else "sgd",
                       weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,
                       warmup_steps=10, lr=3e-4 if args.model.startswith("gpt2-medium") else 6e-4, bucket_mb=args.bucket_mb, log_every=10**9,
-                      graph=args.graph)
+                      graph=args.graph, ddp=args.ddp, comm=args.comm)
     tr = Trainer(cfg)
     world = tr.world
     dev = tr.device
@@ -136,6 +140,7 @@ def main():
             "optimizer": ("fused AdamW" if cfg.optimizer == "adamw" else "fused SGD-momentum")
             + " (fp32 master) + grad-norm clip",
             "hipgraph": tr._graph is not None,
+            "comm": (tr.ddp.comm.name if tr.ddp is not None else None),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         },
     }
@@ -147,6 +152,7 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

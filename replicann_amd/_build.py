@@ -29,6 +29,7 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "objs"
 OUT = Path(__file__).resolve().parent / "_C.so"
 ARCH = os.environ.get("REPLICANN_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 HIP_FLAGS = [
     f"--offload-arch={ARCH}",
@@ -148,7 +149,9 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
 def _build_locked(verbose, jobs):
     torch_inc, torch_lib = _torch_paths()
     hdr = _headers_digest()
-    srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "bindings").glob("*.cpp"))
+    # kernels (device code) + host-only bindings; csrc/comm is the native RCCL communicator
+    srcs = (sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "bindings").glob("*.cpp"))
+            + sorted((CSRC / "comm").glob("*.cpp")))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hdr, torch_inc), srcs))
@@ -161,7 +164,7 @@ def _build_locked(verbose, jobs):
     tmp = f"{OUT}.tmp.{os.getpid()}"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", tmp,
            f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-           f"-Wl,-rpath,{torch_lib}"]
+           f"-Wl,-rpath,{torch_lib}", f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

@@ -8,6 +8,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from .comm import NativeComm, TorchComm, make_comm
 from .ddp import DistributedDataParallel
 
 
@@ -17,8 +18,17 @@ def dist_env():
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
-def init_distributed(backend=None, timeout_s=600):
-    """Initialise torch.distributed from env:// if WORLD_SIZE>1.
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def init_distributed(backend=None, timeout_s=600, force=False):
+    """Initialise torch.distributed from env:// if WORLD_SIZE>1 (or ``force``: also a
+    one-process group, for the one-GPU rehearsal of the data-parallel step).
 
     GPU → backend "nccl" (RCCL over xGMI), one process per GPU, device =
     LOCAL_RANK.  CPU → "gloo".  Returns (rank, local_rank, world, device).
@@ -37,7 +47,11 @@ def init_distributed(backend=None, timeout_s=600):
     else:
         device = torch.device("cpu")
     use_gpu = gpu
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
+        if world == 1:
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         be = backend or ("nccl" if use_gpu else "gloo")
@@ -48,4 +62,4 @@ def init_distributed(backend=None, timeout_s=600):
     return rank, local_rank, world, device
 
 
-__all__ = ["DistributedDataParallel", "dist_env", "init_distributed"]
+__all__ = ["DistributedDataParallel", "NativeComm", "TorchComm", "dist_env", "init_distributed", "make_comm"]

@@ -1,0 +1,133 @@
+"""Collective back-ends for the data-parallel reducer (SURVEY.md §1 L1', N16).
+
+Two implementations of one small interface (``all_reduce`` / ``broadcast`` /
+``all_gather`` / ``reduce_scatter`` issue asynchronously, ``wait`` joins them into the
+caller's stream, ``synchronize`` blocks the host):
+
+* :class:`NativeComm` — the framework's own RCCL communicator
+  (``csrc/comm/rccl_comm.cpp``): collectives on a dedicated high-priority HIP comm
+  stream forked from the compute stream by an event, a watchdog thread that aborts a
+  hung or failed communicator, and hipGraph-capturable fork/join.  The ncclUniqueId is
+  drawn by rank 0 and exchanged over the ``torch.distributed`` rendezvous;
+* :class:`TorchComm` — ``torch.distributed`` async collectives (``nccl`` = RCCL on a
+  GPU, ``gloo`` on the CPU).  The CPU tests and gloo rehearsals run this one.
+
+``make_comm("auto")`` picks native for GPU tensors on an ``nccl`` process group and
+torch otherwise.  The reference has no collective code (``/root/reference/poetry.lock:1222``
+is its only NCCL touchpoint).
+"""
+
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+_OPS = {"sum": 0, "max": 1, "min": 2, "avg": 3}
+
+
+class TorchComm:
+    """``torch.distributed`` async collectives; ``wait`` waits on the outstanding works."""
+
+    name = "torch"
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._works = []
+
+    def all_reduce(self, t, op="sum"):
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        self._works.append(dist.all_reduce(t, op=rop, group=self.group, async_op=True))
+
+    def broadcast(self, t, root=0):
+        self._works.append(dist.broadcast(t, root, group=self.group, async_op=True))
+
+    def all_gather(self, inp, out):
+        self._works.append(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
+
+    def reduce_scatter(self, inp, out, op="sum"):
+        self._works.append(dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True))
+
+    def wait(self):
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+    synchronize = wait
+
+    def close(self):
+        self.wait()
+
+
+class NativeComm:
+    """The framework's RCCL communicator (``torch.ops.replicann.comm_*``) for one device."""
+
+    name = "native"
+
+    def __init__(self, group=None, device=None, timeout_s: float = 600.0):
+        from .. import _ext
+
+        self.ops = _ext.ops()
+        self.group = group
+        if dist.is_initialized():
+            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        uid = self.ops.comm_unique_id() if self.rank == 0 else None
+        if self.world > 1:  # rank 0's id over the existing rendezvous (a CPU object broadcast)
+            box = [bytes(uid.numpy()) if uid is not None else None]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group, device=self.device if _is_nccl(group) else None)
+            uid = torch.frombuffer(bytearray(box[0]), dtype=torch.uint8)
+        self.handle = int(self.ops.comm_init(uid, self.rank, self.world, self.device.index, float(timeout_s)))
+
+    def all_reduce(self, t, op="sum"):
+        self.ops.comm_all_reduce(self.handle, t, _OPS[op])
+
+    def broadcast(self, t, root=0):
+        self.ops.comm_broadcast(self.handle, t, root)
+
+    def all_gather(self, inp, out):
+        self.ops.comm_all_gather(self.handle, inp, out)
+
+    def reduce_scatter(self, inp, out, op="sum"):
+        self.ops.comm_reduce_scatter(self.handle, inp, out, _OPS[op])
+
+    def wait(self):
+        """The current stream waits for every collective issued so far (stream-ordered)."""
+        self.ops.comm_wait(self.handle)
+
+    def synchronize(self):
+        self.ops.comm_synchronize(self.handle)
+
+    def info(self):
+        r, w, n, b, failed = self.ops.comm_info(self.handle)
+        return {"rank": r, "world": w, "collectives": n, "bytes": b, "failed": bool(failed)}
+
+    def close(self):
+        if self.handle is not None:
+            self.ops.comm_destroy(self.handle)
+            self.handle = None
+
+
+def _is_nccl(group=None) -> bool:
+    return dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+
+def make_comm(kind: str = "auto", group=None, device=None, timeout_s: float = 600.0):
+    """``kind``: ``auto`` (env ``REPLICANN_COMM`` if set; else native on an nccl group),
+    ``native`` or ``torch``."""
+    if kind == "auto":
+        kind = os.environ.get("REPLICANN_COMM", "auto")
+    dev = torch.device(device) if device is not None else None
+    if kind == "auto":
+        kind = "native" if (_is_nccl(group) and (dev is None or dev.type == "cuda")) else "torch"
+    if kind == "native":
+        return NativeComm(group, dev, timeout_s)
+    if kind == "torch":
+        return TorchComm(group)
+    raise ValueError(f"unknown comm kind {kind!r} (auto | native | torch)")

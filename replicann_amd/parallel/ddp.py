@@ -36,7 +36,13 @@ parallelism at all; this is built MI355X-first:
   their slice is zero on every rank), and checks every bucket was reduced
   exactly once;
 * ``no_sync()`` disables reduction for gradient accumulation;
-* construction broadcasts rank 0's parameters and buffers (one flat broadcast).
+* construction broadcasts rank 0's parameters and buffers (one flat broadcast);
+* the collectives go through a :mod:`~replicann_amd.parallel.comm` back-end: on GPUs
+  over an ``nccl`` group the framework's own RCCL communicator (``csrc/comm``: a
+  high-priority comm stream forked/joined by events — hipGraph-capturable — plus a
+  hang/async-error watchdog), otherwise ``torch.distributed`` async works (gloo tests);
+* ``force=True`` keeps the reducer active at world size 1 (a one-GPU rehearsal of the
+  multi-GPU step: same widening copies, same collective calls, same stream joins).
 """
 
 from __future__ import annotations
@@ -49,20 +55,22 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..utils.flat import FlatParams
+from .comm import make_comm
 
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, flat: FlatParams, bucket_mb: float = 64.0,
                  process_group=None, broadcast: bool = True, check_unused: bool = False,
-                 reduce_dtype=torch.float32, split_tied: bool = True):
+                 reduce_dtype=torch.float32, split_tied: bool = True, comm="auto", force: bool = False):
         super().__init__()
         self.module = module
         self.flat = flat
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.active = self.world > 1 or force  # reduce at all (force: one-rank rehearsal)
         self.check_unused = check_unused
         self._sync = True
-        self._works = []
+        self.comm = make_comm(comm, process_group, flat.grad.device) if isinstance(comm, str) else comm
         if broadcast and self.world > 1:
             self._broadcast_state()
         self.reduce_dtype = reduce_dtype
@@ -111,16 +119,17 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------
     def _broadcast_state(self):
-        dist.broadcast(self.flat.data, 0, group=self.pg)
+        self.comm.broadcast(self.flat.data, 0)
         for b in self.module.buffers():
-            dist.broadcast(b.data, 0, group=self.pg)
+            if b.is_contiguous() and b.numel():
+                self.comm.broadcast(b.data, 0)
+        self.comm.wait()
 
     def _reset(self):
         self._pending = [b[2] for b in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
         self._next = 0
-        self._works = []
         self._seen = set()
         self._split_done = {k: 0 for k in self.split}  # contributions reduced this step
         self.launched_in_backward = 0
@@ -132,7 +141,7 @@ class DistributedDataParallel(nn.Module):
             dst = self.reduce_buf[lo:hi]
         if dst.data_ptr() != g.data_ptr():
             dst.copy_(g)  # stream-ordered after the kernels that produced the gradient
-        self._works.append(dist.all_reduce(dst, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        self.comm.all_reduce(dst)
 
     def _launch_ready(self, from_hook=False):
         while self._next < len(self.buckets) and self._ready[self._next]:
@@ -144,7 +153,7 @@ class DistributedDataParallel(nn.Module):
 
     def _contribution(self, p, final):
         """A direct gradient contribution to a split parameter is complete (``final``: its last)."""
-        if not self._sync or self.world == 1 or id(p) not in self.split:
+        if not self._sync or not self.active or id(p) not in self.split:
             return
         lo, hi, uses, sides = self.split[id(p)]
         k = self._split_done[id(p)]
@@ -161,12 +170,12 @@ class DistributedDataParallel(nn.Module):
         else:
             sides[k].copy_(g)
             g.zero_()
-            self._works.append(dist.all_reduce(sides[k], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+            self.comm.all_reduce(sides[k])
         self._split_done[id(p)] = k + 1
         self.launched_in_backward += 1
 
     def _hook(self, p):
-        if not self._sync or self.world == 1:
+        if not self._sync or not self.active:
             return
         if id(p) in self.split:
             return  # handled per contribution
@@ -194,7 +203,7 @@ class DistributedDataParallel(nn.Module):
 
     def finish(self):
         """Complete the gradient reduction (call after backward, before the optimizer)."""
-        if not self._sync or self.world == 1:
+        if not self._sync or not self.active:
             return
         t0 = time.perf_counter()
         unused = [i for i, r in enumerate(self._ready) if not r]
@@ -221,13 +230,11 @@ class DistributedDataParallel(nn.Module):
                 for s_ in unused_sides:
                     s_.zero_()
             self._split_done[pid] = uses
-        for w in self._works:
-            w.wait()
+        self.comm.wait()  # native: the compute stream joins the comm stream (no host sync)
         for pid, (lo, hi, uses, sides) in self.split.items():
             for s in sides:
                 self.reduce_buf[lo:hi].add_(s)
         assert all(self._launched), "a gradient bucket was never reduced"
-        self._works = []
         self.comm_wait_ms = (time.perf_counter() - t0) * 1e3
 
     @contextlib.contextmanager

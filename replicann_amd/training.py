@@ -81,6 +81,8 @@ class TrainConfig:
     grad_accum: int = 1
     max_grad_norm: float = 1.0
     bucket_mb: float = 64.0
+    ddp: str = "auto"             # auto (world > 1) | on (also at world 1: one-GPU rehearsal of the DDP step)
+    comm: str = "auto"            # auto (native RCCL communicator on GPUs, torch.distributed otherwise) | native | torch
     graph: str = "auto"           # auto | on | off — capture the whole step in one hipGraph
     log_every: int = 10
     metrics_path: str | None = None
@@ -100,7 +102,7 @@ class Trainer:
     def __init__(self, cfg: TrainConfig, model=None):
         self.cfg = cfg
         self.rank, self.local_rank, self.world, dev = init_distributed(
-            backend="gloo" if cfg.device == "cpu" else None)
+            backend="gloo" if cfg.device == "cpu" else None, force=cfg.ddp == "on")
         self.device = torch.device(cfg.device) if cfg.device else dev
         torch.manual_seed(cfg.seed)
         if self.device.type == "cuda":
@@ -114,7 +116,9 @@ class Trainer:
         for p in self.model.parameters():
             p.data = p.data.to(dtype)
         self.flat = FlatParams(self.model)
-        self.ddp = DistributedDataParallel(self.model, self.flat, cfg.bucket_mb) if self.world > 1 else None
+        use_ddp = self.world > 1 or cfg.ddp == "on"
+        self.ddp = (DistributedDataParallel(self.model, self.flat, cfg.bucket_mb, comm=cfg.comm, force=True)
+                    if use_ddp else None)
         gs = 1.0 / self.world
         if cfg.optimizer == "adamw":
             self.opt = FusedAdamW(self.flat, lr=cfg.lr, weight_decay=cfg.weight_decay,
@@ -222,8 +226,9 @@ class Trainer:
             return True
         # auto: single process (dropout seeds are drawn on the device — ops/rng.py — so stochastic
         # models capture too; multi-rank steps run eager: N=1 eager vs graph measured within 0.3 %,
-        # profiles/graph_vs_eager_r2.txt)
-        return self.world == 1
+        # profiles/graph_vs_eager_r2.txt).  A one-rank DDP rehearsal captures only with the
+        # native communicator (its fork/join is capturable; torch's async works are not).
+        return self.world == 1 and (self.ddp is None or self.ddp.comm.name == "native")
 
     def _capture(self):
         """Capture zero_grad → fwd → bwd → (all-reduce) → optimizer as ONE hipGraph.
