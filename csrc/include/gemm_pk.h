@@ -173,8 +173,21 @@ constexpr int pk_epi_stores() {
 // issues the DMA between the two k-steps' MFMAs, bit 4 issues every main-loop DMA instruction with
 // an out-of-range offset (same instructions, no memory traffic, no LDS writes), bit 5 issues each
 // half-tile's DMA with the SAME descriptor every phase (no per-phase descriptor rebuild).
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0>
+// FP8: e4m3 operands, both K-contiguous (the forward x·Wᵀ), staged as "bf16 pairs" (K, lda, ldb
+// in 2-byte units, so the DMA stream, the LDS images and the fragment reads are byte-identical to
+// the bf16 kernel's); each phase's two k-step fragments of a row (16 B each) are concatenated into
+// the 32-B operand of ONE v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales, the per-tensor
+// scales in alpha).  A and B use the same byte→k mapping, so the permutation of k inside the
+// 128-deep step cancels in the dot product.  8 scaled MFMAs (2x the cycles of a bf16 16x16x32
+// each) per phase instead of 16: the same MFMA time per staged byte, i.e. twice the FLOP rate.
+RN_DEV i32x8 pk_cat8(const s16x8 a, const s16x8 b) {
+    const i32x4 x = __builtin_bit_cast(i32x4, a), y = __builtin_bit_cast(i32x4, b);
+    return (i32x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+}
+
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
+    static_assert(!FP8 || (AK && BKC && !(DBG & 8)), "fp8: K-contiguous operands only");
     constexpr int BM = 256, BN = 256;
     constexpr int S_EPI = pk_epi_stores<ACT, SPLIT, F32>();
     static_assert(6 + S_EPI <= 63, "vmcnt range");
@@ -551,10 +564,18 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         __builtin_amdgcn_sched_barrier(0);
     };
 #define RN_PK_MMA(MH, NH, BF)                                                                          \
+    if constexpr (FP8) {                                                                               \
+        _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                             \
+        _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                             \
+            acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(                   \
+                pk_cat8(BF[j_][0], BF[j_][1]), pk_cat8(Af[i_][0], Af[i_][1]), acc[MH][NH][i_][j_], 0, 0, 0, \
+                127, 0, 127);                                                                          \
+    } else {                                                                                           \
     _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                 \
     _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                                 \
-        acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j_][s_], Af[i_][s_], acc[MH][NH][i_][j_], 0, 0, 0);
+        acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j_][s_], Af[i_][s_], acc[MH][NH][i_][j_], 0, 0, 0); \
+    }
 
 #define RN_PK_MMA_S(MH, NH, BF, S)                                                                    \
     _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                 \
@@ -640,9 +661,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 }
 
 // Launch: persistent grid of min(items, 256 × blocks-per-CU) workgroups (1 per CU: 128 KiB LDS).
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0>
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false>
 void launch_pk_t(GemmArgs& a, hipStream_t st) {
-    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG>;
+    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8>;
     static int attr_dev = -1;  // the >64 KiB LDS opt-in, per device the process launches on
     int dev = 0;
     (void)hipGetDevice(&dev);

@@ -8,6 +8,8 @@
 // * the GEMM runs on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales:
 //   2x the bf16 MFMA rate per clock (MI355X_MICROARCH.md §Matrix cores), with the
 //   product of the two tensor scales applied as the epilogue alpha.
+#include <cstdlib>
+
 #include "gemm_impl.h"
 
 namespace {
@@ -111,7 +113,19 @@ inline int gridn(long n) {
     return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
+// REPLICANN_FP8_GEMM=0: the one-tile-per-block 256x192 kernel (A/B only); default 9 (persistent)
+int fp8_gemm_kernel() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("REPLICANN_FP8_GEMM");
+        v = (e && e[0] == '0') ? 0 : 9;
+    }
+    return v;
+}
+
 }  // namespace
+
+void rn_gemm_launch_pk_fp8(rn_gemm_detail::GemmArgs& a, int act, hipStream_t st);
 
 extern "C" {
 
@@ -144,6 +158,12 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     a.M = M; a.N = N; a.K = K / 2; a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
     a.split = 1; a.k_per_split = ((K / 2) + 63) / 64 * 64; a.out_f32 = 0; a.accumulate = 0;
     using namespace rn_gemm_detail;
+    if (fp8_gemm_kernel() == 9) {  // persistent 256x256 half-tile stream (gemm_pk<.., FP8>), default
+        a.tiles_m = (M + 255) / 256;
+        a.tiles_n = (N + 255) / 256;
+        rn_gemm_launch_pk_fp8(a, act, st);
+        return 0;
+    }
     if (act == ACT_GELU) launch_fp8_t<256, 192, 2, 4, ACT_GELU>(a, st);
     else if (act == ACT_GELU_D) launch_fp8_t<256, 192, 2, 4, ACT_GELU_D>(a, st);
     else if (act == ACT_RELU) launch_fp8_t<256, 192, 2, 4, ACT_RELU>(a, st);
