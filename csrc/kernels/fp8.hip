@@ -113,14 +113,11 @@ inline int gridn(long n) {
     return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
-// REPLICANN_FP8_GEMM=0: the one-tile-per-block 256x192 kernel (A/B only); default 9 (persistent)
+// REPLICANN_FP8_GEMM: unset = by shape, 0 = one-tile-per-block 256x192, 9 = persistent 256x256
 int fp8_gemm_kernel() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("REPLICANN_FP8_GEMM");
-        v = (e && e[0] == '0') ? 0 : 9;
-    }
-    return v;
+    const char* e = std::getenv("REPLICANN_FP8_GEMM");
+    if (!e || !e[0]) return -1;  // by shape
+    return e[0] == '0' ? 0 : 9;
 }
 
 }  // namespace
@@ -158,7 +155,13 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     a.M = M; a.N = N; a.K = K / 2; a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
     a.split = 1; a.k_per_split = ((K / 2) + 63) / 64 * 64; a.out_f32 = 0; a.accumulate = 0;
     using namespace rn_gemm_detail;
-    if (fp8_gemm_kernel() == 9) {  // persistent 256x256 half-tile stream (gemm_pk<.., FP8>), default
+    // persistent 256x256 half-tile stream (gemm_pk<.., FP8>): its epilogue stores 8 contiguous
+    // columns per lane, so it takes N % 8 == 0 and ldc % 8 == 0 only.  Measured on the GPT-2-medium
+    // b64 shapes (profiles/fp8_gemm_ab_r2r.txt): it wins at K = 4096 (1.94 vs 1.85 PF/s) and loses
+    // at K = 1024 (1.32 vs 1.59 PF/s: 8 K-tiles per output tile, the per-tile epilogue dominates),
+    // so by default it takes K >= 2048 only; REPLICANN_FP8_GEMM=9 forces it, =0 never.
+    const int kern = fp8_gemm_kernel();
+    if (N % 8 == 0 && ldc % 8 == 0 && (kern == 9 || (kern < 0 && K >= 2048))) {
         a.tiles_m = (M + 255) / 256;
         a.tiles_n = (N + 255) / 256;
         rn_gemm_launch_pk_fp8(a, act, st);

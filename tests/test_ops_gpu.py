@@ -661,6 +661,32 @@ def test_gemm_fp8_matches_dequantized_reference(cuda, M, N, K):
     assert rel_err(out, a.float() @ b.float().t()) < 0.08  # vs the unquantised product
 
 
+@pytest.mark.parametrize("act", [0, 2, 5])
+@pytest.mark.parametrize("M,N,K", [(1000, 1100, 1040), (4096, 3072, 1024)])
+def test_gemm_fp8_persistent_vs_tile_kernel(cuda, monkeypatch, M, N, K, act):
+    """The persistent 256x256 fp8 kernel (default) against the one-tile-per-block 256x192 one:
+    same operands, same epilogue (bias + GELU / GELU with saved derivative); tails in M, N, K."""
+    torch.manual_seed(23)
+    a, b = bf(M, K), bf(N, K, scale=0.2)
+    bias = bf(N, scale=0.1)
+    qa, sa = ops.quantize_fp8(a)
+    qb, sb = ops.quantize_fp8(b)
+    outs = []
+    for kern in ("9", "0"):
+        monkeypatch.setenv("REPLICANN_FP8_GEMM", kern)
+        pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if act == 5 else None
+        o = torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, None, act, pre)
+        outs.append((o, pre))
+    torch.cuda.synchronize()
+    ref = ops.dequantize_fp8(qa, sa).float() @ ops.dequantize_fp8(qb, sb).float().t() + bias.float()
+    if act:
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    assert rel_err(outs[0][0], ref) < 1e-2
+    assert rel_err(outs[0][0], outs[1][0]) < 5e-3
+    if act == 5:
+        assert rel_err(outs[0][1], outs[1][1]) < 5e-3
+
+
 def test_linear_fp8_autograd(cuda):
     torch.manual_seed(22)
     x = bf(4, 64, 256).requires_grad_()
