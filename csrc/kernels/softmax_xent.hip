@@ -6,6 +6,8 @@
 // one rescale per 8 elements) and stores only the per-row lse + NLL; backward
 // writes (softmax - onehot) * g / n in place over the logits, zero in the
 // padded columns [n_valid, V).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -190,6 +192,99 @@ __global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, co
     }
 }
 
+// Fused-gradient row kernel, v2 (the default for V % 8 == 0, V <= 8·1024·CH, write_grad):
+//   * ONE block reduction: each thread reduces its registers to a local (max, Σ exp) pair first,
+//     the pairs are merged across the block (m, s) ⊕ (m', s') = (M, s·2^(m-M) + s'·2^(m'-M));
+//   * ONE exponential per element: the exp2 of the local pass is kept (as bf16, over the logits
+//     in registers) and the gradient is e · 2^(m_local - lse): a multiply, not a second exp;
+//   * base-2 throughout (x·log2e folded into one FMA with the max), padded-column and target
+//     masks only where a chunk straddles them.
+// Output differs from xent_row_k by the extra bf16 rounding of e (≤ 1 bf16 ulp of the gradient).
+template <int CH>
+__global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                    float* __restrict__ loss, float* __restrict__ lse_out, int V,
+                                                    int nvalid, long ignore) {
+    constexpr float L2E = 1.4426950408889634f;
+    __shared__ float sm_m[16], sm_s[16];
+    bf16* row = logits + (long)blockIdx.x * V;
+    const int n8 = V / 8;
+    const long t = tgt[blockIdx.x];
+    const bool ign = (t == ignore || t < 0 || t >= nvalid);
+    RN_CHECK(t == ignore || (t >= 0 && t < nvalid));
+    const float xt = ign ? 0.f : bf2f(row[t]);
+    bf16x8 v[CH];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        if (i < n8) {
+            v[k] = *reinterpret_cast<const bf16x8*>(row + i * 8);
+            if (i * 8 + 8 <= nvalid) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m = fmaxf(m, (float)v[k][j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (i * 8 + j < nvalid) m = fmaxf(m, (float)v[k][j]);
+            }
+        }
+    }
+    const float mL = (m == -INFINITY) ? 0.f : m * L2E;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        if (i < n8) {
+            bf16x8 e;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x = (i * 8 + j < nvalid) ? exp2f(fmaf((float)v[k][j], L2E, -mL)) : 0.f;
+                s += x;
+                e[j] = (bf16)x;
+            }
+            v[k] = e;
+        }
+    }
+    // block merge of (m, s): wave butterfly, then the 16 wave results (every thread, same order)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+        const float M = fmaxf(m, m2);
+        s = (M == -INFINITY) ? 0.f : s * exp2f((m - M) * L2E) + s2 * exp2f((m2 - M) * L2E);
+        m = M;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        sm_m[wid] = m;
+        sm_s[wid] = s;
+    }
+    __syncthreads();
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) M = fmaxf(M, sm_m[w]);
+    float S = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) S += sm_s[w] * exp2f((sm_m[w] - M) * L2E);
+    const float lse = M + __logf(S);
+    if (threadIdx.x == 0) {
+        lse_out[blockIdx.x] = lse;
+        loss[blockIdx.x] = ign ? 0.f : lse - xt;
+    }
+    // this thread's e values were taken relative to ITS local max (mL): rescale to the row's lse
+    const float f = ign ? 0.f : exp2f(mL - lse * L2E);
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        if (i < n8) {
+            float g[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] = (float)v[k][j] * f;
+            if (!ign && t >= (long)i * 8 && t < (long)i * 8 + 8) g[t - (long)i * 8] -= 1.f;
+            store8(row + i * 8, g);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(TPB) xent_bwd_k(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                   const float* __restrict__ lse, const float* __restrict__ gscale,
                                                   bf16* __restrict__ grad, int V, int nvalid, long ignore) {
@@ -233,7 +328,11 @@ void rn_xent_fwd(void* logits, const int64_t* tgt, float* loss, float* lse, int 
                  int write_grad, hipStream_t st) {
     if (V % 8 == 0 && V <= 8 * 1024 * 8) {
         const int ch = (V / 8 + 1023) / 1024;
-#define RN_XR(C) { if (write_grad) xent_row_k<C, true><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
+        // REPLICANN_XENT=1: the round-1 row kernel (two block reductions, two exps per element)
+        const char* ev = std::getenv("REPLICANN_XENT");
+        const bool v2 = !(ev && ev[0] == '1');
+#define RN_XR(C) { if (write_grad && v2) xent_row2_k<C><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
+                   else if (write_grad) xent_row_k<C, true><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
                    else xent_row_k<C, false><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); }
         if (ch <= 1) RN_XR(1) else if (ch <= 2) RN_XR(2) else if (ch <= 4) RN_XR(4) else if (ch <= 7) RN_XR(7)
         else RN_XR(8)

@@ -293,6 +293,35 @@ def test_cross_entropy_padded(cuda):
     assert lg.grad[:, nv:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("kern", ["2", "1"])
+def test_fused_lm_xent_rows_gpt2_vocab(cuda, monkeypatch, kern):
+    """The in-place gradient row kernels at GPT-2's padded vocab (50304 columns, 50257 valid):
+    v2 (one block reduction, one exp per element; default) and the round-1 kernel (=1)."""
+    monkeypatch.setenv("REPLICANN_XENT", kern)
+    torch.manual_seed(8)
+    N, V, nv = 96, 50304, 50257
+    logits = bf(N, V, scale=4.0)
+    tgt = torch.randint(0, nv, (N,), device="cuda")
+    tgt[5] = -100
+    tgt[7] = nv - 1
+    tgt[9] = 0
+    g = logits.clone()
+    loss_rows, lse = torch.ops.replicann.xent_fwd(g, tgt, nv, -100, True)
+    lf = logits.float()[:, :nv]
+    ref_lse = torch.logsumexp(lf, 1)
+    ref_rows = F.cross_entropy(lf, tgt.clamp(min=0), reduction="none")
+    ref_rows[5] = 0
+    ref_g = torch.softmax(lf, 1)
+    ref_g[torch.arange(N), tgt.clamp(min=0)] -= 1
+    ref_g[5] = 0
+    torch.cuda.synchronize()
+    assert (lse - ref_lse).abs().max().item() < 1e-3
+    assert (loss_rows - ref_rows).abs().max().item() < 2e-2
+    assert (g[:, :nv].float() - ref_g).abs().max().item() < 4e-3
+    assert rel_err(g[:, :nv], ref_g) < 1e-2
+    assert g[:, nv:].abs().max().item() == 0 and g[5].abs().max().item() == 0
+
+
 # ----------------------------------------------------------------- attention
 def _attn_check(B, T, H, D, causal, bias=None, Tk=None, tol=2e-2):
     Tk = Tk or T
