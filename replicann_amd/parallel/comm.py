@@ -125,7 +125,15 @@ def make_comm(kind: str = "auto", group=None, device=None, timeout_s: float = 60
         kind = os.environ.get("REPLICANN_COMM", "auto")
     dev = torch.device(device) if device is not None else None
     if kind == "auto":
-        kind = "native" if (_is_nccl(group) and (dev is None or dev.type == "cuda")) else "torch"
+        if _is_nccl(group) and (dev is None or dev.type == "cuda"):
+            try:
+                return NativeComm(group, dev, timeout_s)
+            except Exception as e:  # e.g. extension built without RCCL: same collectives via torch
+                import warnings
+
+                warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
+                return TorchComm(group)
+        kind = "torch"
     if kind == "native":
         return NativeComm(group, dev, timeout_s)
     if kind == "torch":

@@ -132,6 +132,7 @@ class Trainer:
         self.opt.set_schedule(cfg.warmup_steps, max(cfg.steps, 1), cfg.min_lr_ratio)
         self.step_idx = 0
         self._graph = None
+        self._tuned = False
         self._resume_state = None
         if cfg.resume:
             self.step_idx, _, self._resume_state = load_checkpoint(cfg.resume, self.model, self.opt)
@@ -218,6 +219,30 @@ class Trainer:
             self.opt.step(lr)
         return loss.detach()
 
+    def _tune(self):
+        """Multi-rank GPU runs: time every GEMM shape of the step (the runtime autotuner picks
+        configs on the first eager call of a shape) in one forward + backward with the reducer
+        suspended, before the first real step — otherwise those timings would run beside the
+        first step's RCCL all-reduces and pick configs on a busy device.  The pass is invisible
+        to training: a fresh copy of the data source supplies the batch, and gradients, optimizer
+        state, buffers and the device RNG streams are restored afterwards."""
+        self._tuned = True
+        if self.device.type != "cuda" or self.ddp is None:
+            return
+        from .ops import rng as dev_rng
+        probe = self._make_data()
+        x, y = next(probe)
+        del probe
+        state = self.opt.state_tensors() + list(self.model.buffers()) + dev_rng.state_tensors(self.device)
+        snap = [t.clone() for t in state]
+        with self.ddp.no_sync(), self.timer.paused():
+            self.opt.zero_grad()
+            self.net(x, y).backward()
+        self.opt.zero_grad()
+        for t, v in zip(state, snap):
+            t.copy_(v)
+        torch.cuda.synchronize(self.device)
+
     def graph_enabled(self):
         c = self.cfg
         if c.graph == "off" or self.device.type != "cuda":
@@ -268,6 +293,8 @@ class Trainer:
 
         ``lr`` (eager mode only) overrides the device-side schedule."""
         c = self.cfg
+        if not self._tuned:
+            self._tune()
         if lr is None and self.graph_enabled():
             if self._graph is None:
                 self._capture()

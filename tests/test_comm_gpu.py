@@ -115,12 +115,13 @@ def test_native_comm_graph_capture():
         c.close()
 
 
-def _run(cfg_kw, steps=4):
+def _run(cfg_kw, steps=4, skip_tune=False):
     from replicann_amd.training import TrainConfig, Trainer
 
     cfg = TrainConfig(model="gpt2-tiny", batch_size=4, seq_len=128, steps=100, warmup_steps=1, lr=1e-3,
                       log_every=10**9, bucket_mb=0.5, seed=3, **cfg_kw)
     tr = Trainer(cfg)
+    tr._tuned = tr._tuned or skip_tune
     losses = [float(tr.step()) for _ in range(steps)]
     torch.cuda.synchronize()
     out = (losses, tr.flat.data.float().clone(), tr._graph is not None,
@@ -150,3 +151,11 @@ def test_ddp_step_native_graph_matches_eager(one_rank_pg):
     gr_l, gr_w, gr_g, gr_c, _ = _run(dict(graph="auto", ddp="on", comm="native"))
     assert gr_c == "native" and gr_g and not eag_g  # the whole DDP step replays as one hipGraph
     assert eag_l == gr_l and torch.equal(eag_w, gr_w)
+
+
+def test_ddp_pre_step_tuning_pass_is_invisible(one_rank_pg):
+    """The reducer-suspended autotuning pass before the first DDP step changes nothing the
+    training sees (batch stream, gradients, optimizer state, RNG)."""
+    a_l, a_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"))
+    b_l, b_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"), skip_tune=True)
+    assert a_l == b_l and torch.equal(a_w, b_w)
