@@ -33,7 +33,8 @@ void rn_add(const void*, const void*, void*, long, int, hipStream_t);
 void rn_bias_act_grad(const void*, const void*, void*, float*, void*, float*, int, int, int, int, int, hipStream_t);
 int rn_bias_act_grad_splits(int, int);
 int rn_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
-              hipStream_t);
+              hipStream_t, void*, float*);
+void rn_fp8_roll(float*, hipStream_t);
 int rn_ln_bwd_waves(int);
 long rn_ln_bwd_ws(int, int);
 int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
@@ -446,10 +447,31 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const 
     Tensor rstd = at::empty({M}, x.options().dtype(at::kFloat));
     if (M) {
         int rc = rn_ln_fwd(x.data_ptr(), optr(r), w.data_ptr(), optr(b), y.data_ptr(), h.data_ptr(), mean.data_ptr<float>(),
-                           rstd.data_ptr<float>(), M, E, (float)eps, cur_stream());
+                           rstd.data_ptr<float>(), M, E, (float)eps, cur_stream(), nullptr, nullptr);
         TORCH_CHECK(rc == 0, "layernorm: E must be a multiple of 8 and <= 8192, got ", E);
     }
     return {y, h, mean, rstd};
+}
+// LayerNorm whose output also comes out as e4m3 for the consumer's fp8 GEMM: `state` is that
+// GEMM's activation Fp8State slot (delayed scaling: rolled here, amax recorded by the kernel)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> layernorm_fwd_q8(const Tensor& x, const optional<Tensor>& r,
+                                                                    const Tensor& w, const optional<Tensor>& b,
+                                                                    double eps, const Tensor& state) {
+    CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); GUARD(x);
+    TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda() && state.is_contiguous());
+    const int M = x.size(0), E = x.size(1);
+    Tensor y = at::empty_like(x);
+    Tensor h = (r && r->defined()) ? at::empty_like(x) : x;
+    Tensor mean = at::empty({M}, x.options().dtype(at::kFloat));
+    Tensor rstd = at::empty({M}, x.options().dtype(at::kFloat));
+    Tensor q = at::empty(x.sizes(), x.options().dtype(at::kByte));
+    rn_fp8_roll(state.data_ptr<float>(), cur_stream());
+    if (M) {
+        int rc = rn_ln_fwd(x.data_ptr(), optr(r), w.data_ptr(), optr(b), y.data_ptr(), h.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), M, E, (float)eps, cur_stream(), q.data_ptr(), state.data_ptr<float>());
+        TORCH_CHECK(rc == 0, "layernorm: E must be a multiple of 8 and <= 8192, got ", E);
+    }
+    return {y, h, mean, rstd, q};
 }
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optional<Tensor>& gh, const Tensor& h,
                                                  const Tensor& w, const Tensor& mean, const Tensor& rstd,
@@ -917,6 +939,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("xent_fwd(Tensor(a!) logits, Tensor target, int nvalid, int ignore, bool write_grad=False) -> (Tensor, Tensor)");
     m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale, Tensor(a!) grad, int nvalid, int ignore) -> ()");
     m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("layernorm_fwd_q8(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps, Tensor(a!) state) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd, "
           "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None, Tensor(c!)? dxs_accum=None) -> (Tensor, Tensor, Tensor)");
     m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
@@ -974,6 +997,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("xent_fwd", &xent_fwd);
     m.impl("xent_bwd", &xent_bwd);
     m.impl("layernorm_fwd", &layernorm_fwd);
+    m.impl("layernorm_fwd_q8", &layernorm_fwd_q8);
     m.impl("layernorm_bwd", &layernorm_bwd);
     m.impl("embedding_fwd", &embedding_fwd);
     m.impl("embedding_bwd", &embedding_bwd);

@@ -139,6 +139,9 @@ void rn_fp8_quantize_delayed(const void* x, long n, void* q, float* state, hipSt
     quant_delayed_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
 
+// The delayed-scaling roll alone (for producers that quantise inside their own kernel).
+void rn_fp8_roll(float* state, hipStream_t st) { fp8_roll_k<<<1, 1, 0, st>>>(state); }
+
 void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
     dequant_k<<<gridn(n), 256, 0, st>>>((const uint8_t*)q, n, state, (bf16*)y);
 }

@@ -12,59 +12,91 @@
 
 namespace {
 
-template <int NV, bool RES, bool BIAS>
+// Q8: also write the output as OCP e4m3 (q8 = y / st8[0], saturating) for the consumer's fp8
+// GEMM and record amax(|y|) in st8[1] (delayed scaling, ops/fp8.py: the scale was rolled from the
+// previous amax just before this launch) — the consumer's separate quantisation pass (read y,
+// write q) is gone.  Rows are grid-strided so the amax costs one atomic per block.
+template <int NV, bool RES, bool BIAS, bool Q8 = false>
 __global__ void __launch_bounds__(256) ln_fwd_k(const bf16* __restrict__ x, const bf16* __restrict__ r,
                                                 const bf16* __restrict__ w, const bf16* __restrict__ b,
                                                 bf16* __restrict__ y, bf16* __restrict__ hout,
                                                 float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                int M, int E, float eps) {
+                                                int M, int E, float eps, uint8_t* __restrict__ q8 = nullptr,
+                                                float* __restrict__ st8 = nullptr) {
+    constexpr float E4M3_MAX = 448.f;
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= M) return;
     const int nvec = E / 8;
-    const bf16* xr = x + (long)row * E;
-    float v[NV][8];
-    float s = 0.f;
+    [[maybe_unused]] float amax = 0.f, inv8 = 0.f;
+    if constexpr (Q8) inv8 = 1.f / st8[0];
+    for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
+        const bf16* xr = x + (long)row * E;
+        float v[NV][8];
+        float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int c = (lane + i * 64);
-        if (c < nvec) {
-            load8(xr + c * 8, v[i]);
-            if constexpr (RES) {
-                float t[8];
-                load8(r + (long)row * E + c * 8, t);
+        for (int i = 0; i < NV; ++i) {
+            int c = (lane + i * 64);
+            if (c < nvec) {
+                load8(xr + c * 8, v[i]);
+                if constexpr (RES) {
+                    float t[8];
+                    load8(r + (long)row * E + c * 8, t);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[i][j] += t[j];
-                store8(hout + (long)row * E + c * 8, v[i]);
+                    for (int j = 0; j < 8; ++j) v[i][j] += t[j];
+                    store8(hout + (long)row * E + c * 8, v[i]);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s += v[i][j];
             }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s += v[i][j];
         }
-    }
-    const float mu = wave_sum(s) / E;
-    float q = 0.f;
+        const float mu = wave_sum(s) / E;
+        float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int c = lane + i * 64;
-        if (c < nvec) {
+        for (int i = 0; i < NV; ++i) {
+            int c = lane + i * 64;
+            if (c < nvec) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { float d = v[i][j] - mu; q += d * d; }
+                for (int j = 0; j < 8; ++j) { float d = v[i][j] - mu; q += d * d; }
+            }
         }
-    }
-    const float rs = rsqrtf(wave_sum(q) / E + eps);
+        const float rs = rsqrtf(wave_sum(q) / E + eps);
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int c = lane + i * 64;
-        if (c < nvec) {
-            float wf[8], bfv[8], o[8];
-            load8(w + c * 8, wf);
-            if constexpr (BIAS) load8(b + c * 8, bfv);
+        for (int i = 0; i < NV; ++i) {
+            int c = lane + i * 64;
+            if (c < nvec) {
+                float wf[8], bfv[8], o[8];
+                load8(w + c * 8, wf);
+                if constexpr (BIAS) load8(b + c * 8, bfv);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mu) * rs * wf[j] + (BIAS ? bfv[j] : 0.f);
-            store8(y + (long)row * E + c * 8, o);
+                for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mu) * rs * wf[j] + (BIAS ? bfv[j] : 0.f);
+                store8(y + (long)row * E + c * 8, o);
+                if constexpr (Q8) {
+                    float f[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {  // from the stored bf16 y: same bytes as a separate pass
+                        const float yb = bf2f(f2bf(o[j]));
+                        amax = fmaxf(amax, fabsf(yb));
+                        f[j] = fminf(fmaxf(yb * inv8, -E4M3_MAX), E4M3_MAX);
+                    }
+                    int w0 = 0, w1 = 0;
+                    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w0, false);
+                    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+                    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
+                    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+                    *reinterpret_cast<int2*>(q8 + (long)row * E + c * 8) = make_int2(w0, w1);
+                }
+            }
         }
+        if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
     }
-    if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+    if constexpr (Q8) {
+        __shared__ float am[4];
+        amax = wave_max(amax);
+        if (lane == 0) am[threadIdx.x >> 6] = amax;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<int*>(st8 + 1),
+                      __float_as_int(fmaxf(fmaxf(am[0], am[1]), fmaxf(am[2], am[3]))));
+    }
 }
 
 // One row per wave; each block folds its 4 waves' column partials in LDS and
@@ -179,10 +211,22 @@ extern "C" {
 
 int rn_ln_nv(int E) { return (E / 8 + 63) / 64; }
 
+// q8 / st8 (optional): fused e4m3 output with delayed scaling (st8 already rolled by the caller)
 int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* y, void* h, float* mean,
-              float* rstd, int M, int E, float eps, hipStream_t st) {
+              float* rstd, int M, int E, float eps, hipStream_t st, void* q8, float* st8) {
     if (E % 8 != 0 || E > 8192) return -1;
     int nv = rn_ln_nv(E);
+    if (q8) {
+        dim3 grid((M + 3) / 4 < 1024 ? (M + 3) / 4 : 1024);
+#define RN_LNF(NV, R, B) ln_fwd_k<NV, R, B, true><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)r, (const bf16*)w, (const bf16*)b, (bf16*)y, (bf16*)h, mean, rstd, M, E, eps, (uint8_t*)q8, st8)
+#define RN_LNF2(NV) { if (r) { if (b) RN_LNF(NV, true, true); else RN_LNF(NV, true, false); } \
+                      else { if (b) RN_LNF(NV, false, true); else RN_LNF(NV, false, false); } }
+        if (nv <= 1) RN_LNF2(1) else if (nv <= 2) RN_LNF2(2) else if (nv <= 4) RN_LNF2(4) else if (nv <= 8) RN_LNF2(8)
+        else RN_LNF2(16)
+#undef RN_LNF2
+#undef RN_LNF
+        return 0;
+    }
     dim3 grid((M + 3) / 4);
 #define RN_LNF(NV, R, B) ln_fwd_k<NV, R, B><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)r, (const bf16*)w, (const bf16*)b, (bf16*)y, (bf16*)h, mean, rstd, M, E, eps)
 #define RN_LNF2(NV) { if (r) { if (b) RN_LNF(NV, true, true); else RN_LNF(NV, true, false); } \

@@ -54,17 +54,18 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(n))
         self.eps = eps
 
-    def forward(self, x, return_sum=False, producer_bias=None):
+    def forward(self, x, return_sum=False, producer_bias=None, fp8=None):
         return ops.layer_norm(x, self.weight, self.bias, self.eps, return_sum=return_sum,
-                              producer_bias=producer_bias)
+                              producer_bias=producer_bias, fp8=fp8)
 
 
 class Attention(nn.Module):
-    def __init__(self, n_embd, n_head, causal, attn_dropout=0.0, resid_dropout=0.0, n_layer=12, fp8=False):
+    def __init__(self, n_embd, n_head, causal, attn_dropout=0.0, resid_dropout=0.0, n_layer=12, fp8=False,
+                 fp8_proj=True):
         super().__init__()
         self.n_head, self.causal = n_head, causal
         self.c_attn = Linear(n_embd, 3 * n_embd, fp8=fp8)
-        self.c_proj = Linear(n_embd, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
+        self.c_proj = Linear(n_embd, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8 and fp8_proj)
         self.attn_dropout, self.resid_dropout = attn_dropout, resid_dropout
 
     def out_bias(self):
@@ -84,10 +85,10 @@ class Attention(nn.Module):
 
 
 class MLP(nn.Module):
-    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12, fp8=False):
+    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12, fp8=False, fp8_proj=True):
         super().__init__()
         self.c_fc = Linear(n_embd, hidden, fp8=fp8)
-        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
+        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8 and fp8_proj)
         self.dropout = dropout
 
     def out_bias(self):
@@ -104,12 +105,13 @@ class MLP(nn.Module):
 
 
 class PreLNBlock(nn.Module):
-    def __init__(self, n_embd, n_head, causal, mlp_ratio=4, dropout=0.0, n_layer=12, eps=1e-5, fp8=False):
+    def __init__(self, n_embd, n_head, causal, mlp_ratio=4, dropout=0.0, n_layer=12, eps=1e-5, fp8=False,
+                 fp8_proj=True):
         super().__init__()
         self.ln_1 = LayerNorm(n_embd, eps)
-        self.attn = Attention(n_embd, n_head, causal, dropout, dropout, n_layer, fp8=fp8)
+        self.attn = Attention(n_embd, n_head, causal, dropout, dropout, n_layer, fp8=fp8, fp8_proj=fp8_proj)
         self.ln_2 = LayerNorm(n_embd, eps)
-        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer, fp8=fp8)
+        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer, fp8=fp8, fp8_proj=fp8_proj)
 
     def out_bias(self):
         return self.mlp.out_bias()
@@ -117,8 +119,9 @@ class PreLNBlock(nn.Module):
     def forward(self, x, prev_bias=None):
         """``prev_bias``: out_bias() of the block that produced x (its gradient is
         then reduced inside ln_1's backward kernel)."""
-        h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias)
+        # fp8 blocks: the LayerNorms also emit the e4m3 input of c_attn / c_fc
+        h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias, fp8=self.attn.c_attn.fp8_state)
         x = self.attn(h, residual=x)
-        h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias())
+        h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias(), fp8=self.mlp.c_fc.fp8_state)
         x = self.mlp(h, residual=x)
         return x

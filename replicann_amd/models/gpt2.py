@@ -36,6 +36,11 @@ class GPT2Config:
     dropout: float = 0.0
     ln_eps: float = 1e-5
     fp8: bool = False  # fp8 e4m3 forward GEMMs in the transformer blocks ("fp8 weights" config)
+    # fp8 also for the two output projections (attention c_proj, MLP c_proj).  Off by default: their
+    # inputs (attention output, GELU output) would need a separate quantisation pass that costs what
+    # the fp8 GEMM saves (profiles/fp8_gemm_ab_r2r.txt); c_attn / c_fc take e4m3 straight from the
+    # LayerNorm kernel
+    fp8_proj: bool = False
 
     @staticmethod
     def small(**kw):
@@ -68,7 +73,7 @@ class GPT2(nn.Module):
         self.wte._rn_direct_uses = 2  # ... each accumulated in place into the flat .grad
         self.h = nn.ModuleList(
             PreLNBlock(cfg.n_embd, cfg.n_head, causal=True, dropout=cfg.dropout, n_layer=cfg.n_layer,
-                       eps=cfg.ln_eps, fp8=cfg.fp8)
+                       eps=cfg.ln_eps, fp8=cfg.fp8, fp8_proj=cfg.fp8_proj)
             for _ in range(cfg.n_layer)
         )
         self.ln_f = LayerNorm(cfg.n_embd, cfg.ln_eps)

@@ -50,8 +50,26 @@ class Fp8State:
     def __init__(self):
         self.t = None
         self.ready = [False, False]
+        self._offer = None  # (activation tensor, its e4m3 copy) written by the producer kernel
+        self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
+
+    def producer_ready(self, device) -> bool:
+        """True once the activation slot has a delayed scale, so a producer kernel (LayerNorm)
+        can emit the e4m3 activation itself (first call: current scaling in quant())."""
+        return self.t is not None and self.t.device == device and self.ready[0] and _ext.use_native(self.t)
+
+    def offer(self, x, q):
+        """A producer quantised ``x`` into ``q`` with this state's activation slot (rolled +
+        amax recorded by that kernel); the next quant(x, 0) of the same tensor returns it."""
+        self._offer = (x, q)
 
     def quant(self, x, i):
+        if i == 0 and self._offer is not None:
+            src, q = self._offer
+            self._offer = None
+            if src.data_ptr() == x.data_ptr() and src.shape == x.shape:
+                self.fed += 1
+                return q, self.t[0]
         if self.t is None or self.t.device != x.device:
             self.t = torch.zeros(2, 4, device=x.device, dtype=torch.float32)
             self.ready = [False, False]

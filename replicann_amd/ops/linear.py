@@ -276,10 +276,13 @@ class _MLPFn(torch.autograd.Function):
         res2 = residual.reshape(-1, w2.shape[0]).contiguous() if residual is not None else None
         ops = _ext.ops()
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
-        if fp8 is not None:  # (state of layer 1, state of layer 2): e4m3 forward GEMMs
+        if fp8 is not None:  # (state of layer 1, state of layer 2 or None): e4m3 forward GEMMs
             from .fp8 import fp8_forward
             u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0])
-            y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
+            if fp8[1] is not None:
+                y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
+            else:
+                y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)
         else:
             u = ops.gemm(x2, w1, False, True, b1, None, _MLP_FWD_ACT[act], pre, None, False, 0, False, None, -1)
             y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)

@@ -35,12 +35,17 @@ class _LayerNormFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual, two_out, producer_bias):
+    def forward(ctx, x, weight, bias, eps, residual, two_out, producer_bias, fp8=None):
         shp = x.shape
         E = shp[-1]
         x2 = x.reshape(-1, E).contiguous()
         r2 = residual.reshape(-1, E).contiguous() if residual is not None else None
-        y, h, mean, rstd = _ext.ops().layernorm_fwd(x2, r2, weight, bias, eps)
+        if fp8 is not None and fp8.producer_ready(x2.device):
+            # the consumer's e4m3 activation comes out of this kernel (delayed scaling)
+            y, h, mean, rstd, q8 = _ext.ops().layernorm_fwd_q8(x2, r2, weight, bias, eps, fp8.t[0])
+            fp8.offer(y, q8)
+        else:
+            y, h, mean, rstd = _ext.ops().layernorm_fwd(x2, r2, weight, bias, eps)
         ctx.save_for_backward(x2 if residual is None else h, weight, mean, rstd)
         ctx.set_materialize_grads(False)  # an unused second output → gh None → no zero-tensor read
         ctx.bias_ref = bias
@@ -79,19 +84,22 @@ class _LayerNormFn(torch.autograd.Function):
         if direct:  # gradients already accumulated in the flat buffer
             _notify(weight)
             _notify(bias)
-            return dx, None, None, None, g_res, None, None
-        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None, g_res, None, None)
+            return dx, None, None, None, g_res, None, None, None
+        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None, g_res, None, None, None)
 
 
-def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, producer_bias=None):
+def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, producer_bias=None, fp8=None):
     """LayerNorm over the last dim.  With ``residual``: h = x + residual, y = LN(h).
 
     Returns y, or (y, h) when ``return_sum`` (h = x when there is no residual;
     use that h as the block's residual so both gradients meet in one kernel).
     ``producer_bias``: see :class:`_LayerNormFn`.
+    ``fp8``: the :class:`~replicann_amd.ops.fp8.Fp8State` of the fp8 GEMM that consumes y — the
+    kernel then also writes y in e4m3 (delayed scaling) and hands it to that GEMM, which skips its
+    own quantisation pass.
     """
     if _ext.use_native(x):
-        out = _LayerNormFn.apply(x, weight, bias, eps, residual, return_sum, producer_bias)
+        out = _LayerNormFn.apply(x, weight, bias, eps, residual, return_sum, producer_bias, fp8)
         if residual is None and not return_sum:
             return out
         return out if return_sum else out[0]

@@ -163,3 +163,25 @@ def test_gpt2_fp8_train_steps(cuda):
     tr = Trainer(cfg)
     losses = [float(tr.step()) for _ in range(6)]
     assert all(torch.isfinite(torch.tensor(losses))) and losses[-1] < losses[0]
+
+
+@pytest.mark.gpu
+def test_gpt2_fp8_layernorm_fed_and_tracks_bf16(cuda):
+    """fp8 GPT-2 blocks: c_attn / c_fc take their e4m3 input from the LayerNorm kernel (after the
+    first, current-scaling step), the output projections stay bf16, and the loss trajectory tracks
+    the bf16 model's."""
+    kw = {"n_embd": 256, "n_head": 4}
+
+    def run(fp8):
+        torch.manual_seed(4)
+        cfg = TrainConfig(model="gpt2-tiny", batch_size=4, seq_len=128, steps=8, lr=1e-3, warmup_steps=1,
+                          log_every=1000, graph="off", model_kwargs={**kw, "fp8": fp8})
+        tr = Trainer(cfg)
+        return tr, [float(tr.step()) for _ in range(8)]
+
+    tr8, l8 = run(True)
+    _, l16 = run(False)
+    for blk in tr8.model.h:
+        assert blk.attn.c_attn.fp8_state.fed >= 7 and blk.mlp.c_fc.fp8_state.fed >= 7
+        assert blk.attn.c_proj.fp8_state is None and blk.mlp.c_proj.fp8_state is None
+    assert all(abs(a - b) < 0.05 * abs(b) for a, b in zip(l8, l16)), (l8, l16)

@@ -716,6 +716,25 @@ def test_gemm_fp8_persistent_vs_tile_kernel(cuda, monkeypatch, M, N, K, act):
         assert rel_err(outs[0][1], outs[1][1]) < 5e-3
 
 
+def test_layernorm_fused_fp8_output(cuda):
+    """LayerNorm emitting its output in e4m3 for an fp8 consumer (delayed scaling): the bytes match
+    a separate delayed quantisation of y with the same rolled scale, and the recorded amax is |y|max."""
+    torch.manual_seed(24)
+    M, E = 3000, 1024
+    x, r = bf(M, E), bf(M, E)
+    w, b = bf(E, scale=0.5) + 1.0, bf(E, scale=0.1)
+    st_a = torch.tensor([0.0, 3.0, 0.0, 0.0], device="cuda")  # previous amax 3 -> scale 2*3/448
+    st_b = st_a.clone()
+    y, h, mean, rstd, q8 = torch.ops.replicann.layernorm_fwd_q8(x, r, w, b, 1e-5, st_a)
+    y_ref, h_ref, _, _ = torch.ops.replicann.layernorm_fwd(x, r, w, b, 1e-5)
+    q_ref = torch.ops.replicann.fp8_quantize_delayed(y_ref, st_b)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref) and torch.equal(h, h_ref)
+    assert abs(st_a[0].item() - 2 * 3.0 / 448) < 1e-7 and st_a[2].item() == 3.0
+    assert st_a[1].item() == y.float().abs().max().item()
+    assert torch.equal(q8, q_ref)
+
+
 def test_linear_fp8_autograd(cuda):
     torch.manual_seed(22)
     x = bf(4, 64, 256).requires_grad_()
