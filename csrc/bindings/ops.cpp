@@ -79,7 +79,7 @@ void rn_fp8_quantize(const void*, long, void*, float*, hipStream_t);
 void rn_fp8_dequantize(const void*, long, const float*, void*, hipStream_t);
 void rn_fp8_quantize_delayed(const void*, long, void*, float*, hipStream_t);
 int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
-                int, int, int, long, long, long, int, hipStream_t);
+                int, int, int, long, long, long, int, hipStream_t, void*, float*);
 long rn_bn_ws_floats(int, int);
 int rn_bn_supported(int);
 void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, float*, float*, float*, int, int, float,
@@ -915,9 +915,29 @@ Tensor gemm_fp8(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tens
     int rc = rn_gemm_fp8(a8.data_ptr(), b8.data_ptr(), c.data_ptr(), optr(bias), optr(residual),
                          preact && preact->defined() ? preact->data_ptr() : nullptr, sa.data_ptr<float>(),
                          sb.data_ptr<float>(), alpha.data_ptr<float>(), M, N, K, a8.stride(0), b8.stride(0), c.stride(0),
-                         (int)act, cur_stream());
+                         (int)act, cur_stream(), nullptr, nullptr);
     TORCH_CHECK(rc == 0, "gemm_fp8: K and row strides must be multiples of 16, got K=", K);
     return c;
+}
+// gemm_fp8 whose activation output also comes out in e4m3 for the next fp8 GEMM (`q8_state`: that
+// GEMM's activation Fp8State slot; delayed scaling, rolled here, amax recorded by the epilogue)
+std::tuple<Tensor, Tensor> gemm_fp8_q8(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb,
+                                       const optional<Tensor>& bias, int64_t act, const Tensor& preact,
+                                       const Tensor& q8_state) {
+    GUARD(a8);
+    TORCH_CHECK(a8.scalar_type() == at::kByte && b8.scalar_type() == at::kByte, "fp8 operands are uint8 storage");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.size(1) == b8.size(1) && a8.is_contiguous() && b8.is_contiguous());
+    TORCH_CHECK(q8_state.scalar_type() == at::kFloat && q8_state.numel() >= 4 && q8_state.is_cuda());
+    const int M = a8.size(0), N = b8.size(0), K = a8.size(1);
+    TORCH_CHECK(preact.size(0) == M && preact.size(1) == N && preact.is_contiguous());
+    Tensor c = at::empty({M, N}, a8.options().dtype(at::kBFloat16));
+    Tensor q = at::empty({M, N}, a8.options().dtype(at::kByte));
+    Tensor alpha = at::empty({1}, a8.options().dtype(at::kFloat));
+    int rc = rn_gemm_fp8(a8.data_ptr(), b8.data_ptr(), c.data_ptr(), optr(bias), nullptr, preact.data_ptr(),
+                         sa.data_ptr<float>(), sb.data_ptr<float>(), alpha.data_ptr<float>(), M, N, K, a8.stride(0),
+                         b8.stride(0), c.stride(0), (int)act, cur_stream(), q.data_ptr(), q8_state.data_ptr<float>());
+    TORCH_CHECK(rc == 0, "gemm_fp8_q8: unsupported shape / activation (rc ", rc, ")");
+    return {c, q};
 }
 
 int64_t native_version() { return 1; }
@@ -980,6 +1000,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
+    m.def("gemm_fp8_q8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, int act, Tensor(a!) preact, Tensor(b!) q8_state) -> (Tensor, Tensor)");
     m.def("native_version() -> int");
     m.def("gemm_tuning_table() -> str");
 }
@@ -1026,6 +1047,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("fp8_dequantize", &fp8_dequantize);
     m.impl("fp8_quantize_delayed", &fp8_quantize_delayed);
     m.impl("gemm_fp8", &gemm_fp8);
+    m.impl("gemm_fp8_q8", &gemm_fp8_q8);
 }
 
 TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {

@@ -56,6 +56,11 @@ struct GemmArgs {
     // on configs with (threads % (BN/8)) == 0, see colpart_ok()
     float* colpart;
     ConvGeom cv;
+    // optional e4m3 copy of an activation-forward output for the NEXT fp8 GEMM (delayed scaling:
+    // q8st[0] = scale, rolled before the launch; the kernel records amax(|out|) in q8st[1]);
+    // staged epilogue of the one-tile-per-block kernels only
+    uint8_t* q8;
+    float* q8st;
 };
 
 template <int BN, int NT>
@@ -585,6 +590,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
             constexpr int ITERS = BM * CPR / NTH;
             const int mlim = min(BM, p.M - m0), nlim = min(BN, p.N - n0);
             const bool two_out = act_fwd(ACT) && p.pre != nullptr;
+            [[maybe_unused]] float q8max = 0.f;
+            [[maybe_unused]] const float q8inv = (act_fwd(ACT) && p.q8) ? 1.f / p.q8st[0] : 0.f;
             const bf16* auxp = act_bwd(ACT) ? p.pre
                                : (p.res ? p.res : (p.accumulate ? (const bf16*)p.C : (const bf16*)nullptr));
             s16x8 aux[ITERS];
@@ -649,6 +656,21 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                         if constexpr (ACT == ACT_GELU_D) store8(p.pre + goff, pv);
                         else *reinterpret_cast<s16x8*>(p.pre + goff) = v;
                         changed = true;
+                        if (p.q8) {  // e4m3 of the stored bf16 values (same bytes as a separate pass)
+                            float e[8];
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const float yb = (float)(bf16)f[t];
+                                q8max = fmaxf(q8max, fabsf(yb));
+                                e[t] = fminf(fmaxf(yb * q8inv, -448.f), 448.f);
+                            }
+                            int w0 = 0, w1 = 0;
+                            w0 = __builtin_amdgcn_cvt_pk_fp8_f32(e[0], e[1], w0, false);
+                            w0 = __builtin_amdgcn_cvt_pk_fp8_f32(e[2], e[3], w0, true);
+                            w1 = __builtin_amdgcn_cvt_pk_fp8_f32(e[4], e[5], w1, false);
+                            w1 = __builtin_amdgcn_cvt_pk_fp8_f32(e[6], e[7], w1, true);
+                            *reinterpret_cast<int2*>(p.q8 + goff) = make_int2(w0, w1);
+                        }
                     }
                 }
                 if (!auxp) {  // no residual / accumulate / activation-backward operand
@@ -687,6 +709,20 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
                     }
                 }
                 store8(dst + goff, f);
+            }
+            if constexpr (act_fwd(ACT)) {
+                if (p.q8) {  // block amax -> one atomic (non-negative floats order as ints)
+                    float* red = reinterpret_cast<float*>(smem);
+                    q8max = wave_max(q8max);
+                    __syncthreads();  // staged tile fully read
+                    if (lane == 0) red[threadIdx.x >> 6] = q8max;
+                    __syncthreads();
+                    if (threadIdx.x == 0) {
+                        float t = 0.f;
+                        for (int w = 0; w < NW; ++w) t = fmaxf(t, red[w]);
+                        atomicMax(reinterpret_cast<int*>(p.q8st + 1), __float_as_int(t));
+                    }
+                }
             }
             if constexpr (CSUM_OK) {
                 if (p.colpart) {  // fold the NT/CPR row-groups of each chunk (fixed order)

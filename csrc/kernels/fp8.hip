@@ -147,16 +147,21 @@ void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipSt
 }
 
 // C[M,N] (bf16) = act(sa·sb · A8[M,K] · B8[N,K]ᵀ + bias) + res ; K % 16 == 0, lda/ldb in bytes % 16 == 0
+// q8 / q8st (optional, activation-forward with a saved pre-activation only): also write the output
+// in e4m3 for the next fp8 GEMM (q8st rolled here; the tile kernel's epilogue quantises and records amax)
 int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const void* res, void* pre,
                 const float* sa, const float* sb, float* alpha_ws, int M, int N, int K, long lda, long ldb, long ldc,
-                int act, hipStream_t st) {
+                int act, hipStream_t st, void* q8, float* q8st) {
     if (K % 16 || lda % 16 || ldb % 16) return -1;
+    if (q8 && (!pre || (act != ACT_GELU && act != ACT_GELU_D && act != ACT_RELU) || N % 8 || ldc % 8)) return -2;
     scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
+    if (q8) fp8_roll_k<<<1, 1, 0, st>>>(q8st);
     rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
     a.pre = (bf16*)pre; a.ws = nullptr; a.alpha = alpha_ws;
     a.M = M; a.N = N; a.K = K / 2; a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
     a.split = 1; a.k_per_split = ((K / 2) + 63) / 64 * 64; a.out_f32 = 0; a.accumulate = 0;
+    a.q8 = (uint8_t*)q8; a.q8st = q8st;
     using namespace rn_gemm_detail;
     // persistent 256x256 half-tile stream (gemm_pk<.., FP8>): its epilogue stores 8 contiguous
     // columns per lane, so it takes N % 8 == 0 and ldc % 8 == 0 only.  Measured on the GPT-2-medium
@@ -164,7 +169,7 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     // at K = 1024 (1.32 vs 1.59 PF/s: 8 K-tiles per output tile, the per-tile epilogue dominates),
     // so by default it takes K >= 2048 only; REPLICANN_FP8_GEMM=9 forces it, =0 never.
     const int kern = fp8_gemm_kernel();
-    if (N % 8 == 0 && ldc % 8 == 0 && (kern == 9 || (kern < 0 && K >= 2048))) {
+    if (!q8 && N % 8 == 0 && ldc % 8 == 0 && (kern == 9 || (kern < 0 && K >= 2048))) {
         a.tiles_m = (M + 255) / 256;
         a.tiles_n = (N + 255) / 256;
         rn_gemm_launch_pk_fp8(a, act, st);

@@ -85,10 +85,11 @@ class Attention(nn.Module):
 
 
 class MLP(nn.Module):
-    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12, fp8=False, fp8_proj=True):
+    def __init__(self, n_embd, hidden, dropout=0.0, n_layer=12, fp8=False):
         super().__init__()
         self.c_fc = Linear(n_embd, hidden, fp8=fp8)
-        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8 and fp8_proj)
+        # fp8 c_proj takes its e4m3 input from c_fc's GEMM epilogue (ops.mlp)
+        self.c_proj = Linear(hidden, n_embd, std=0.02 / math.sqrt(2 * n_layer), fp8=fp8)
         self.dropout = dropout
 
     def out_bias(self):
@@ -111,7 +112,7 @@ class PreLNBlock(nn.Module):
         self.ln_1 = LayerNorm(n_embd, eps)
         self.attn = Attention(n_embd, n_head, causal, dropout, dropout, n_layer, fp8=fp8, fp8_proj=fp8_proj)
         self.ln_2 = LayerNorm(n_embd, eps)
-        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer, fp8=fp8, fp8_proj=fp8_proj)
+        self.mlp = MLP(n_embd, mlp_ratio * n_embd, dropout, n_layer, fp8=fp8)
 
     def out_bias(self):
         return self.mlp.out_bias()

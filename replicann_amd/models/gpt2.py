@@ -36,10 +36,10 @@ class GPT2Config:
     dropout: float = 0.0
     ln_eps: float = 1e-5
     fp8: bool = False  # fp8 e4m3 forward GEMMs in the transformer blocks ("fp8 weights" config)
-    # fp8 also for the two output projections (attention c_proj, MLP c_proj).  Off by default: their
-    # inputs (attention output, GELU output) would need a separate quantisation pass that costs what
-    # the fp8 GEMM saves (profiles/fp8_gemm_ab_r2r.txt); c_attn / c_fc take e4m3 straight from the
-    # LayerNorm kernel
+    # fp8 also for the attention output projection.  Off by default: its input (the attention
+    # output) would need a separate quantisation pass that costs what the fp8 GEMM saves
+    # (profiles/fp8_gemm_ab_r2r.txt).  c_attn / c_fc take e4m3 straight from the LayerNorm kernel,
+    # the MLP c_proj from c_fc's GEMM epilogue
     fp8_proj: bool = False
 
     @staticmethod

@@ -82,12 +82,20 @@ class Fp8State:
         return _ext.ops().fp8_quantize_delayed(x, st), st
 
 
-def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State):
+def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State, out8: Fp8State | None = None):
     """act(x2·weightᵀ + bias) + res2 with both operands in e4m3 (GPU: block-scaled MFMA;
-    CPU: the same quantise → dequantise numerics in fp32)."""
+    CPU: the same quantise → dequantise numerics in fp32).
+
+    ``out8``: the state of the fp8 GEMM that consumes this output — the epilogue then also writes
+    the output in e4m3 with that state's delayed scale and hands it over (no quantisation pass)."""
     xq, xs = state.quant(x2, 0)
     wq, ws = state.quant(weight.contiguous(), 1)
     if _ext.use_native(x2):
+        if (out8 is not None and res2 is None and preact is not None and x2.shape[0] > 0
+                and out8.producer_ready(x2.device)):
+            y, q = _ext.ops().gemm_fp8_q8(xq, wq, xs, ws, bias, act, preact, out8.t[0])
+            out8.offer(y, q)
+            return y
         return _ext.ops().gemm_fp8(xq, wq, xs, ws, bias, res2, act, preact)
     h = dequantize_fp8(xq, xs).float() @ dequantize_fp8(wq, ws).float().t()
     if bias is not None:

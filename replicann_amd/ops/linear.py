@@ -278,7 +278,8 @@ class _MLPFn(torch.autograd.Function):
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
         if fp8 is not None:  # (state of layer 1, state of layer 2 or None): e4m3 forward GEMMs
             from .fp8 import fp8_forward
-            u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0])
+            # layer 2's e4m3 input comes out of layer 1's epilogue (its delayed scale permitting)
+            u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1])
             if fp8[1] is not None:
                 y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
             else:

@@ -183,5 +183,6 @@ def test_gpt2_fp8_layernorm_fed_and_tracks_bf16(cuda):
     _, l16 = run(False)
     for blk in tr8.model.h:
         assert blk.attn.c_attn.fp8_state.fed >= 7 and blk.mlp.c_fc.fp8_state.fed >= 7
-        assert blk.attn.c_proj.fp8_state is None and blk.mlp.c_proj.fp8_state is None
+        assert blk.mlp.c_proj.fp8_state.fed >= 7  # from c_fc's GEMM epilogue
+        assert blk.attn.c_proj.fp8_state is None
     assert all(abs(a - b) < 0.05 * abs(b) for a, b in zip(l8, l16)), (l8, l16)

@@ -735,6 +735,29 @@ def test_layernorm_fused_fp8_output(cuda):
     assert torch.equal(q8, q_ref)
 
 
+@pytest.mark.parametrize("act", [2, 5])
+def test_gemm_fp8_with_e4m3_output(cuda, act):
+    """The fp8 GEMM whose GELU output also comes out in e4m3 for the next fp8 GEMM: same bf16
+    output as the plain call, e4m3 bytes equal to a separate delayed quantisation with the same
+    rolled scale, amax recorded."""
+    torch.manual_seed(25)
+    M, N, K = 1500, 4096, 1024
+    a, b, bias = bf(M, K), bf(N, K, scale=0.05), bf(N, scale=0.1)
+    qa, sa = ops.quantize_fp8(a)
+    qb, sb = ops.quantize_fp8(b)
+    pre1 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    pre2 = torch.empty_like(pre1)
+    st = torch.tensor([0.0, 2.0, 0.0, 0.0], device="cuda")
+    st_ref = st.clone()
+    y, q = torch.ops.replicann.gemm_fp8_q8(qa, qb, sa, sb, bias, act, pre1, st)
+    y_ref = torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, None, act, pre2)
+    q_ref = torch.ops.replicann.fp8_quantize_delayed(y_ref, st_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref) and torch.equal(pre1, pre2)
+    assert torch.equal(q, q_ref)
+    assert st[1].item() == y.float().abs().max().item() and st[2].item() == 2.0
+
+
 def test_linear_fp8_autograd(cuda):
     torch.manual_seed(22)
     x = bf(4, 64, 256).requires_grad_()
