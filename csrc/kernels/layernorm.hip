@@ -217,7 +217,8 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
     if (E % 8 != 0 || E > 8192) return -1;
     int nv = rn_ln_nv(E);
     if (q8) {
-        dim3 grid((M + 3) / 4 < 1024 ? (M + 3) / 4 : 1024);
+        // 4096 blocks (16 per CU): enough rows in flight for HBM, one amax atomic per block
+        dim3 grid((M + 3) / 4 < 4096 ? (M + 3) / 4 : 4096);
 #define RN_LNF(NV, R, B) ln_fwd_k<NV, R, B, true><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)r, (const bf16*)w, (const bf16*)b, (bf16*)y, (bf16*)h, mean, rstd, M, E, eps, (uint8_t*)q8, st8)
 #define RN_LNF2(NV) { if (r) { if (b) RN_LNF(NV, true, true); else RN_LNF(NV, true, false); } \
                       else { if (b) RN_LNF(NV, false, true); else RN_LNF(NV, false, false); } }
