@@ -59,12 +59,13 @@ __global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long 
 // Delayed scaling (one pass over x): the scale comes from the amax recorded by the PREVIOUS
 // quantisation of this tensor (x2 headroom), and this pass records the current amax for the
 // next one.  state: [0] scale used, [1] amax of the last pass, [2] amax the scale came from.
-__global__ void fp8_roll_k(float* __restrict__ state) {
+__device__ inline void fp8_roll_k_body(float* __restrict__ state) {
     const float a = state[1];
     state[2] = a;
     state[0] = a > 0.f ? 2.f * a / E4M3_MAX : 1.f;
     state[1] = 0.f;
 }
+__global__ void fp8_roll_k(float* __restrict__ state) { fp8_roll_k_body(state); }
 
 __global__ void __launch_bounds__(256) quant_delayed_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
                                                        float* __restrict__ state) {
@@ -103,6 +104,50 @@ __global__ void dequant_k(const uint8_t* __restrict__ q, long n, const float* __
         y[i] = (bf16)(__builtin_amdgcn_cvt_f32_fp8((int)q[i], 0) * scale);
 }
 
+// ---- e4m3 weight cache (ops/fp8.py Fp8WeightCache): every fp8 weight of the model re-quantised
+// right after the optimizer step, in two launches for the whole model.  segs: int64 [nseg][4] =
+// (element offset in the flat bf16 parameter buffer, numel, byte offset in the e4m3 buffer,
+// address of the weight's Fp8State slot).  Delayed scaling as fp8_roll_k / quant_delayed_k.
+__global__ void fp8_roll_many_k(const long* __restrict__ segs, int nseg) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nseg) fp8_roll_k_body(reinterpret_cast<float*>(segs[i * 4 + 3]));
+}
+
+__global__ void __launch_bounds__(256) fp8_quant_many_k(const bf16* __restrict__ flat, const long* __restrict__ segs,
+                                                        uint8_t* __restrict__ qbuf) {
+    __shared__ float sm[16];
+    const long* sg = segs + blockIdx.y * 4;
+    const bf16* x = flat + sg[0];
+    const long n = sg[1];
+    uint8_t* q = qbuf + sg[2];
+    float* state = reinterpret_cast<float*>(sg[3]);
+    const float inv = 1.f / state[0];
+    float m = 0.f;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            m = fmaxf(m, fabsf(f[j]));
+            f[j] = fminf(fmaxf(f[j] * inv, -E4M3_MAX), E4M3_MAX);
+        }
+        int w0 = 0, w1 = 0;
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+        *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    }
+    for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float v = bf2f(x[i]);
+        m = fmaxf(m, fabsf(v));
+        const float f = fminf(fmaxf(v * inv, -E4M3_MAX), E4M3_MAX);
+        q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(f, 0.f, 0, false) & 0xFF);
+    }
+    m = block_max(m, sm);
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
+}
+
 // alpha = sa * sb on device
 __global__ void scale_mul_k(const float* __restrict__ sa, const float* __restrict__ sb, float* __restrict__ alpha) {
     alpha[0] = sa[0] * sb[0];
@@ -137,6 +182,15 @@ void rn_fp8_quantize(const void* x, long n, void* q, float* state, hipStream_t s
 void rn_fp8_quantize_delayed(const void* x, long n, void* q, float* state, hipStream_t st) {
     fp8_roll_k<<<1, 1, 0, st>>>(state);
     quant_delayed_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
+}
+
+// Re-quantise every cached fp8 weight (segs: device int64 [nseg][4], see fp8_quant_many_k).
+void rn_fp8_quant_many(const void* flat, const long* segs, int nseg, long max_n, void* qbuf, hipStream_t st) {
+    if (nseg <= 0) return;
+    fp8_roll_many_k<<<(nseg + 255) / 256, 256, 0, st>>>(segs, nseg);
+    long per = (max_n / 8 + 255) / 256;  // blocks that cover the largest weight in one sweep
+    const int bx = (int)(per < 1 ? 1 : (per > 64 ? 64 : per));
+    fp8_quant_many_k<<<dim3(bx, nseg), 256, 0, st>>>((const bf16*)flat, segs, (uint8_t*)qbuf);
 }
 
 // The delayed-scaling roll alone (for producers that quantise inside their own kernel).

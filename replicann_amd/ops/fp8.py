@@ -52,6 +52,7 @@ class Fp8State:
         self.ready = [False, False]
         self._offer = None  # (activation tensor, its e4m3 copy) written by the producer kernel
         self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
+        self.wcache = None  # Fp8WeightCache holding this GEMM's e4m3 weight (refreshed by the optimizer)
 
     def producer_ready(self, device) -> bool:
         """True once the activation slot has a delayed scale, so a producer kernel (LayerNorm)
@@ -64,6 +65,10 @@ class Fp8State:
         self._offer = (x, q)
 
     def quant(self, x, i):
+        if i == 1 and self.wcache is not None:
+            q = self.wcache.lookup(self, x)
+            if q is not None:
+                return q, self.t[1]
         if i == 0 and self._offer is not None:
             src, q = self._offer
             self._offer = None
@@ -113,3 +118,78 @@ def linear_fp8(x, weight, bias=None, act=None, residual=None, state: Fp8State | 
     (ops.linear: direct flat-buffer gradient accumulation, fused bias reduction)."""
     from .linear import linear
     return linear(x, weight, bias, act=act, residual=residual, fp8=state if state is not None else Fp8State())
+
+
+class Fp8WeightCache:
+    """e4m3 copies of every fp8 weight of a model, written right after each optimizer step.
+
+    The forward then reads the weight operand straight from this cache instead of quantising
+    the bf16 weight per GEMM call: the ~3 small launches per fp8 GEMM per step (roll, quantise,
+    scale) become 2 launches for the whole model (``fp8_quant_many``: roll every weight slot,
+    then quantise every weight from the flat bf16 parameter buffer, delayed scaling with one
+    amax per weight).  The optimizer calls :meth:`refresh` at the end of ``step()`` (inside a
+    captured step graph as well).  A cached copy is used only while the weight's version
+    counter is the one recorded at the refresh, so a weight changed any other way (checkpoint
+    load, manual edit) falls back to per-call quantisation until the next refresh."""
+
+    def __init__(self, pairs, flat):
+        """``pairs``: [(weight Parameter living in ``flat``, Fp8State)]."""
+        self.flat = flat
+        off = {id(p): o for p, o, _ in flat.segments()}
+        self.entries = []
+        qoff = 0
+        for w, st in pairs:
+            self.entries.append([w, st, off[id(w)], qoff])
+            qoff += (w.numel() + 15) // 16 * 16
+        dev = flat.data.device
+        self.qbuf = torch.empty(max(qoff, 16), dtype=torch.uint8, device=dev)
+        self.max_n = max((w.numel() for w, _ in pairs), default=0)
+        self.segs = None
+        self.version = {}
+        self.refreshes = 0
+        for w, st, _, _ in self.entries:
+            st.wcache = self
+
+    def _ensure_states(self):
+        for w, st, _, _ in self.entries:
+            if st.t is None or st.t.device != self.flat.data.device:
+                st.t = torch.zeros(2, 4, device=self.flat.data.device, dtype=torch.float32)
+                st.ready = [False, False]
+        rows = [[o, w.numel(), qo, st.t[1].data_ptr()] for w, st, o, qo in self.entries]
+        self.segs = torch.tensor(rows, dtype=torch.int64).to(self.flat.data.device)
+
+    def refresh(self):
+        if not self.entries or not _ext.use_native(self.flat.data):
+            return
+        if self.segs is None or any(st.t is None for _, st, _, _ in self.entries):
+            self._ensure_states()
+        for _, st, _, _ in self.entries:
+            if not st.ready[1]:  # first quantisation of this weight: current scaling, seeds the amax
+                return
+        _ext.ops().fp8_quant_many(self.flat.data, self.segs, self.max_n, self.qbuf)
+        self.refreshes += 1
+        for w, st, _, _ in self.entries:
+            self.version[id(st)] = w._version
+
+    def lookup(self, st, w):
+        """The cached e4m3 weight of ``st`` if it is current for ``w``, else None."""
+        v = self.version.get(id(st))
+        if v is None or v != w._version:
+            return None
+        for ww, s2, _, qo in self.entries:
+            if s2 is st and ww.data_ptr() == w.data_ptr():
+                return self.qbuf[qo:qo + w.numel()].view(w.shape)
+        return None
+
+
+def attach_weight_cache(model, flat, optimizer):
+    """Give every fp8 Linear of ``model`` (``fp8_state`` + ``weight`` in ``flat``) an e4m3 weight
+    copy refreshed by ``optimizer`` after each step.  Returns the cache (None if no fp8 layer)."""
+    in_flat = {id(p) for p in flat.params}
+    pairs = [(m.weight, m.fp8_state) for m in model.modules()
+             if getattr(m, "fp8_state", None) is not None and id(getattr(m, "weight", None)) in in_flat]
+    if not pairs:
+        return None
+    cache = Fp8WeightCache(pairs, flat)
+    optimizer.post_step_hooks.append(cache.refresh)
+    return cache

@@ -37,6 +37,7 @@ class _FlatOptimizer:
         self.max_grad_norm = max_grad_norm
         self.grad_scale = grad_scale  # e.g. 1/world_size for DDP SUM-reduced grads
         self.step_count = 0
+        self.post_step_hooks = []  # callables run at the end of every step (fp8 weight cache refresh)
         # gradient the step reads: the flat bf16 .grad buffer, or (data parallel) the fp32
         # all-reduced copy the DDP reducer owns (``DistributedDataParallel.grad_source``)
         self.grad_source = None
@@ -70,6 +71,12 @@ class _FlatOptimizer:
 
     def zero_grad(self):
         self.flat.zero_grad()
+
+    def _post_step(self):
+        """Run the registered post-step hooks (e.g. the fp8 weight cache refresh): stream-ordered
+        after the update, and captured with it when the step is graph-captured."""
+        for h in self.post_step_hooks:
+            h()
 
     def set_schedule(self, warmup, total, min_ratio=0.1):
         """Warmup + cosine decay, evaluated on device each step (graph-safe)."""
@@ -129,6 +136,7 @@ class FusedAdamW(_FlatOptimizer):
             ops.adamw_step(self.flat.data, self.master, self.grad, self.m, self.v, self.flat.wd_mask,
                            self.norm_buf, b1, b2, self.eps, self.weight_decay, self.grad_scale, clip,
                            self.stochastic_round)
+            self._post_step()
             return
         lr = self._host_lr(lr)
         bc1 = 1 - b1 ** self.step_count
@@ -146,6 +154,7 @@ class FusedAdamW(_FlatOptimizer):
         self.master.add_(upd, alpha=-lr)
         if self.master is not self.flat.data:
             self.flat.data.copy_(self.master)
+        self._post_step()
 
     def _extra_state(self):
         return [self.m, self.v]
@@ -182,6 +191,7 @@ class FusedSGD(_FlatOptimizer):
             ops.sumsq(self.grad, self.norm_buf)
             ops.sgd_step(self.flat.data, self.master, self.grad, self.buf, self.flat.wd_mask,
                          self.norm_buf, self.momentum, self.weight_decay, self.nesterov, self.grad_scale, clip)
+            self._post_step()
             return
         lr = self._host_lr(lr)
         g = self.grad.float() * self.grad_scale

@@ -129,6 +129,10 @@ class Trainer:
                                 max_grad_norm=cfg.max_grad_norm, grad_scale=gs)
         if self.ddp is not None:
             self.opt.grad_source = self.ddp.grad_source  # fp32 all-reduced gradients
+        self.fp8_cache = None
+        if self.device.type == "cuda":  # fp8 layers read e4m3 weights the optimizer step writes
+            from .ops.fp8 import attach_weight_cache
+            self.fp8_cache = attach_weight_cache(self.model, self.flat, self.opt)
         self.opt.set_schedule(cfg.warmup_steps, max(cfg.steps, 1), cfg.min_lr_ratio)
         self.step_idx = 0
         self._graph = None
@@ -279,6 +283,8 @@ class Trainer:
         for t, v in zip(state, snap):
             t.copy_(v)
         self.opt.step_count = count
+        if self.fp8_cache is not None:
+            self.fp8_cache.refresh()  # e4m3 weights of the restored parameters
         torch.cuda.synchronize()
         del snap
         g = torch.cuda.CUDAGraph()

@@ -181,7 +181,9 @@ def test_gpt2_fp8_layernorm_fed_and_tracks_bf16(cuda):
 
     tr8, l8 = run(True)
     _, l16 = run(False)
+    assert tr8.fp8_cache is not None and tr8.fp8_cache.refreshes == 8  # e4m3 weights from the optimizer
     for blk in tr8.model.h:
+        assert blk.attn.c_attn.fp8_state.wcache is tr8.fp8_cache
         assert blk.attn.c_attn.fp8_state.fed >= 7 and blk.mlp.c_fc.fp8_state.fed >= 7
         assert blk.mlp.c_proj.fp8_state.fed >= 7  # from c_fc's GEMM epilogue
         assert blk.attn.c_proj.fp8_state is None

@@ -758,6 +758,50 @@ def test_gemm_fp8_with_e4m3_output(cuda, act):
     assert st[1].item() == y.float().abs().max().item() and st[2].item() == 2.0
 
 
+def test_fp8_weight_cache_matches_per_call_quantisation(cuda):
+    """Fp8WeightCache: after an optimizer step the cached e4m3 weight equals a delayed quantisation
+    of the updated bf16 weight with the same rolled scale; a weight changed outside the optimizer
+    is not served from the cache."""
+    from replicann_amd.ops.fp8 import Fp8State, attach_weight_cache
+    from replicann_amd.optim import FusedAdamW
+    from replicann_amd.utils.flat import FlatParams
+
+    torch.manual_seed(26)
+
+    class L(torch.nn.Module):
+        def __init__(self, n, k):
+            super().__init__()
+            self.weight = torch.nn.Parameter(torch.randn(n, k) * 0.05)
+            self.fp8_state = Fp8State()
+
+    m = torch.nn.Sequential(L(384, 256), L(1000, 384)).cuda()
+    for p in m.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    flat = FlatParams(m)
+    opt = FusedAdamW(flat, lr=1e-2)
+    cache = attach_weight_cache(m, flat, opt)
+    assert cache is not None and len(cache.entries) == 2
+    for layer in m:  # first use: current scaling (seeds the amax)
+        layer.fp8_state.quant(layer.weight, 1)
+    flat.grad.normal_()
+    opt.step()
+    assert cache.refreshes == 1
+    for layer in m:
+        st = layer.fp8_state
+        q, s_ = st.quant(layer.weight, 1)
+        assert q.data_ptr() >= cache.qbuf.data_ptr()  # served from the cache
+        ref_state = st.t[1].clone()
+        ref_state[1] = ref_state[2]  # replay the roll from the amax the cache's roll consumed
+        q_ref = torch.ops.replicann.fp8_quantize_delayed(layer.weight.contiguous(), ref_state)
+        torch.cuda.synchronize()
+        assert torch.equal(q, q_ref)
+        assert st.t[1][1].item() == layer.weight.float().abs().max().item()
+    with torch.no_grad():
+        m[0].weight.mul_(2.0)  # outside the optimizer: version changes, cache not used
+    q2, _ = m[0].fp8_state.quant(m[0].weight, 1)
+    assert not (cache.qbuf.data_ptr() <= q2.data_ptr() < cache.qbuf.data_ptr() + cache.qbuf.numel())
+
+
 def test_linear_fp8_autograd(cuda):
     torch.manual_seed(22)
     x = bf(4, 64, 256).requires_grad_()
