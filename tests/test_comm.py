@@ -51,3 +51,60 @@ def test_one_rank_ddp_rehearsal_cpu(monkeypatch):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+class _FakeRccl:
+    """Stand-in for the native comm ops on CPU: records the rendezvous the Python side performs."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.calls = []
+
+    def comm_unique_id(self):
+        return torch.arange(128, dtype=torch.uint8) ^ 0x5A  # a recognisable id from rank 0
+
+    def comm_init(self, uid, rank, world, device, timeout_s):
+        self.calls.append(("init", bytes(uid.numpy()), rank, world, device, timeout_s))
+        return 7
+
+
+def _native_rendezvous_worker(rank, world, port, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from replicann_amd import _ext
+        from replicann_amd.parallel.comm import NativeComm
+
+        fake = _FakeRccl(rank)
+        _ext.ops = lambda: fake  # the comm layer's only entry into the extension
+        c = NativeComm(device=torch.device("cuda", rank))  # device index only: no GPU work on the fake
+        q.put((rank, c.rank, c.world, c.handle, fake.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_comm_rendezvous_multi_rank(world):
+    """N>1 setup of the native communicator (not reachable on a one-GPU box, RCCL refuses two ranks
+    per device): every rank receives rank 0's ncclUniqueId over the torch.distributed rendezvous
+    and initialises with its own rank, the world size and its LOCAL device."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_rendezvous_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    uid0 = bytes((torch.arange(128, dtype=torch.uint8) ^ 0x5A).numpy())
+    for rank, (r, cr, cw, h, calls) in enumerate(res):
+        assert (r, cr, cw, h) == (rank, rank, world, 7)
+        assert len(calls) == 1
+        _, uid, crank, cworld, dev, _ = calls[0]
+        assert uid == uid0 and crank == rank and cworld == world and dev == rank
