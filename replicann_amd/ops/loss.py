@@ -79,10 +79,9 @@ class _LinearXentFn(torch.autograd.Function):
         ops = _ext.ops()
         gh = gw = None
         if ctx.needs_input_grad[0]:
-            # plain GEMM (the autotuner may pick the vendor library for it), g/n applied after:
-            # a 16k×E scale is ~1 % of the GEMM
-            gh = ops.gemm(dlogits, weight, False, False, None, None, 0, None, None, False, 0, False, None, -1)
-            gh = gh.mul_(alpha.reshape(())).reshape(ctx.shp)  # 0-dim fp32: computed in fp32, stored bf16
+            # g/n as the epilogue alpha (fp32, before the bf16 rounding): no separate scaling pass
+            gh = ops.gemm(dlogits, weight, False, False, None, None, 0, None, None, False, 0, False, alpha, -1)
+            gh = gh.reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
             acc = _direct_grad(weight)
             if acc is not None:
