@@ -298,6 +298,12 @@ std::vector<int64_t> comm_info(int64_t h) {
     return {c.rank, c.world, c.n_collectives, c.bytes, (int64_t)c.failed.load()};
 }
 
+// stop the watchdog thread only (interpreter exit: no HIP call may race the runtime's teardown)
+void comm_quiesce(int64_t h) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (h >= 0 && h < (int64_t)g_comms.size() && g_comms[h]) g_comms[h]->stop_watchdog();
+}
+
 void comm_destroy(int64_t h) {
     std::unique_ptr<Comm> c;
     {
@@ -328,5 +334,6 @@ TORCH_LIBRARY_FRAGMENT(replicann, m) {
     m.def("comm_wait(int h) -> ()", &comm_wait);
     m.def("comm_synchronize(int h) -> ()", &comm_synchronize);
     m.def("comm_info(int h) -> int[]", &comm_info);
+    m.def("comm_quiesce(int h) -> ()", &comm_quiesce);
     m.def("comm_destroy(int h) -> ()", &comm_destroy);
 }

@@ -84,6 +84,13 @@ class NativeComm:
                                        group=group, device=self.device if _is_nccl(group) else None)
             uid = torch.frombuffer(bytearray(box[0]), dtype=torch.uint8)
         self.handle = int(self.ops.comm_init(uid, self.rank, self.world, self.device.index, float(timeout_s)))
+        import atexit
+
+        atexit.register(self._quiesce)  # watchdog stopped before the HIP runtime tears down
+
+    def _quiesce(self):
+        if self.handle is not None:
+            self.ops.comm_quiesce(self.handle)
 
     def all_reduce(self, t, op="sum"):
         self.ops.comm_all_reduce(self.handle, t, _OPS[op])

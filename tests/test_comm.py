@@ -67,6 +67,9 @@ class _FakeRccl:
         self.calls.append(("init", bytes(uid.numpy()), rank, world, device, timeout_s))
         return 7
 
+    def comm_quiesce(self, h):
+        pass
+
 
 def _native_rendezvous_worker(rank, world, port, q):
     import os
