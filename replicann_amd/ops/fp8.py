@@ -147,8 +147,10 @@ class Fp8WeightCache:
         self.segs = None
         self.version = {}
         self.refreshes = 0
-        for w, st, _, _ in self.entries:
+        self.by_state = {}  # id(Fp8State) -> (weight, cached e4m3 view)
+        for w, st, _, qo in self.entries:
             st.wcache = self
+            self.by_state[id(st)] = (w, self.qbuf[qo:qo + w.numel()].view(w.shape))
 
     def _ensure_states(self):
         for w, st, _, _ in self.entries:
@@ -176,10 +178,8 @@ class Fp8WeightCache:
         v = self.version.get(id(st))
         if v is None or v != w._version:
             return None
-        for ww, s2, _, qo in self.entries:
-            if s2 is st and ww.data_ptr() == w.data_ptr():
-                return self.qbuf[qo:qo + w.numel()].view(w.shape)
-        return None
+        ww, q = self.by_state[id(st)]
+        return q if ww.data_ptr() == w.data_ptr() else None
 
 
 def attach_weight_cache(model, flat, optimizer):
