@@ -63,7 +63,12 @@ class TorchComm:
 
 
 class NativeComm:
-    """The framework's RCCL communicator (``torch.ops.replicann.comm_*``) for one device."""
+    """The framework's RCCL communicator (``torch.ops.replicann.comm_*``) for one device.
+
+    Lifetime contract: a tensor handed to a collective must stay alive (not be freed / reused)
+    until :meth:`wait` has joined the comm stream into the stream that frees it — the DDP reducer's
+    buckets are persistent slices of its flat buffers.  (Registering the comm stream with the
+    caching allocator via recordStream on the external stream crashed in round-2 testing.)"""
 
     name = "native"
 
