@@ -136,13 +136,36 @@ std::string gemm_tuning_table() {
     for (auto& kv : g_tune) {
         const TuneKey& k = kv.first;
         os << (first ? "" : ",") << "{\"M\":" << k.M << ",\"N\":" << k.N << ",\"K\":" << k.K << ",\"ta\":" << k.ta
-           << ",\"tb\":" << k.tb << ",\"act\":" << k.act << ",\"epi\":" << k.epi << ",\"cfg\":" << kv.second.first
-           << ",\"split\":"
-           << kv.second.second << "}";
+           << ",\"tb\":" << k.tb << ",\"act\":" << k.act << ",\"f32\":" << k.f32 << ",\"as\":" << k.autosplit
+           << ",\"epi\":" << k.epi << ",\"cfg\":" << kv.second.first << ",\"split\":" << kv.second.second << "}";
         first = false;
     }
     os << "]";
     return os.str();
+}
+
+// Replace/insert tuning entries from a gemm_tuning_table() string (data-parallel ranks adopt rank 0's
+// measured picks, so every rank runs the same kernels).  Returns the number of entries loaded.
+int64_t gemm_tuning_load(const std::string& js) {
+    int64_t n = 0;
+    size_t pos = 0;
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    while ((pos = js.find('{', pos)) != std::string::npos) {
+        const size_t end = js.find('}', pos);
+        if (end == std::string::npos) break;
+        const std::string obj = js.substr(pos, end - pos + 1);
+        long M, N, K;
+        int ta, tb, act, f32, as, epi, cfg, split;
+        if (std::sscanf(obj.c_str(),
+                        "{\"M\":%ld,\"N\":%ld,\"K\":%ld,\"ta\":%d,\"tb\":%d,\"act\":%d,\"f32\":%d,\"as\":%d,"
+                        "\"epi\":%d,\"cfg\":%d,\"split\":%d}",
+                        &M, &N, &K, &ta, &tb, &act, &f32, &as, &epi, &cfg, &split) == 11) {
+            g_tune[TuneKey{M, N, K, ta, tb, act, f32, as, epi}] = {cfg, split};
+            ++n;
+        }
+        pos = end + 1;
+    }
+    return n;
 }
 
 // "cfg 7": the vendor library (hipBLASLt through at::mm) for PLAIN GEMMs only — no
@@ -1015,6 +1038,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_quant_many(Tensor flat, Tensor segs, int max_n, Tensor(a!) qbuf) -> ()");
     m.def("native_version() -> int");
     m.def("gemm_tuning_table() -> str");
+    m.def("gemm_tuning_load(str table) -> int");
 }
 
 TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
@@ -1066,4 +1090,5 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
 TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {
     m.impl("native_version", &native_version);
     m.impl("gemm_tuning_table", &gemm_tuning_table);
+    m.impl("gemm_tuning_load", &gemm_tuning_load);
 }

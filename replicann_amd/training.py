@@ -229,7 +229,9 @@ class Trainer:
         suspended, before the first real step — otherwise those timings would run beside the
         first step's RCCL all-reduces and pick configs on a busy device.  The pass is invisible
         to training: a fresh copy of the data source supplies the batch, and gradients, optimizer
-        state, buffers and the device RNG streams are restored afterwards."""
+        state, buffers and the device RNG streams are restored afterwards.  Multi-rank: rank 0's
+        measured configs are then broadcast and adopted by every rank (one kernel choice per shape
+        across the node, so the step's max-over-ranks time is not set by one rank's noisy pick)."""
         self._tuned = True
         if self.device.type != "cuda" or self.ddp is None:
             return
@@ -246,6 +248,12 @@ class Trainer:
         for t, v in zip(state, snap):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
+        if self.world > 1:  # every rank adopts rank 0's picks: the same kernels on every GPU
+            import torch.distributed as dist
+            box = [torch.ops.replicann.gemm_tuning_table() if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=0, device=self.device if dist.get_backend() == "nccl" else None)
+            if self.rank != 0:
+                torch.ops.replicann.gemm_tuning_load(box[0])
 
     def graph_enabled(self):
         c = self.cfg
