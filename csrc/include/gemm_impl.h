@@ -167,14 +167,17 @@ RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, in
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// fp8 fragment for v_mfma_scale_f32_16x16x128_f8f6f4: 32 consecutive e4m3 bytes
-// (k = 32*(lane>>4) + 0..31) of row mnbase + (lane&15) = 16-B chunks 2g, 2g+1 of
-// the same K-contiguous 128-B-row LDS image the bf16 path uses.
+// fp8 fragment for v_mfma_scale_f32_16x16x128_f8f6f4: 32 e4m3 bytes of row mnbase + (lane&15)
+// from the same K-contiguous 128-B-row LDS image the bf16 path uses: 16-B chunks g and g + 4
+// (g = lane>>4), i.e. exactly the two chunks the bf16 path's k-steps 0 and 1 read, so the XOR
+// swizzle keeps each ds_read_b128 lane group conflict-free (chunks 2g, 2g+1 — the round-1 mapping —
+// measured 50 % LDS bank conflicts).  The MFMA's k order inside the 128-deep step is then a
+// permutation of the row's bytes, the SAME one for A and B, so it cancels in the dot product.
 RN_DEV i32x8 frag8(const char* lds, int mnbase, int lane) {
     const int row = mnbase + (lane & 15), g = lane >> 4;
     const char* rp = lds + row * 128;
-    const i32x4 lo = *reinterpret_cast<const i32x4*>(rp + (((2 * g) ^ swz_kc(row)) << 4));
-    const i32x4 hi = *reinterpret_cast<const i32x4*>(rp + (((2 * g + 1) ^ swz_kc(row)) << 4));
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(rp + ((g ^ swz_kc(row)) << 4));
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(rp + (((g + 4) ^ swz_kc(row)) << 4));
     return (i32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
