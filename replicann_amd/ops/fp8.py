@@ -159,11 +159,15 @@ class Fp8WeightCache:
                 st.ready = [False, False]
         rows = [[o, w.numel(), qo, st.t[1].data_ptr()] for w, st, o, qo in self.entries]
         self.segs = torch.tensor(rows, dtype=torch.int64).to(self.flat.data.device)
+        self._slot_ptrs = [st.t.data_ptr() for _, st, _, _ in self.entries]
 
     def refresh(self):
         if not self.entries or not _ext.use_native(self.flat.data):
             return
-        if self.segs is None or any(st.t is None for _, st, _, _ in self.entries):
+        # (re)build the device table if a state slot was (re)allocated since: the kernel writes
+        # through the addresses in it
+        if (self.segs is None or any(st.t is None for _, st, _, _ in self.entries)
+                or [st.t.data_ptr() for _, st, _, _ in self.entries] != self._slot_ptrs):
             self._ensure_states()
         for _, st, _, _ in self.entries:
             if not st.ready[1]:  # first quantisation of this weight: current scaling, seeds the amax
