@@ -28,6 +28,18 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const bf16* __restrict__ x, cons
     const int nvec = E / 8;
     [[maybe_unused]] float amax = 0.f, inv8 = 0.f;
     if constexpr (Q8) inv8 = 1.f / st8[0];
+    // gamma / beta chunks loaded once, before the row's loads and reductions (not after them:
+    // that was a second memory round trip per row)
+    bf16x8 wv[NV];
+    [[maybe_unused]] bf16x8 bv[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = lane + i * 64;
+        if (c < nvec) {
+            wv[i] = *reinterpret_cast<const bf16x8*>(w + c * 8);
+            if constexpr (BIAS) bv[i] = *reinterpret_cast<const bf16x8*>(b + c * 8);
+        }
+    }
     for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
         const bf16* xr = x + (long)row * E;
         float v[NV][8];
@@ -63,11 +75,10 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const bf16* __restrict__ x, cons
         for (int i = 0; i < NV; ++i) {
             int c = lane + i * 64;
             if (c < nvec) {
-                float wf[8], bfv[8], o[8];
-                load8(w + c * 8, wf);
-                if constexpr (BIAS) load8(b + c * 8, bfv);
+                float o[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mu) * rs * wf[j] + (BIAS ? bfv[j] : 0.f);
+                for (int j = 0; j < 8; ++j)
+                    o[j] = (v[i][j] - mu) * rs * (float)wv[i][j] + (BIAS ? (float)bv[i][j] : 0.f);
                 store8(y + (long)row * E + c * 8, o);
                 if constexpr (Q8) {
                     float f[8];

@@ -22,7 +22,13 @@ def main():
     x = torch.randn(M, E, device="cuda").bfloat16().requires_grad_()
     gy, gh = torch.randn(M, E, device="cuda").bfloat16(), torch.randn(M, E, device="cuda").bfloat16()
 
+    fwd_only = os.environ.get("LN_AB_FWD_ONLY") == "1"
+
     def step():
+        if fwd_only:
+            with torch.no_grad():
+                ops.layer_norm(x, mod.w, mod.b, 1e-5, return_sum=True, producer_bias=mod.pb)
+            return
         y, h = ops.layer_norm(x, mod.w, mod.b, 1e-5, return_sum=True, producer_bias=mod.pb)
         torch.autograd.backward([y, h], [gy, gh])
 
@@ -35,7 +41,7 @@ def main():
         step()
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"op": "ln_fwd_bwd", "M": M, "E": E, "waves": os.environ.get("REPLICANN_LN_BWD_WAVES", "default"),
+    print(json.dumps({"op": "ln_fwd" if fwd_only else "ln_fwd_bwd", "M": M, "E": E, "waves": os.environ.get("REPLICANN_LN_BWD_WAVES", "default"),
                       "ms": round(e0.elapsed_time(e1) / 20, 4)}), flush=True)
 
 
