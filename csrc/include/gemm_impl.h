@@ -872,6 +872,17 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
     }
 }
 
+// true the first time `mask`'s owner launches on the current device (the >64 KiB LDS opt-in
+// attribute is per device; a process may drive several GPUs)
+inline bool first_on_device(uint64_t& mask) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t bit = 1ull << (dev & 63);
+    if (mask & bit) return false;
+    mask |= bit;
+    return true;
+}
+
 template <int BM, int BN, int WM, int WN, bool PIPE, bool AK, bool BK_, int ACT, int NS = 2, int CONV = 0>
 void launch_t(GemmArgs& a, hipStream_t st) {
     constexpr int NT = WM * WN * 64;
@@ -880,9 +891,8 @@ void launch_t(GemmArgs& a, hipStream_t st) {
     static_assert(CONV == 0 || (PIPE && NS > 2), "implicit-GEMM conv loaders live in the NS-stage path");
     auto kmain = gemm_k<BM, BN, WM, WN, AK, BK_, ACT, false, PIPE, false, NS, CONV>;
     auto ksplit = gemm_k<BM, BN, WM, WN, AK, BK_, ACT_NONE, true, PIPE, false, NS, CONV>;
-    static bool attr = false;
-    if (!attr) {  // >64 KiB of dynamic LDS must be opted into, once per instantiation
-        attr = true;
+    static uint64_t attr_devs = 0;  // devices this instantiation opted in on
+    if (first_on_device(attr_devs)) {  // >64 KiB of dynamic LDS must be opted into, per instantiation and device
         (void)hipFuncSetAttribute((const void*)kmain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void*)ksplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
@@ -927,11 +937,9 @@ void launch_fp8_t(GemmArgs& a, hipStream_t st) {
     constexpr int NT = WM * WN * 64;
     const size_t lds = std::max<size_t>(2 * (BM + BN) * BK * 2, (size_t)BM * (BN * 2 + 16));
     auto kmain = gemm_k<BM, BN, WM, WN, true, true, ACT, false, false, true>;
-    static bool attr = false;
-    if (!attr) {
-        attr = true;
+    static uint64_t attr_devs = 0;
+    if (first_on_device(attr_devs))
         (void)hipFuncSetAttribute((const void*)kmain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    }
     a.tiles_m = (a.M + BM - 1) / BM;
     a.tiles_n = (a.N + BN - 1) / BN;
     kmain<<<a.tiles_m * a.tiles_n, NT, lds, st>>>(a);
