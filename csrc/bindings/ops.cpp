@@ -660,11 +660,7 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
     std::vector<long> s;
     for (const Tensor* t : {&q, &k, &v, &o, &dout, &dq, &dk, &dv}) strides_bth(*t, s);
     Tensor delta = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
-    Tensor dk32, dv32;
-    if (!rn_attn_is_fast(D)) {
-        dk32 = at::zeros({B, Tk, H, D}, q.options().dtype(at::kFloat));
-        dv32 = at::zeros({B, Tk, H, D}, q.options().dtype(at::kFloat));
-    }
+    Tensor dk32, dv32;  // (no scratch: the generic path's dK/dV kernel writes dk / dv directly)
     int bias_b = bias && bias->defined() ? bias->size(0) : 1;
     if (B * H * Tq == 0) return;
     // packed-QKV bias gradient: per-64-row-block column partials from the kernels, then one reduction

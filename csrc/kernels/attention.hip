@@ -1224,27 +1224,70 @@ __global__ void __launch_bounds__(256) attn_bwd_generic_k(AttnArgs p) {
         for (int kj = 0; kj < p.Tk; ++kj) acc += ds[kj] * bf2f(p.k[b * p.k_sb + (long)kj * p.k_st + h * p.k_sh + d]);
         dqp[d] = f2bf(acc * p.scale);
     }
-    // dK, dV (fp32 scratch [B][Tk][H][D], atomics)
-    for (long e = threadIdx.x; e < (long)p.Tk * p.D; e += 256) {
-        const int kj = e / p.D, d = e % p.D;
-        const long idx = (((long)b * p.Tk + kj) * p.H + h) * p.D + d;
-        if (ds[kj] != 0.f) atomicAdd(p.dk32 + idx, ds[kj] * qv[d] * p.scale);
-        if (pp[kj] != 0.f) atomicAdd(p.dv32 + idx, pp[kj] * dov[d]);
+    // delta for the dK/dV kernel (dK/dV are NOT accumulated here: that took fp32 atomics across
+    // query rows, i.e. a run-to-run varying summation order)
+    if (threadIdx.x == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qi] = dl;
+}
+
+// Generic-head-size dK/dV, deterministic: one block per key row j sums over the query rows in a
+// fixed order — dVⱼ = Σᵢ P̃ᵢⱼ dOᵢ, dKⱼ = scale · Σᵢ dSᵢⱼ qᵢ with P, dP recomputed from q, k, v, dO,
+// the forward's lse and delta = rowsum(dO∘O) written by attn_bwd_generic_k (same dropout mask:
+// the hash of the same (b, h, i, j) index).  Scalar (odd head sizes only; 32/64/128 run on MFMA).
+__global__ void __launch_bounds__(256) attn_bwd_generic_kv_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* pd = reinterpret_cast<float*>(smem);  // P̃ (dropped, rescaled) per query row
+    float* ds = pd + p.Tq;                       // dS per query row
+    float* kv = ds + p.Tq;                       // k row
+    float* vv = kv + p.D;                        // v row
+    const int kj = blockIdx.x, bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+    const bf16* kp = p.k + b * p.k_sb + (long)kj * p.k_st + h * p.k_sh;
+    const bf16* vp = p.v + b * p.v_sb + (long)kj * p.v_st + h * p.v_sh;
+    for (int d = threadIdx.x; d < p.D; d += 256) {
+        kv[d] = bf2f(kp[d]);
+        vv[d] = bf2f(vp[d]);
+    }
+    __syncthreads();
+    const float lsc = p.lse_log2 ? LN2 : 1.f;
+    const float rd = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+    if (p.p_drop > 0.f && p.seed_ptr) p.seed = *p.seed_ptr;
+    for (int qi = threadIdx.x; qi < p.Tq; qi += 256) {
+        const bf16* qp = p.q + b * p.q_sb + (long)qi * p.q_st + h * p.q_sh;
+        const bf16* dop = p.dout + b * p.do_sb + (long)qi * p.do_st + h * p.do_sh;
+        const float L = p.lse[((long)b * p.H + h) * p.Tq + qi] * lsc;
+        float pv = 0.f, dp = 0.f;
+        if (visible(p, qi, kj) && L != INFINITY) {
+            float sc = 0.f;
+            for (int d = 0; d < p.D; ++d) {
+                sc += bf2f(qp[d]) * kv[d];
+                dp += bf2f(dop[d]) * vv[d];
+            }
+            pv = __expf(sc * p.scale + bias_at(p, b, qi, kj) - L);
+        }
+        float pdv = pv;
+        if (p.p_drop > 0.f) {
+            const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qi, kj)) >= p.p_drop;
+            pdv = keep ? pv * rd : 0.f;
+            dp = keep ? dp * rd : 0.f;
+        }
+        pd[qi] = pdv;
+        ds[qi] = pv * (dp - p.delta[((long)b * p.H + h) * p.Tq + qi]);
+    }
+    __syncthreads();
+    bf16* dkp = p.dk + b * p.dk_sb + (long)kj * p.dk_st + h * p.dk_sh;
+    bf16* dvp = p.dv + b * p.dv_sb + (long)kj * p.dv_st + h * p.dv_sh;
+    for (int d = threadIdx.x; d < p.D; d += 256) {
+        float ak = 0.f, av = 0.f;
+        for (int qi = 0; qi < p.Tq; ++qi) {
+            const float dsv = ds[qi], pdq = pd[qi];
+            if (dsv == 0.f && pdq == 0.f) continue;  // masked (causal / dropped) pairs
+            ak += dsv * bf2f(p.q[b * p.q_sb + (long)qi * p.q_st + h * p.q_sh + d]);
+            av += pdq * bf2f(p.dout[b * p.do_sb + (long)qi * p.do_st + h * p.do_sh + d]);
+        }
+        dkp[d] = f2bf(ak * p.scale);
+        dvp[d] = f2bf(av);
     }
 }
 
-__global__ void scatter_kv_k(AttnArgs p) {
-    const long n = (long)p.B * p.Tk * p.H * p.D;
-    for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-        const int d = e % p.D;
-        const long t1 = e / p.D;
-        const int h = t1 % p.H;
-        const long t2 = t1 / p.H;
-        const int kj = t2 % p.Tk, b = t2 / p.Tk;
-        p.dk[b * p.dk_sb + (long)kj * p.dk_st + h * p.dk_sh + d] = f2bf(p.dk32[e]);
-        p.dv[b * p.dv_sb + (long)kj * p.dv_st + h * p.dv_sh + d] = f2bf(p.dv32[e]);
-    }
-}
 
 #define RN_DISPATCH3(KERN, grid, lds, st, args)                                                       \
     do {                                                                                               \
@@ -1399,11 +1442,19 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
             RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
         }
     } else {
-        if (D > 256 || Tk > 12000 || !dk32 || !dv32) return -1;
+        if (D > 256 || Tk > 12000 || Tq > 12000) return -1;
+        // dQ + delta per query row, then dK/dV per key row: no atomics, bitwise repeatable
         dim3 grid(Tq, B * H);
-        attn_bwd_generic_k<<<grid, 256, (2 * Tk + 2 * D) * 4, st>>>(a);
-        long n = (long)B * Tk * H * D;
-        scatter_kv_k<<<(int)std::min<long>((n + 255) / 256, 4096), 256, 0, st>>>(a);
+        const int lds_q = (2 * Tk + 2 * D) * 4, lds_k = (2 * Tq + 2 * D) * 4;
+        if (lds_q > 65536)
+            (void)hipFuncSetAttribute((const void*)attn_bwd_generic_k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_q);
+        attn_bwd_generic_k<<<grid, 256, lds_q, st>>>(a);
+        dim3 gkv(Tk, B * H);
+        if (lds_k > 65536)
+            (void)hipFuncSetAttribute((const void*)attn_bwd_generic_kv_k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_k);
+        attn_bwd_generic_kv_k<<<gkv, 256, lds_k, st>>>(a);
+        (void)dk32;
+        (void)dv32;
     }
     return 0;
 }

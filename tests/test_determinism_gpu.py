@@ -2,7 +2,7 @@
 
 Every reduction in the framework runs in a fixed order (split-K slabs, column
 sums, LayerNorm partials, attention dK/dV/dQ without atomics, the global grad
-norm), so two runs on the same inputs must agree bit for bit.  The one
+norm; odd head sizes included since round 2), so two runs on the same inputs must agree bit for bit.  The one
 exception is the token-embedding scatter-add, which uses fp32 atomics (order of
 additions varies; bf16 atomics are never used) — it is checked for agreement to
 fp32 rounding instead.
@@ -53,6 +53,27 @@ def test_attention_fwd_bwd_bitwise(cuda, D, drop):
         qkv.grad = None
         rng.manual_seed(5)
         o = ops.attention_packed(qkv, causal=True, dropout_p=drop, training=drop > 0)
+        o.backward(g)
+        return o.detach().clone(), qkv.grad.clone()
+
+    a, b = twice(run)
+    assert same(a, b)
+
+
+@pytest.mark.parametrize("D,drop,causal", [(48, 0.0, True), (80, 0.0, False), (48, 0.1, True)])
+def test_attention_generic_head_bitwise(cuda, D, drop, causal):
+    """Odd head sizes (scalar generic kernels): dQ per query row, dK/dV per key row — no atomics,
+    so the backward is bitwise repeatable too (it used fp32 atomics for dK/dV until round 2)."""
+    from replicann_amd.ops import rng
+    torch.manual_seed(3)
+    H = 4
+    qkv = bf(2, 200, 3, H, D).requires_grad_()
+    g = bf(2, 200, H, D)
+
+    def run():
+        qkv.grad = None
+        rng.manual_seed(6)
+        o = ops.attention_packed(qkv, causal=causal, dropout_p=drop, training=drop > 0)
         o.backward(g)
         return o.detach().clone(), qkv.grad.clone()
 

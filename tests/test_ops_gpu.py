@@ -404,9 +404,18 @@ def test_attention_packed_qkv_bias_grad_d(cuda, D):
 
 
 @pytest.mark.parametrize("D", [4, 48, 80])
-def test_attention_generic_d(cuda, D):
+@pytest.mark.parametrize("causal,Tk", [(True, None), (False, None), (True, 56), (False, 33)])
+def test_attention_generic_d(cuda, D, causal, Tk):
+    """Odd head sizes: generic forward, dQ per query row + deterministic dK/dV per key row."""
     torch.manual_seed(9)
-    _attn_check(2, 40, 3, D, True)
+    _attn_check(2, 40, 3, D, causal, Tk=Tk)
+
+
+@pytest.mark.parametrize("D", [48])
+def test_attention_generic_d_bias(cuda, D):
+    torch.manual_seed(11)
+    bias = torch.randn(1, 40, 40, device="cuda") * 0.5
+    _attn_check(2, 40, 3, D, False, bias=bias)
 
 
 def test_attention_packed_grad(cuda):
