@@ -46,6 +46,7 @@ void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int
 void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
 void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, int, hipStream_t);
 void rn_emb_bwd_acc(const int64_t*, const void*, float*, unsigned*, void*, void*, int, int, int, int, hipStream_t);
+void rn_emb_bwd_acc_det(const int64_t*, const void*, void*, unsigned*, void*, void*, int, int, int, int, hipStream_t);
 void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
 int rn_norm_ws_floats();
 void rn_sumsq(const void*, long, int, float*, float*, hipStream_t);
@@ -566,25 +567,32 @@ void embedding_bwd_acc(const Tensor& dx, const Tensor& ids, const Tensor& gwte, 
         CHECK_BF16(*gwpe); CHECK_CONTIG(*gwpe);
         TORCH_CHECK(gwpe->size(0) >= T && gwpe->size(1) == E);
     }
-    static std::map<std::tuple<int, int64_t, int64_t>, std::pair<Tensor, Tensor>> scratch;
+    // REPLICANN_DETERMINISTIC=1: 64-bit fixed-point scratch, order-independent integer atomics
+    const char* de = std::getenv("REPLICANN_DETERMINISTIC");
+    const bool det = de && de[0] == '1';
+    static std::map<std::tuple<int, int64_t, int64_t, int>, std::pair<Tensor, Tensor>> scratch;
     static std::mutex mu;
     std::pair<Tensor, Tensor> buf;
     {
         std::lock_guard<std::mutex> lk(mu);
-        auto key = std::make_tuple((int)dx.get_device(), V, E);
+        auto key = std::make_tuple((int)dx.get_device(), V, E, (int)det);
         auto it = scratch.find(key);
         if (it == scratch.end()) {
             hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
             (void)hipStreamIsCapturing(cur_stream(), &cs);
             TORCH_CHECK(cs == hipStreamCaptureStatusNone,
                         "embedding_bwd_acc: first call must be eager (scratch allocation)");
-            Tensor d32 = at::zeros({V * E}, dx.options().dtype(at::kFloat));
+            Tensor d32 = at::zeros({V * E * (det ? 2 : 1)}, dx.options().dtype(at::kFloat));
             Tensor own = at::full({V}, -1, dx.options().dtype(at::kInt));
             it = scratch.emplace(key, std::make_pair(d32, own)).first;
         }
         buf = it->second;
     }
-    if (ids.numel())
+    if (ids.numel() && det)
+        rn_emb_bwd_acc_det(ids.data_ptr<int64_t>(), dx.data_ptr(), buf.first.data_ptr(),
+                           reinterpret_cast<unsigned*>(buf.second.data_ptr<int>()), gwte.data_ptr(),
+                           (gwpe && gwpe->defined()) ? gwpe->data_ptr() : nullptr, B, T, (int)E, (int)V, cur_stream());
+    else if (ids.numel())
         rn_emb_bwd_acc(ids.data_ptr<int64_t>(), dx.data_ptr(), buf.first.data_ptr<float>(),
                        reinterpret_cast<unsigned*>(buf.second.data_ptr<int>()), gwte.data_ptr(),
                        (gwpe && gwpe->defined()) ? gwpe->data_ptr() : nullptr, B, T, (int)E, (int)V, cur_stream());

@@ -76,6 +76,47 @@ __global__ void __launch_bounds__(256) emb_finish_k(const int64_t* __restrict__ 
     if (lane == 0) owner[id] = 0xFFFFFFFFu;
 }
 
+// Deterministic variant (REPLICANN_DETERMINISTIC=1): the same owner scheme, but the scratch
+// accumulates 64-bit FIXED-POINT values (x · 2^32, exact for a bf16 input) with integer atomics,
+// whose sum does not depend on the order the rows arrive in — unlike fp32 atomics.  Range ±2^31
+// per element, resolution 2^-32 (far below a bf16 ulp of any gradient that survives the final
+// bf16 add); twice the scratch bytes and atomic traffic of the fp32 path.
+constexpr float FX_SCALE = 4294967296.f;  // 2^32
+
+__global__ void __launch_bounds__(256) emb_scatter_own_fx_k(const int64_t* __restrict__ ids,
+                                                            const bf16* __restrict__ dx,
+                                                            unsigned long long* __restrict__ d64,
+                                                            unsigned* __restrict__ owner, int rows, int E, int V) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long id = ids[row];
+    RN_CHECK(id >= 0 && id < V);
+    if (lane == 0) atomicMin(owner + id, (unsigned)row);
+    for (int c = lane; c < E; c += 64) {
+        const long long fx = __float2ll_rn(bf2f(dx[(long)row * E + c]) * FX_SCALE);
+        atomicAdd(d64 + id * E + c, (unsigned long long)fx);  // two's complement: signed sum
+    }
+}
+
+__global__ void __launch_bounds__(256) emb_finish_fx_k(const int64_t* __restrict__ ids,
+                                                       unsigned long long* __restrict__ d64,
+                                                       unsigned* __restrict__ owner, bf16* __restrict__ g, int rows,
+                                                       int E) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long id = ids[row];
+    if (owner[id] != (unsigned)row) return;
+    for (int c = lane; c < E; c += 64) {
+        const long long v = (long long)d64[id * E + c];
+        d64[id * E + c] = 0ull;
+        bf16* q = g + id * E + c;
+        q[0] = (bf16)((float)q[0] + (float)((double)v * (1.0 / 4294967296.0)));
+    }
+    if (lane == 0) owner[id] = 0xFFFFFFFFu;
+}
+
 // dwpe[t] += sum_b dx[b, t]
 __global__ void emb_pos_acc_k(const bf16* __restrict__ dx, bf16* __restrict__ dwpe, int B, int T, int E) {
     const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -308,6 +349,16 @@ void rn_emb_bwd_acc(const int64_t* ids, const void* dx, float* d32, unsigned* ow
     const int rows = B * T;
     emb_scatter_own_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (const bf16*)dx, d32, owner, rows, E, V);
     emb_finish_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, d32, owner, (bf16*)gwte, rows, E);
+    if (gwpe) emb_pos_acc_k<<<rn_cdiv((long)T * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)gwpe, B, T, E);
+}
+
+// deterministic variant: d64 = persistent zeroed V×E 64-bit scratch
+void rn_emb_bwd_acc_det(const int64_t* ids, const void* dx, void* d64, unsigned* owner, void* gwte, void* gwpe, int B,
+                        int T, int E, int V, hipStream_t st) {
+    const int rows = B * T;
+    emb_scatter_own_fx_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (const bf16*)dx, (unsigned long long*)d64, owner, rows,
+                                                        E, V);
+    emb_finish_fx_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (unsigned long long*)d64, owner, (bf16*)gwte, rows, E);
     if (gwpe) emb_pos_acc_k<<<rn_cdiv((long)T * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)gwpe, B, T, E);
 }
 

@@ -5,7 +5,8 @@ sums, LayerNorm partials, attention dK/dV/dQ without atomics, the global grad
 norm; odd head sizes included since round 2), so two runs on the same inputs must agree bit for bit.  The one
 exception is the token-embedding scatter-add, which uses fp32 atomics (order of
 additions varies; bf16 atomics are never used) — it is checked for agreement to
-fp32 rounding instead.
+fp32 rounding instead; with REPLICANN_DETERMINISTIC=1 the training path's scatter
+accumulates 64-bit fixed point with integer atomics and is bitwise repeatable too.
 """
 
 import pytest
@@ -147,3 +148,46 @@ def test_embedding_scatter_close(cuda):
     ref = torch.zeros(V, E, device="cuda").index_add_(0, ids.reshape(-1), g.reshape(-1, E).float())
     assert ((a - b).abs().max() <= 1e-2 * ref.abs().max())
     assert ((a - ref).norm() / ref.norm()) < 1e-2
+
+
+def test_embedding_scatter_deterministic_mode(cuda, monkeypatch):
+    """REPLICANN_DETERMINISTIC=1: the flat-buffer (training) embedding backward is bitwise repeatable
+    under heavy id repetition and matches the fp32 index_add reference."""
+    from replicann_amd.utils.flat import FlatParams
+
+    monkeypatch.setenv("REPLICANN_DETERMINISTIC", "1")
+    torch.manual_seed(7)
+    V, E = 1000, 256
+    mod = torch.nn.Module()
+    mod.wte = torch.nn.Parameter(bf(V, E))
+    flat = FlatParams(mod)
+    ids = torch.randint(0, 50, (8, 128), device="cuda")  # many repeats per row
+    g = bf(8, 128, E)
+
+    def run():
+        flat.zero_grad()
+        ops.embedding(ids, mod.wte).backward(g)
+        return mod.wte.grad.float().clone()
+
+    a, b = twice(run)
+    assert torch.equal(a, b)
+    ref = torch.zeros(V, E, device="cuda").index_add_(0, ids.reshape(-1), g.reshape(-1, E).float())
+    assert ((a - ref).norm() / ref.norm()) < 1e-2
+
+
+def test_training_step_bitwise_deterministic_mode(cuda, monkeypatch):
+    """With REPLICANN_DETERMINISTIC=1 a whole GPT-2 training run (embedding scatter, GEMMs incl.
+    split-K, attention, LayerNorm, CE, grad-norm, AdamW with stochastic rounding) repeats bit for bit."""
+    from replicann_amd.training import TrainConfig, Trainer
+
+    monkeypatch.setenv("REPLICANN_DETERMINISTIC", "1")
+
+    def run():
+        cfg = TrainConfig(model="gpt2-tiny", batch_size=4, seq_len=128, steps=100, warmup_steps=1, lr=1e-3,
+                          log_every=10**9, seed=11, graph="off")
+        tr = Trainer(cfg)
+        losses = [float(tr.step()) for _ in range(4)]
+        return losses, tr.flat.data.clone()
+
+    (la, wa), (lb, wb) = run(), run()
+    assert la == lb and torch.equal(wa, wb)
