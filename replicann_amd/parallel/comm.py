@@ -132,9 +132,11 @@ def _is_nccl(group=None) -> bool:
 
 def make_comm(kind: str = "auto", group=None, device=None, timeout_s: float = 600.0):
     """``kind``: ``auto`` (env ``REPLICANN_COMM`` if set; else native on an nccl group),
-    ``native`` or ``torch``."""
+    ``native`` or ``torch``.  ``REPLICANN_COMM_TIMEOUT`` overrides ``timeout_s``."""
     if kind == "auto":
         kind = os.environ.get("REPLICANN_COMM", "auto")
+    # REPLICANN_COMM_TIMEOUT (seconds): the native watchdog's hang limit per collective
+    timeout_s = float(os.environ.get("REPLICANN_COMM_TIMEOUT", timeout_s))
     dev = torch.device(device) if device is not None else None
     if kind == "auto":
         if _is_nccl(group) and (dev is None or dev.type == "cuda"):

@@ -353,6 +353,9 @@ class Trainer:
                 extra = self.timer.summary()  # forward_ms, backward_ms, allreduce_wait_ms (comm wait), optimizer_ms
                 if self.ddp is not None:
                     extra["comm_host_ms"] = round(self.ddp.comm_wait_ms, 3)
+                    if hasattr(self.ddp.comm, "info"):  # native communicator: issued collectives / bytes
+                        ci = self.ddp.comm.info()
+                        extra["comm_collectives"], extra["comm_gbytes"] = ci["collectives"], round(ci["bytes"] / 1e9, 3)
                 self.logger.log(step=i, loss=round(lv, 5), lr=round(float(self.opt._host_lr(None)), 8),
                                 **self._throughput(i - start, dt), **extra)
                 last = lv
