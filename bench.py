@@ -6,7 +6,13 @@ whole node, synthetic 1024-token sequences, random-init weights.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One rank per GPU over RCCL.  W untimed warm-up steps, then EXACTLY K timed
+One rank per GPU over RCCL.  Without an external launcher (no WORLD_SIZE in the
+environment) ``--gpus N`` with N > 1 makes this process a launcher: it never touches
+the GPU, spawns N fresh worker processes of itself (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / a free MASTER_PORT), forwards rank 0's output and exits with
+the worst worker exit code.  A worker whose process group or communicator does not
+span exactly ``--gpus`` ranks exits non-zero instead of reporting a number.
+W untimed warm-up steps, then EXACTLY K timed
 steps bracketed by barrier + device synchronize on both sides; the elapsed
 time is the MAX over ranks.  Every timed step is a full training step:
 forward, loss, backward, bucketed gradient all-reduce, grad-norm clip and
@@ -23,20 +29,18 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 METRIC = "train-step samples/sec (whole node), GPT-2-small DDP at 1/2/4/8 MI355X"
 OTHER_METRICS = {  # secondary BASELINE.json configs (same harness)
     "gpt2-medium": "train-step samples/sec (whole node), GPT-2-medium bf16",
     "gpt2-medium-fp8": "train-step samples/sec (whole node), GPT-2-medium fp8 forward GEMMs",
     "vit-b16": "train-step images/sec (whole node), ViT-B/16 bf16 DDP",
     "resnet18": "train-step images/sec (whole node), ResNet-18 bf16",
+    "mlp": "train-step samples/sec, 2-layer MLP on MNIST-shaped tensors (CPU plumbing config)",
 }
 BASELINE_VALUE = None  # the reference publishes no number
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -49,20 +53,71 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--ddp", default="auto", choices=["auto", "on"],
                     help="on: run the data-parallel step (buckets, fp32 widening, collectives) even on 1 GPU")
-    ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch"],
-                    help="collective back-end: native RCCL communicator (csrc/comm) or torch.distributed")
+    ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
+                    help="collective back-end: native RCCL communicator (csrc/comm), torch.distributed, or "
+                         "proxy (1-GPU stand-in with RCCL's CU/HBM footprint, for interference measurements)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra torch.profiler steps (not timed)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="capture the whole training step as one hipGraph (auto: on for 1 process)")
-    args = ap.parse_args()
+    ap.add_argument("--device", default=None, help="cpu: run the same harness on the CPU/gloo path (tests)")
+    return ap.parse_args(argv)
+
+
+def launch_workers(args, argv):
+    """``--gpus N`` without an external launcher: N fresh worker processes of this script, one
+    per GPU (the parent imports nothing that initialises the GPU and never execs)."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [None] * len(procs)
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):  # one rank failed: the others would hang in a collective
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.2)
+    bad = [rc for rc in rcs if rc]
+    return (max(abs(rc) for rc in bad) or 1) if bad else 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_workers(args, argv))
+
+    import torch
+    import torch.distributed as dist
 
     from replicann_amd import _ext
     from replicann_amd.training import TrainConfig, Trainer
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
-    if torch.cuda.is_available() and not _ext.available():
+        print(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks", file=sys.stderr)
+        sys.exit(3)
+    if torch.cuda.is_available() and args.device != "cpu" and not _ext.available():
         raise RuntimeError(f"native extension missing: {_ext.load_error()}")
 
     is_lm = args.model.startswith("gpt2")
@@ -72,10 +127,15 @@ def main():
                       optimizer="adamw" if not args.model.startswith("resnet") else "sgd",
                       weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,
                       warmup_steps=10, lr=3e-4 if args.model.startswith("gpt2-medium") else 6e-4, bucket_mb=args.bucket_mb, log_every=10**9,
-                      graph=args.graph, ddp=args.ddp, comm=args.comm)
+                      graph=args.graph, ddp=args.ddp, comm=args.comm, device=args.device)
     tr = Trainer(cfg)
     world = tr.world
     dev = tr.device
+    comm_world = tr.ddp.comm.world if tr.ddp is not None else 1
+    if world != args.gpus or (args.comm != "proxy" and comm_world != world):
+        print(f"error: --gpus {args.gpus} but the process group has {world} ranks and the "
+              f"communicator {comm_world}", file=sys.stderr)
+        sys.exit(3)
 
     def sync():
         if dev.type == "cuda":
@@ -113,13 +173,18 @@ def main():
         with open("gpurun_out/torch_profile.txt", "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
 
+    graphs = [tr._graph is not None]
+    if world > 1:  # per-rank capture state (every rank must run the same step form)
+        graphs = [None] * world
+        dist.all_gather_object(graphs, tr._graph is not None)
+
     ms = elapsed * 1000 / args.steps
     samples = cfg.batch_size * world * args.steps
     value = samples / elapsed
     out = {
         "metric": METRIC if args.model == "gpt2-small" else OTHER_METRICS.get(args.model, args.model),
         "value": round(value, 3),
-        "unit": "samples/s" if is_lm else "images/s",
+        "unit": "samples/s" if (is_lm or args.model == "mlp") else "images/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -127,8 +192,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-        "dtype": "bf16",
+        "dtype": precision(tr.model),
         "data": ("synthetic (random bigram-chain token source, random-init weights)" if is_lm
+                 else "synthetic (random MNIST-shaped tensors and labels, random-init weights)" if args.model == "mlp"
                  else "synthetic (random images and labels, random-init weights)"),
         "config": {
             "model": args.model,
@@ -139,13 +205,16 @@ def main():
             "tokens_per_s": round(value * args.seq, 1) if is_lm else None,
             "optimizer": ("fused AdamW" if cfg.optimizer == "adamw" else "fused SGD-momentum")
             + " (fp32 master) + grad-norm clip",
-            "hipgraph": tr._graph is not None,
+            "hipgraph": graphs,
             "comm": (tr.ddp.comm.name if tr.ddp is not None else None),
+            "comm_world": comm_world,
+            "gemm_cu_reserve": (int(torch.ops.replicann.gemm_get_reserve())
+                                if dev.type == "cuda" and hasattr(torch.ops.replicann, "gemm_get_reserve") else None),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         },
     }
     if tr.rank == 0:
-        if dev.type == "cuda":  # the measured per-shape GEMM configs (runtime autotuner)
+        if dev.type == "cuda" and os.path.isdir("gpurun_out"):  # the measured per-shape GEMM configs (runtime autotuner)
             os.makedirs("gpurun_out", exist_ok=True)
             with open(f"gpurun_out/gemm_tuning_{args.model}.json", "w") as f:
                 f.write(torch.ops.replicann.gemm_tuning_table())
@@ -154,6 +223,15 @@ def main():
         dist.barrier()
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def precision(model) -> str:
+    """The compute precision the timed step actually runs (not just the parameter dtype)."""
+    cfg = getattr(model, "config", None)
+    if getattr(cfg, "fp8", False):
+        return getattr(model, "fp8_description", lambda: "fp8-e4m3 GEMMs + bf16")()
+    p = next(model.parameters())
+    return {"torch.bfloat16": "bf16", "torch.float32": "fp32"}.get(str(p.dtype), str(p.dtype))
 
 
 if __name__ == "__main__":

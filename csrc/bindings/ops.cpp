@@ -56,6 +56,11 @@ int rn_adamw(void*, float*, const void*, int, float*, float*, const uint8_t*, fl
 void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, long, float, float, int, float, float,
             hipStream_t);
 long rn_gemm_ws_floats(int, int, int);
+void rn_gemm_set_sched(int);
+int rn_gemm_get_sched();
+void rn_gemm_set_reserve(int);
+int rn_gemm_get_reserve();
+int rn_gemm_sched_init(int);
 int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, float*, const float*, int, int, int,
             long, long, long, int, int, int, int, int, int, int, hipStream_t, float*);
 int rn_gemm_cfg_bm(int);
@@ -1043,6 +1048,11 @@ TORCH_LIBRARY(replicann, m) {
     m.def("native_version() -> int");
     m.def("gemm_tuning_table() -> str");
     m.def("gemm_tuning_load(str table) -> int");
+    m.def("gemm_set_sched(int mode) -> ()");
+    m.def("gemm_get_sched() -> int");
+    m.def("gemm_set_reserve(int cus) -> ()");
+    m.def("gemm_get_reserve() -> int");
+    m.def("gemm_sched_init(int device) -> int");
 }
 
 TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
@@ -1091,8 +1101,20 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("fp8_quant_many", &fp8_quant_many);
 }
 
+// persistent-GEMM schedule knobs (csrc/include/gemm_pk.h: dynamic tile queue, CU reservation)
+void gemm_set_sched(int64_t m) { rn_gemm_set_sched((int)m); }
+int64_t gemm_get_sched() { return rn_gemm_get_sched(); }
+void gemm_set_reserve(int64_t r) { rn_gemm_set_reserve((int)r); }
+int64_t gemm_get_reserve() { return rn_gemm_get_reserve(); }
+int64_t gemm_sched_init(int64_t dev) { return rn_gemm_sched_init((int)dev); }
+
 TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {
     m.impl("native_version", &native_version);
+    m.impl("gemm_set_sched", &gemm_set_sched);
+    m.impl("gemm_get_sched", &gemm_get_sched);
+    m.impl("gemm_set_reserve", &gemm_set_reserve);
+    m.impl("gemm_get_reserve", &gemm_get_reserve);
+    m.impl("gemm_sched_init", &gemm_sched_init);
     m.impl("gemm_tuning_table", &gemm_tuning_table);
     m.impl("gemm_tuning_load", &gemm_tuning_load);
 }

@@ -18,6 +18,11 @@
 //    the communicator is aborted (ncclCommAbort unblocks every pending RCCL kernel) and the next
 //    call raises, naming the collective that hung.
 //
+//  * proxy mode (comm_init_proxy): no RCCL communicator; every collective launches the comm-proxy
+//    kernel (csrc/kernels/comm_proxy.hip) on the same comm stream with the same fork/join, moving
+//    the emulated W-rank ring's per-GPU volume at an xGMI-like rate — the one-GPU stand-in that
+//    makes the backward's GEMM ↔ collective interference measurable (bench.py --comm proxy).
+//
 // Handles are small integers into a process-wide table so they pass through TORCH_LIBRARY schemas.
 
 #include <ATen/ATen.h>
@@ -31,11 +36,14 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
+
+extern "C" void rn_comm_proxy(void* buf, long bytes, double volume_bytes, int wgs, double gbps, hipStream_t st);
 
 namespace {
 
@@ -58,20 +66,29 @@ struct Comm {
     int rank = 0, world = 1, device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t fork = nullptr;  // recorded on the caller's stream, waited by the comm stream
-    hipEvent_t done = nullptr;  // recorded on the comm stream after every collective
-    // watchdog state
+    hipEvent_t done = nullptr;        // recorded on the comm stream after every collective (capture-safe join)
+    hipEvent_t done_eager = nullptr;  // recorded after EAGER collectives only (never inside a capture)
+    // watchdog state: one pooled event per outstanding eager collective, oldest first
     std::mutex mu;
     std::condition_variable cv;
     std::thread watchdog;
     bool stop = false;
-    bool armed = false;  // an eager collective is in flight (captured ones are not watched)
-    std::chrono::steady_clock::time_point issued;
-    std::string last_op;
+    struct Pending {
+        hipEvent_t ev;
+        std::chrono::steady_clock::time_point issued;
+        std::string op;
+    };
+    std::deque<Pending> pending;
+    std::vector<hipEvent_t> free_events;
     double timeout_s = 600.0;
     std::atomic<int> failed{0};  // 0 ok, 1 timed out, 2 async RCCL error
     std::string failure;
     int64_t n_collectives = 0;
     int64_t bytes = 0;
+    // proxy mode: emulated world size, workgroups, per-GPU bus bandwidth (GB/s)
+    bool proxy = false;
+    int proxy_world = 8, proxy_wgs = 32;
+    double proxy_gbps = 300.0;
 
     void stop_watchdog() {
         {
@@ -84,6 +101,16 @@ struct Comm {
     // at process exit (static destruction) only the thread is stopped: the HIP runtime and the
     // peers may already be gone, so no stream/communicator teardown happens here
     ~Comm() { stop_watchdog(); }
+    hipEvent_t take_event() {  // under mu
+        if (!free_events.empty()) {
+            hipEvent_t e = free_events.back();
+            free_events.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        return e;
+    }
 };
 
 std::mutex g_mu;
@@ -112,26 +139,28 @@ void watchdog_loop(Comm* c) {
         c->cv.wait_for(lk, std::chrono::milliseconds(100));
         if (c->stop || c->failed.load()) continue;
         ncclResult_t async = ncclSuccess;
-        if (ncclCommGetAsyncError(c->comm, &async) == ncclSuccess && async != ncclSuccess &&
+        if (c->comm && ncclCommGetAsyncError(c->comm, &async) == ncclSuccess && async != ncclSuccess &&
             async != ncclInProgress) {
             c->failure = std::string("asynchronous RCCL error: ") + ncclGetErrorString(async);
             c->failed = 2;
             ncclCommAbort(c->comm);
             continue;
         }
-        if (!c->armed) continue;
+        if (c->pending.empty()) continue;
         hipSetDevice(c->device);
-        hipError_t q = hipEventQuery(c->done);
-        if (q == hipSuccess) {
-            c->armed = false;
-            continue;
+        // retire finished collectives in issue order; the timeout runs from the OLDEST unfinished
+        while (!c->pending.empty() && hipEventQuery(c->pending.front().ev) == hipSuccess) {
+            c->free_events.push_back(c->pending.front().ev);
+            c->pending.pop_front();
         }
-        double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->issued).count();
-        if (q == hipErrorNotReady && waited > c->timeout_s) {
-            c->failure = "collective '" + c->last_op + "' did not complete within " +
-                         std::to_string(c->timeout_s) + " s (a peer rank is missing or hung)";
+        if (c->pending.empty()) continue;
+        const auto& old = c->pending.front();
+        double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - old.issued).count();
+        if (waited > c->timeout_s) {
+            c->failure = "collective '" + old.op + "' did not complete within " + std::to_string(c->timeout_s) +
+                         " s (a peer rank is missing or hung)";
             c->failed = 1;
-            ncclCommAbort(c->comm);
+            if (c->comm) ncclCommAbort(c->comm);
         }
     }
 }
@@ -164,11 +193,7 @@ bool fork_from_current(Comm& c) {
     hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(c.device).stream();
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     HIP_OK(hipStreamIsCapturing(cs, &st));
-    bool cap = st == hipStreamCaptureStatusActive;
-    if (cap) {  // captured collectives are not watched (their done event is a capture dependency)
-        std::lock_guard<std::mutex> lk(c.mu);
-        c.armed = false;
-    }
+    bool cap = st == hipStreamCaptureStatusActive;  // captured collectives are not watched
     HIP_OK(hipEventRecord(c.fork, cs));
     HIP_OK(hipStreamWaitEvent(c.stream, c.fork, 0));
     return cap;
@@ -179,11 +204,17 @@ void after_issue(Comm& c, bool capturing, const char* what, int64_t nbytes) {
     c.n_collectives += 1;
     c.bytes += nbytes;
     if (!capturing) {
+        HIP_OK(hipEventRecord(c.done_eager, c.stream));
         std::lock_guard<std::mutex> lk(c.mu);
-        c.armed = true;
-        c.issued = std::chrono::steady_clock::now();
-        c.last_op = what;
+        hipEvent_t e = c.take_event();
+        HIP_OK(hipEventRecord(e, c.stream));
+        c.pending.push_back({e, std::chrono::steady_clock::now(), what});
     }
+}
+
+// proxy mode: the emulated collective's per-GPU volume through the proxy kernel
+void proxy_issue(Comm& c, const Tensor& t, double volume) {
+    rn_comm_proxy(t.data_ptr(), t.numel() * t.element_size(), volume, c.proxy_wgs, c.proxy_gbps, c.stream);
 }
 
 // ---------------------------------------------------------------- ops
@@ -214,7 +245,32 @@ int64_t comm_init(const Tensor& uid, int64_t rank, int64_t world, int64_t device
     HIP_OK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
     HIP_OK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->done_eager, hipEventDisableTiming));
     RCCL_CHECK(ncclCommInitRank(&c->comm, (int)world, id, (int)rank));
+    c->watchdog = std::thread(watchdog_loop, c.get());
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_comms.push_back(std::move(c));
+    return (int64_t)g_comms.size() - 1;
+}
+
+int64_t comm_init_proxy(int64_t device, int64_t world, int64_t wgs, double gbps, double timeout_s) {
+    TORCH_CHECK(world >= 1 && wgs >= 1 && gbps > 0, "comm_init_proxy: world >= 1, wgs >= 1, gbps > 0");
+    auto c = std::make_unique<Comm>();
+    c->rank = 0;
+    c->world = 1;  // the process group is one rank; proxy_world is what the volume emulates
+    c->device = (int)device;
+    c->timeout_s = timeout_s;
+    c->proxy = true;
+    c->proxy_world = (int)world;
+    c->proxy_wgs = (int)wgs;
+    c->proxy_gbps = gbps;
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(at::Device(at::kCUDA, (int)device));
+    int lo = 0, hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_OK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+    HIP_OK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->done_eager, hipEventDisableTiming));
     c->watchdog = std::thread(watchdog_loop, c.get());
     std::lock_guard<std::mutex> lk(g_mu);
     g_comms.push_back(std::move(c));
@@ -229,8 +285,12 @@ void comm_all_reduce(int64_t h, Tensor t, int64_t op) {
                 ", communicator on cuda:", c.device);
     c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
     bool cap = fork_from_current(c);
-    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), nccl_op(op), c.comm,
-                             c.stream));
+    if (c.proxy) {  // ring all-reduce: reduce-scatter + all-gather, each (W-1)/W of the buffer
+        const double S = (double)t.numel() * t.element_size();
+        proxy_issue(c, t, 2.0 * (c.proxy_world - 1) / c.proxy_world * S);
+    } else
+        RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), nccl_op(op), c.comm,
+                                 c.stream));
     after_issue(c, cap, "all_reduce", t.numel() * t.element_size());
 }
 
@@ -240,8 +300,10 @@ void comm_broadcast(int64_t h, Tensor t, int64_t root) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "comm_broadcast: needs a contiguous GPU tensor");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
     bool cap = fork_from_current(c);
-    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), (int)root, c.comm,
-                             c.stream));
+    if (c.proxy) proxy_issue(c, t, (double)t.numel() * t.element_size());
+    else
+        RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), (int)root, c.comm,
+                                 c.stream));
     after_issue(c, cap, "broadcast", t.numel() * t.element_size());
 }
 
@@ -253,8 +315,13 @@ void comm_all_gather(int64_t h, const Tensor& in, Tensor out) {
                     out.scalar_type() == in.scalar_type(),
                 "comm_all_gather: out must hold world x in.numel() elements of in's dtype");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
+    // proxy, world 1: the result is the input, copied on the caller's stream before the fork
+    if (c.proxy) out.copy_(in.reshape(out.sizes()));
     bool cap = fork_from_current(c);
-    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), c.comm, c.stream));
+    if (c.proxy) {
+        proxy_issue(c, out, (double)(c.proxy_world - 1) / c.proxy_world * out.numel() * out.element_size() * c.proxy_world);
+    } else
+        RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), c.comm, c.stream));
     after_issue(c, cap, "all_gather", out.numel() * out.element_size());
 }
 
@@ -266,9 +333,14 @@ void comm_reduce_scatter(int64_t h, const Tensor& in, Tensor out, int64_t op) {
                     out.scalar_type() == in.scalar_type(),
                 "comm_reduce_scatter: in must hold world x out.numel() elements of out's dtype");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
+    // proxy, world 1: the result is the input, copied on the caller's stream before the fork
+    if (c.proxy) out.copy_(in.reshape(out.sizes()));
     bool cap = fork_from_current(c);
-    RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), nccl_dtype(in), nccl_op(op),
-                                 c.comm, c.stream));
+    if (c.proxy) {
+        proxy_issue(c, out, (double)(c.proxy_world - 1) / c.proxy_world * out.numel() * out.element_size() * c.proxy_world);
+    } else
+        RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), nccl_dtype(in), nccl_op(op),
+                                     c.comm, c.stream));
     after_issue(c, cap, "reduce_scatter", in.numel() * in.element_size());
 }
 
@@ -278,14 +350,18 @@ void comm_wait(int64_t h) {
     check_alive(c);
     c10::hip::HIPGuardMasqueradingAsCUDA guard(at::Device(at::kCUDA, c.device));
     hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(c.device).stream();
-    HIP_OK(hipStreamWaitEvent(cs, c.done, 0));
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    HIP_OK(hipStreamIsCapturing(cs, &st));
+    // inside a capture: join the collectives recorded in it; eager: the last eager collective
+    // (an event last recorded inside a finished capture must not be waited on eagerly)
+    HIP_OK(hipStreamWaitEvent(cs, st == hipStreamCaptureStatusActive ? c.done : c.done_eager, 0));
 }
 
 // host blocks until every issued collective finished (raises if the communicator was aborted)
 void comm_synchronize(int64_t h) {
     Comm& c = get(h);
     c10::hip::HIPGuardMasqueradingAsCUDA guard(at::Device(at::kCUDA, c.device));
-    while (hipEventQuery(c.done) == hipErrorNotReady) {
+    while (hipEventQuery(c.done_eager) == hipErrorNotReady) {
         check_alive(c);
         std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
@@ -315,10 +391,13 @@ void comm_destroy(int64_t h) {
     c10::hip::HIPGuardMasqueradingAsCUDA guard(at::Device(at::kCUDA, c->device));
     if (c->failed.load() == 0) {
         hipStreamSynchronize(c->stream);
-        ncclCommDestroy(c->comm);
+        if (c->comm) ncclCommDestroy(c->comm);
     }
     hipEventDestroy(c->fork);
     hipEventDestroy(c->done);
+    hipEventDestroy(c->done_eager);
+    for (auto& p : c->pending) hipEventDestroy(p.ev);
+    for (auto e : c->free_events) hipEventDestroy(e);
     hipStreamDestroy(c->stream);
 }
 
@@ -327,6 +406,7 @@ void comm_destroy(int64_t h) {
 TORCH_LIBRARY_FRAGMENT(replicann, m) {
     m.def("comm_unique_id() -> Tensor", &comm_unique_id);
     m.def("comm_init(Tensor uid, int rank, int world, int device, float timeout_s) -> int", &comm_init);
+    m.def("comm_init_proxy(int device, int world, int wgs, float gbps, float timeout_s) -> int", &comm_init_proxy);
     m.def("comm_all_reduce(int h, Tensor(a!) t, int op) -> ()", &comm_all_reduce);
     m.def("comm_broadcast(int h, Tensor(a!) t, int root) -> ()", &comm_broadcast);
     m.def("comm_all_gather(int h, Tensor inp, Tensor(a!) out) -> ()", &comm_all_gather);

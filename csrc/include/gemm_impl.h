@@ -61,6 +61,9 @@ struct GemmArgs {
     // staged epilogue of the one-tile-per-block kernels only
     uint8_t* q8;
     float* q8st;
+    // persistent kernel (cfg 9) only: dynamic tile queue counters (gemm_pk.h, "Tile schedule"),
+    // nullptr = static walk
+    int* sched;
 };
 
 template <int BN, int NT>

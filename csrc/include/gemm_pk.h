@@ -36,6 +36,26 @@
 //     the in-flight operand DMA; epilogues that read a full tile (residual, saved
 //     pre-activation, accumulate target) do wait for it.
 //
+// Tile schedule (p.sched != nullptr; the default, see rn_gemm_set_sched): the grid does not walk a
+// static list (bid + s·grid) but DEQUEUES its work, so a workgroup that starts late — because an
+// RCCL kernel on the comm stream held its CU when the GEMM launched — simply takes fewer tiles
+// instead of delaying the whole GEMM by the collective's duration.
+//   * work unit = C consecutive items (tile × split-K slice), C·nk ≥ 5 K-tiles, so one dequeue
+//     has ≥ 20 phases to come back before the DMA cursor needs the next unit;
+//   * one queue per dispatch group (blockIdx & 7: the blocks that share an XCD and its L2) over
+//     exactly the units the static walk would give that group in all but its last round, plus
+//     one shared tail queue over the rest: the same L2 locality as the static walk, balanced at
+//     the end;
+//   * wave 0 lane 0 issues the returning atomic (a range-checked buffer atomic: the other lanes'
+//     offsets are out of range, so exec stays full) right after a phase's DMA issue; it is
+//     COUNTED like a DMA: wave 0's waits allow one more outstanding op for the next 4 phases and
+//     the 5th retires it (vmcnt is in order), then the unit id goes to a 4-slot LDS ring past the
+//     operand ring, read by every wave ≥ 1 phase later (the DMA placement rule);
+//   * the counters (home 0-7, tail, exit; one 128-B line each) reset themselves: the last block
+//     to finish zeroes them, so a slot is reusable by the next launch on the stream and graph
+//     replays need no memset node.
+// Outputs are bitwise identical to the static walk's (same per-tile K order and epilogue).
+//
 // LDS images (all written lane-linearly by the DMA, the XOR swizzle applied to the per-lane
 // SOURCE address and again on the read, guide rule 21):
 //   K-contiguous operand, A side: [128 rows][64 k] 128-B rows, chunk c of row r at c ^ swz_kc(r);
@@ -51,7 +71,10 @@
 namespace rn_gemm_detail {
 
 constexpr int PK_HALF = 16384;  // bytes per half-tile slot
-constexpr int PK_LDS = 8 * PK_HALF;
+constexpr int PK_RING = 8 * PK_HALF;   // operand ring
+constexpr int PK_LDS = PK_RING + 64;   // + the dynamic schedule's unit-id ring (4 ints)
+constexpr int PK_CTR_STRIDE = 32;      // ints between schedule counters (one 128-B line each)
+constexpr int PK_SCHED_INTS = 10 * PK_CTR_STRIDE;
 
 RN_DEV int swz_kcp(int r) { return (((r >> 3) & 3) << 1) | ((r >> 1) & 1); }
 RN_DEV int swz_mnp(int k) { return ((k >> 1) & 1) | (((k >> 3) & 1) << 2); }
@@ -185,12 +208,31 @@ RN_DEV i32x8 pk_cat8(const s16x8 a, const s16x8 b) {
     return (i32x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
 }
 
+// Returning +1 on a schedule counter by lane 0 only (a buffer atomic whose other lanes are out of
+// range: no exec-mask branch), invisible to the compiler's waitcnt insertion like the DMA: the
+// caller counts it in its vmcnt waits and reads the value only through pk_deq_take after the wait
+// that retires it.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+RN_DEV uint32_t pk_deq_issue(const int* ctr, int lane) {
+    const u32x4 rs = pk_rsrc_u(ctr, 4u);
+    uint32_t v = 1u;
+    const uint32_t off = lane == 0 ? 0u : 0xFFFFFFF0u;
+    asm volatile("buffer_atomic_add %0, %1, %2, 0 offen sc0 ; rn_deq_issue" : "+v"(v) : "v"(off), "s"(rs) : "memory");
+    return v;
+}
+RN_DEV int pk_deq_take(uint32_t v) {
+    asm volatile("; rn_deq_take %0" : "+v"(v));
+    return (int)__builtin_amdgcn_readfirstlane(v);
+}
+#pragma clang diagnostic pop
+
 template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     static_assert(!FP8 || (AK && BKC && !(DBG & 8)), "fp8: K-contiguous operands only");
     constexpr int BM = 256, BN = 256;
     constexpr int S_EPI = pk_epi_stores<ACT, SPLIT, F32>();
-    static_assert(6 + S_EPI <= 63, "vmcnt range");
+    static_assert(7 + S_EPI <= 63, "vmcnt range");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -200,9 +242,29 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     const int items = tiles * p.split;
     const int grid = gridDim.x;
     const int bid = xcd_remap(blockIdx.x, grid);
-    const int my_items = (items - bid + grid - 1) / grid;
     const int nk = p.k_per_split / BK;
-    const int nphase = my_items * nk * 4;
+
+    // ---- tile schedule (see the header): units of C items, static walk or dynamic queue ----
+    const bool dyn = p.sched != nullptr && DBG == 0;
+    const int C = dyn ? (nk >= 5 ? 1 : (4 + nk) / nk) : 1;
+    const int units = (items + C - 1) / C;
+    const int per = (grid & 7) == 0 ? grid >> 3 : 0;              // blocks per dispatch group
+    const int rounds_home = per ? max(0, units / grid - 1) : 0;
+    const int home_size = rounds_home * per;                       // units per group queue
+    const int tail_base = rounds_home * grid;
+    const int xq = blockIdx.x & 7;
+    int* const cnt = p.sched;
+    int* const ring = reinterpret_cast<int*>(smem + PK_RING);
+    // the unit a group queue's v-th dequeue stands for: the static walk's unit of that slot
+    auto home_unit = [&](int v) { return (v / per) * grid + xq * per + (v % per); };
+    auto unit_of = [&](int s) -> int {
+        if (!dyn) {
+            const int u = bid + s * grid;
+            return u < units ? u : -1;
+        }
+        return __builtin_amdgcn_readfirstlane(*(volatile int*)(ring + (s & 3)));
+    };
+    auto unit_items = [&](int u) { return min(C, items - u * C); };
 
     float alpha = 1.f;
     if (p.alpha) alpha = *p.alpha;
@@ -212,8 +274,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     // items) goes to slot σ % 8.  Phase q of compute K-tile u issues h = (q + 2) % 4 of K-tile
     // u + 1 (q0, q1) or u + 2 (q2, q3): the half index is a compile-time constant per phase and
     // the source comes from a cursor that advances once per K-tile. ----
-    auto item_coords = [&](int li, int& m0, int& n0, int& kb, int& ke, int& tm) {
-        const int item = bid + li * grid;
+    auto item_coords = [&](int item, int& m0, int& n0, int& kb, int& ke, int& tm) {
         const int sid = item / tiles;
         int tn;
         group_tile(item - sid * tiles, p.tiles_m, p.tiles_n, tm, tn);
@@ -250,7 +311,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     // lane then reads out of range and the DMA only zero-fills its slot)
     const bf16* ca = p.A;
     const bf16* cb = p.B;
-    int cml = 0, cnl = 0, ckl = 0, ckt = 0, cli = 0, ct = 0;
+    int cml = 0, cnl = 0, ckl = 0, ckt = 0, ct = 0;
+    int cs = 0, cu = -1, ci = 0, cnit = 0;  // cursor: unit sequence no., unit id, item in unit, items
     // bit H: half-tile H of the K-tile being issued is interior (no per-lane range checks);
     // recomputed once per K-tile instead of in every phase's DMA issue
     uint32_t intr = 0;
@@ -262,7 +324,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     bool in_loop = false;
     auto cur_set = [&]() {
         int m0, n0, kb, ke, tm;
-        item_coords(cli, m0, n0, kb, ke, tm);
+        item_coords(cu * C + ci, m0, n0, kb, ke, tm);
         ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + m0;
         cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + n0;
         cml = p.M - m0;
@@ -272,6 +334,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     };
     auto cur_adv = [&]() {
         ++ct;
+        if (cu < 0) return;  // exhausted: every later DMA only zero-fills its slot
         if (++ckt < nk) {
             ca += a_step;
             cb += b_step;
@@ -280,8 +343,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             return;
         }
         ckt = 0;
-        if (++cli < my_items) cur_set();
-        else {
+        if (++ci < cnit) {
+            cur_set();
+            return;
+        }
+        cu = unit_of(++cs);
+        if (cu >= 0) {
+            ci = 0;
+            cnit = unit_items(cu);
+            cur_set();
+        } else {
             cml = cnl = ckl = 0;
             intr = 0u;
         }
@@ -520,8 +591,45 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         }
     };
 
-    // ---- prologue: σ = 0..5 in flight (K-tile 0, halves 0/1 of K-tile 1), σ 0/1 landed ----
-    if (my_items > 0) {
+    // ---- dynamic schedule: wave 0's dequeue state machine (see the header) ----
+    int deq_state = 0;  // 0 idle, 1 issue at this phase's end, 2 in flight
+    int deq_age = 0, deq_slot = 0;
+    bool deq_home = false, home_ok = home_size > 0, deq_done = false;
+    uint32_t deq_v = 0u;
+    auto publish = [&](int u) {
+        if (lane == 0) *(volatile int*)(ring + (deq_slot & 3)) = u;
+        deq_state = 0;
+        deq_done = u < 0;
+    };
+
+    // ---- prologue: the first unit, then σ = 0..5 in flight (K-tile 0, halves 0/1 of K-tile 1) ----
+    if (dyn) {
+        if (wave == 0) {  // nothing is in flight yet: plain atomics, compiler-managed waits
+            int u = -1;
+            if (lane == 0) {
+                bool hk = home_size > 0;
+                if (hk) {
+                    const int v = __hip_atomic_fetch_add(cnt + xq * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    if ((unsigned)v < (unsigned)home_size) u = home_unit(v);
+                    else hk = false;
+                }
+                if (!hk) {
+                    const int v = __hip_atomic_fetch_add(cnt + 8 * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    u = (unsigned)v < (unsigned)(units - tail_base) ? tail_base + v : -1;
+                }
+                ring[0] = u;
+                ring[1] = hk ? 1 : 0;
+            }
+        }
+        __syncthreads();  // no DMA in flight yet: a plain barrier drains nothing
+        home_ok = ring[1] != 0;
+        deq_done = unit_of(0) < 0;
+    }
+    cu = unit_of(0);
+    if (cu >= 0) {
+        cnit = unit_items(cu);
         cur_set();
         issue_h(H0{});
         issue_h(H1{});
@@ -538,18 +646,47 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     __builtin_amdgcn_sched_barrier(0);
 
     int c_m0 = 0, c_n0 = 0, c_kb = 0, c_ke = 0, c_tm = 0, c_sid = 0;
-    if (my_items > 0) item_coords(0, c_m0, c_n0, c_kb, c_ke, c_tm);
-    c_sid = my_items > 0 ? (bid / tiles) : 0;
-    int c_li = 0, c_kt = 0;
+    int c_s = 0, c_u = unit_of(0), c_i = 0, c_nit = c_u >= 0 ? unit_items(c_u) : 0, c_kt = 0;
+    if (c_u >= 0) {
+        item_coords(c_u * C, c_m0, c_n0, c_kb, c_ke, c_tm);
+        c_sid = (c_u * C) / tiles;
+    }
     int since_epi = 4;
 
     // phase wait: σ ≤ φ+2 must have landed (this wave's DMA); younger = the 3 half-tiles
-    // issued in the previous 3 phases (6 ops) plus, within 4 phases of an epilogue, its stores
+    // issued in the previous 3 phases (6 ops) plus, within 4 phases of an epilogue, its stores,
+    // plus (wave 0) a schedule atomic issued within the last 4 phases
     auto phase_wait = [&]() {
         if constexpr (DBG & 2) return;
-        if (since_epi < 4) vm_wait<6 + S_EPI>();
-        else vm_wait<6>();
+        bool xtra = false;
+        if (dyn && wave == 0 && deq_state == 2) xtra = ++deq_age <= 4;
+        if (since_epi < 4) {
+            if (xtra) vm_wait<7 + S_EPI>();
+            else vm_wait<6 + S_EPI>();
+        } else {
+            if (xtra) vm_wait<7>();
+            else vm_wait<6>();
+        }
         ++since_epi;
+        if (dyn && wave == 0 && deq_state == 2 && deq_age >= 5) {  // retired by the wait above
+            const int v = pk_deq_take(deq_v);
+            // (unsigned compares: a corrupted counter can only end the block's work, never index past it)
+            if (!deq_home) publish((unsigned)v < (unsigned)(units - tail_base) ? tail_base + v : -1);
+            else if ((unsigned)v < (unsigned)home_size) publish(home_unit(v));
+            else {  // this group's queue is drained: the shared tail next
+                home_ok = false;
+                deq_state = 1;
+            }
+        }
+    };
+    // after a phase's DMA issue: wave 0 sends a pending dequeue
+    auto deq_issue = [&]() {
+        if (dyn && wave == 0 && deq_state == 1) {
+            deq_home = home_ok;
+            deq_v = pk_deq_issue(cnt + (home_ok ? xq : 8) * PK_CTR_STRIDE, lane);
+            deq_state = 2;
+            deq_age = 0;
+        }
     };
     auto sync_mma_begin = [&]() {
         __builtin_amdgcn_sched_barrier(0);
@@ -587,6 +724,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     phase_wait();                                                                                      \
     READS                                                                                              \
     if constexpr (!(DBG & 8)) { ISSUE }                                                                \
+    deq_issue();                                                                                       \
     sync_mma_begin();                                                                                  \
     if constexpr (DBG & 8) {                                                                           \
         RN_PK_MMA_S(MH, NH, BF, 0)                                                                     \
@@ -600,8 +738,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     sync_mma_end();
 
 #pragma unroll 1
-    for (int u = 0; u < my_items * nk; ++u) {
+    for (int u = 0; c_u >= 0; ++u) {
         const char* sl = smem + (u & 1) * (4 * PK_HALF);
+        // a unit's first K-tile: wave 0 asks for the unit after it (sent after q0's DMA)
+        if (dyn && wave == 0 && c_kt == 0 && c_i == 0 && !deq_done) {
+            deq_state = 1;
+            deq_slot = c_s + 1;
+        }
         // q0: At + Bl  (fragment reads first: their latency runs under the DMA issue)
         RN_PK_PHASE(
             _Pragma("unroll") for (int s = 0; s < 2; ++s) {
@@ -644,10 +787,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
             c_kt = 0;
-            ++c_li;
-            if (c_li < my_items) {
-                item_coords(c_li, c_m0, c_n0, c_kb, c_ke, c_tm);
-                c_sid = (bid + c_li * grid) / tiles;
+            if (++c_i == c_nit) {
+                c_u = unit_of(++c_s);
+                c_i = 0;
+                c_nit = c_u >= 0 ? unit_items(c_u) : 0;
+            }
+            if (c_u >= 0) {
+                item_coords(c_u * C + c_i, c_m0, c_n0, c_kb, c_ke, c_tm);
+                c_sid = (c_u * C + c_i) / tiles;
             }
         }
     }
@@ -655,12 +802,27 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #undef RN_PK_MMA_S
 #undef RN_PK_PHASE
     if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger barrier
-    (void)nphase;
+    if (dyn && wave == 0 && lane == 0) {  // the last block out resets the counters for the next launch
+        if (__hip_atomic_fetch_add(cnt + 9 * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1) {
+#pragma unroll
+            for (int i = 0; i < 10; ++i) __hip_atomic_store(cnt + i * PK_CTR_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     (void)c_kb;
     (void)c_ke;
 }
 
-// Launch: persistent grid of min(items, 256 × blocks-per-CU) workgroups (1 per CU: 128 KiB LDS).
+// Launch: persistent grid of min(units, CUs − reserve) workgroups (1 per CU: 128 KiB LDS).
+//   reserve (rn_gemm_set_reserve): CUs left free for a concurrently running collective, so RCCL's
+//   workgroups find a CU at once instead of waiting for a GEMM to drain (set while a data-parallel
+//   communicator is active); the dynamic schedule (rn_gemm_set_sched, default on) takes a counter
+//   slot from the device pool, or falls back to the static walk if the pool cannot be created
+//   (first use inside a stream capture).
+}  // namespace rn_gemm_detail
+extern "C" int* rn_gemm_sched_slot(int dev, hipStream_t st);
+extern "C" int rn_gemm_get_reserve();
+namespace rn_gemm_detail {
+
 template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false>
 void launch_pk_t(GemmArgs& a, hipStream_t st) {
     auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8>;
@@ -682,7 +844,13 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
         }
         cus = cu_n;
     }
-    const int grid = items < cus ? items : cus;
+    const int reserve = rn_gemm_get_reserve();
+    if (reserve > 0 && reserve < cus) cus -= reserve;
+    a.sched = DBG == 0 ? rn_gemm_sched_slot(dev, st) : nullptr;
+    const int nk = a.k_per_split / BK;
+    const int C = a.sched ? (nk >= 5 ? 1 : (4 + nk) / nk) : 1;
+    const int units = (items + C - 1) / C;
+    const int grid = units < cus ? units : cus;
     kern<<<grid, 512, PK_LDS, st>>>(a);
 }
 

@@ -39,11 +39,13 @@
 // Block→tile mapping is XCD-aware: the round-robin dispatcher puts blocks b
 // and b+8 on one XCD, so block ids are remapped (bijectively) to give each
 // XCD a contiguous run of tiles, walked in GROUP_M-row groups for L2 reuse.
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 
-#include "gemm_impl.h"
+#include "gemm_pk.h"
 
 using rn_gemm_detail::GemmArgs;
 using rn_gemm_detail::BK;
@@ -60,7 +62,9 @@ void rn_gemm_launch_pk_tt(GemmArgs&, int, hipStream_t);
 void rn_gemm_launch_pk_tf(GemmArgs&, int, hipStream_t);
 void rn_gemm_launch_pk_ff(GemmArgs&, int, hipStream_t);
 void rn_gemm_launch_pk_ft(GemmArgs&, int, hipStream_t);
+#ifdef REPLICANN_DEV
 int rn_gemm_launch_pk_dbg(GemmArgs&, bool, bool, int, hipStream_t);
+#endif
 
 namespace {
 
@@ -105,6 +109,60 @@ inline Choice pick(int M, int N, int K, int split_req) {
 
 extern "C" {
 
+// ---- persistent-GEMM schedule knobs (gemm_pk.h) ----
+// sched: 1 = dynamic tile queue (default), 0 = static walk.  reserve: CUs a cfg-9 launch leaves
+// free for a concurrent collective.  Host-side state read at launch (captured graphs keep the
+// values of their capture).
+static std::atomic<int> g_sched{-1};
+static std::atomic<int> g_reserve{0};
+void rn_gemm_set_sched(int m) { g_sched = m ? 1 : 0; }
+int rn_gemm_get_sched() {
+    int v = g_sched.load();
+    if (v < 0) {  // REPLICANN_GEMM_SCHED=static selects the static walk process-wide
+        const char* e = std::getenv("REPLICANN_GEMM_SCHED");
+        v = (e && e[0] == 's') ? 0 : 1;
+        g_sched = v;
+    }
+    return v;
+}
+void rn_gemm_set_reserve(int r) { g_reserve = r < 0 ? 0 : (r > 128 ? 128 : r & ~7); }
+int rn_gemm_get_reserve() { return g_reserve.load(); }
+
+// Counter slots of the dynamic schedule: a per-device pool of self-resetting counter blocks
+// (PK_SCHED_INTS ints each), handed out round robin.  Launches that share a slot are ordered on
+// one stream (the compute stream runs every GEMM), and a launch leaves its slot zeroed.
+constexpr int kSchedSlots = 256;
+static std::mutex g_pool_mu;
+static int* g_pool[64] = {};
+static std::atomic<unsigned> g_next_slot{0};
+int rn_gemm_sched_init(int dev) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (dev < 0 || dev >= 64) return -1;
+    if (g_pool[dev]) return 0;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    int* p = nullptr;
+    const size_t bytes = (size_t)kSchedSlots * rn_gemm_detail::PK_SCHED_INTS * sizeof(int);
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) e = hipMemset(p, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e != hipSuccess) return -1;
+    g_pool[dev] = p;
+    return 0;
+}
+int* rn_gemm_sched_slot(int dev, hipStream_t st) {
+    if (rn_gemm_get_sched() == 0 || dev < 0 || dev >= 64) return nullptr;
+    if (!g_pool[dev]) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(st, &cap);
+        if (cap != hipStreamCaptureStatusNone || rn_gemm_sched_init(dev) != 0) return nullptr;
+    }
+    const unsigned s = g_next_slot.fetch_add(1) % kSchedSlots;
+    return g_pool[dev] + (size_t)s * rn_gemm_detail::PK_SCHED_INTS;
+}
+
 // Workspace floats needed for a split-K launch.
 long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split * M * N : 0; }
 
@@ -145,11 +203,15 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     }
     if (cfg == 9 && !pk_ok(N, ldc, out_f32, act)) cfg = 1;  // shapes the persistent kernel does not take
     if (cfg >= 90 && cfg < 110) {  // timing-only ablation builds of cfg 9 (wrong outputs)
+#ifndef REPLICANN_DEV
+        return -1;  // not in a production library (REPLICANN_DEV=1 builds them)
+#else
         GemmArgs d = {};
         d.A = (const bf16*)A; d.B = (const bf16*)B; d.C = C; d.M = M; d.N = N; d.K = K;
         d.lda = lda; d.ldb = ldb; d.ldc = ldc; d.split = 1; d.k_per_split = (K + BK - 1) / BK * BK;
         d.tiles_m = (M + 255) / 256; d.tiles_n = (N + 255) / 256;
         return rn_gemm_launch_pk_dbg(d, !trans_a, trans_b, cfg - 90, st) == 0 ? 0 : -1;
+#endif
     }
     a.split = split < 1 ? 1 : split;
     int kps = (K + a.split - 1) / a.split;

@@ -42,6 +42,12 @@ HIP_FLAGS = [
 ]
 if os.environ.get("REPLICANN_CHECK", "0") == "1":  # debug build: device bounds checks (RN_CHECK)
     HIP_FLAGS.append("-DREPLICANN_CHECK=1")
+# developer build: also links the timing-only GEMM ablation kernels (gemm_pk_dbg.hip, cfg 90+:
+# WRONG outputs by design), which a default build neither compiles nor dispatches to
+DEV = os.environ.get("REPLICANN_DEV", "0") == "1"
+if DEV:
+    HIP_FLAGS.append("-DREPLICANN_DEV=1")
+DEV_ONLY = {"gemm_pk_dbg"}
 
 # Per-translation-unit extra flags.  The attention kernels run VALU-bound beside their MFMAs;
 # SLP vectorisation packs adjacent f32 adds/muls into v_pk_add/v_pk_mul_f32, which cost ~22-26
@@ -96,6 +102,27 @@ def _compile(src: Path, hdr: str, torch_inc) -> Path:
 
 
 IO_OUT = Path(__file__).resolve().parent / "_io.so"
+SRC_STAMP = OUT.with_suffix(".srcstamp")
+
+
+def _sources():
+    """Every source that goes into ``_C.so`` (the dev-only ablation kernels only in a dev build)."""
+    return [s for s in (sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "bindings").glob("*.cpp"))
+                        + sorted((CSRC / "comm").glob("*.cpp"))) if DEV or s.stem not in DEV_ONLY]
+
+
+def source_digest() -> str:
+    """Location-independent digest of what ``_C.so`` is built from: the relative path and bytes
+    of every compiled source and shared header, plus the build-mode flags.  Written next to the
+    library at link time; ``_ext.load()`` recomputes it and refuses a library built from other
+    sources (a stale ``_C.so`` pushed with a newer tree)."""
+    h = hashlib.sha1()
+    for p in sorted(_sources() + sorted((CSRC / "include").glob("*.h"))):
+        h.update(str(p.relative_to(ROOT)).encode())
+        h.update(b"\0")
+        h.update(p.read_bytes())
+    h.update(" ".join(f for f in HIP_FLAGS if f.startswith("-D")).encode())
+    return h.hexdigest()
 
 
 @contextlib.contextmanager
@@ -150,14 +177,16 @@ def _build_locked(verbose, jobs):
     torch_inc, torch_lib = _torch_paths()
     hdr = _headers_digest()
     # kernels (device code) + host-only bindings; csrc/comm is the native RCCL communicator
-    srcs = (sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "bindings").glob("*.cpp"))
-            + sorted((CSRC / "comm").glob("*.cpp")))
+    srcs = _sources()
     jobs = jobs or min(8, os.cpu_count() or 4)
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hdr, torch_inc), srcs))
     link_key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
     stamp = OUT.with_suffix(".stamp")
+    digest = source_digest()
     if OUT.exists() and stamp.exists() and stamp.read_text() == link_key:
+        if not SRC_STAMP.exists() or SRC_STAMP.read_text() != digest:
+            SRC_STAMP.write_text(digest)
         if verbose:
             print(f"[replicann build] up to date: {OUT}")
         return OUT
@@ -170,6 +199,7 @@ def _build_locked(verbose, jobs):
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
     os.replace(tmp, OUT)
     stamp.write_text(link_key)
+    SRC_STAMP.write_text(digest)
     if verbose:
         print(f"[replicann build] linked {OUT} from {len(objs)} objects")
     return OUT

@@ -15,8 +15,24 @@ from pathlib import Path
 
 import torch
 
-# REPLICANN_SO: load another build of the library (A/B timing of two kernel revisions only)
+# REPLICANN_SO: load another build of the library (A/B timing of two kernel revisions only; no
+# staleness check for an explicitly named library)
 _SO = Path(os.environ.get("REPLICANN_SO") or Path(__file__).resolve().parent / "_C.so")
+_EXPLICIT = bool(os.environ.get("REPLICANN_SO"))
+
+
+def check_fresh(so: Path = _SO) -> None:
+    """Raise unless ``so`` was built from the sources in this tree (``_build.source_digest``)."""
+    from . import _build
+
+    stamp = so.with_suffix(".srcstamp")
+    if not stamp.exists():
+        raise RuntimeError(f"{so} has no source stamp ({stamp.name}); rebuild with `python -m replicann_amd._build`")
+    want = _build.source_digest()
+    if stamp.read_text().strip() != want:
+        raise RuntimeError(f"{so} is stale: it was built from other csrc/ sources than this tree's "
+                           f"(stamp {stamp.read_text().strip()[:12]} != {want[:12]}); rebuild with "
+                           "`python -m replicann_amd._build`")
 _state = {"loaded": False, "error": None}
 _ref = {"on": False}  # process-wide: autograd runs backward on its own device threads
 
@@ -29,6 +45,8 @@ def load() -> bool:
     try:
         if not _SO.exists():
             raise FileNotFoundError(f"{_SO} not built (run `python -m replicann_amd._build`)")
+        if not _EXPLICIT:
+            check_fresh(_SO)
         torch.ops.load_library(str(_SO))
         _state["loaded"] = True
     except Exception as e:  # pragma: no cover - depends on build state

@@ -124,13 +124,69 @@ class _MultiheadAttention(nn.Module):
         return len(self._heads)
 
     # fused-parameter views --------------------------------------------------
-    def _cat_weights(self, names):
-        hs = self._heads
-        w = torch.cat([getattr(h, n).weight for n in names for h in hs], 0)
-        if getattr(hs[0], names[0]).bias is not None:
-            b = torch.cat([getattr(h, n).bias for n in names for h in hs], 0)
-        else:
-            b = None
+    _FUSED = ("_query",)  # per-head Linears fused into one projection (self-attention: q, k, v)
+
+    def _members(self, kind):
+        return [getattr(getattr(h, n), kind) for n in self._FUSED for h in self._heads]
+
+    def _rn_fuse_groups(self):
+        """FlatParams packs the per-head weights (and biases) back to back in fused order, so the
+        fused projection is a zero-copy view of the flat buffers (utils/flat.py)."""
+        groups = [self._members("weight")]
+        if self._heads[0]._query.bias is not None:
+            groups.append(self._members("bias"))
+        return groups
+
+    def _fused_param(self, kind):
+        """A leaf Parameter aliasing the packed flat-buffer region of the fused weight / bias
+        (its .grad aliases the flat gradient region), or None when the parameters do not live
+        in a FlatParams buffer.  Backward kernels accumulate straight into that region and
+        notify every member (ops.linear._notify); the optimizer sees only the members."""
+        members = self._members(kind)
+        if members[0] is None:
+            return None
+        flat = getattr(members[0], "_rn_flat", None)
+        if flat is None:
+            return None
+        cache = self.__dict__.setdefault("_rn_fused", {})
+        hit = cache.get(kind)
+        if hit is not None and hit[0] is flat and hit[1] == members[0].data_ptr():
+            return hit[2]
+        shape = (sum(p.shape[0] for p in members),) + tuple(members[0].shape[1:])
+        views = flat.fused_view(members, shape)
+        if views is None:
+            return None
+        proxy = nn.Parameter(views[0], requires_grad=True)
+        proxy.grad = views[1]
+        proxy._rn_flat = flat
+        proxy._rn_members = members
+
+        def _ready(p, flat=flat, members=members):  # autograd-accumulated (non-direct) path
+            for m in members:
+                flat.mark_ready(m)
+        proxy.register_post_accumulate_grad_hook(_ready)
+        cache[kind] = (flat, members[0].data_ptr(), proxy)
+        return proxy
+
+    def _cat_weights(self, names=None):
+        """(weight, bias) of the fused projection: flat-buffer views when the parameters are
+        packed (training runs), else a concatenation — cached by the members' versions when no
+        gradient is recorded (eval / inference), so repeated forwards do not re-concatenate."""
+        w = self._fused_param("weight")
+        if w is not None:
+            b = self._fused_param("bias") if self._heads[0]._query.bias is not None else None
+            return w, b
+        ws, bs = self._members("weight"), self._members("bias")
+        key = None
+        if not torch.is_grad_enabled():
+            key = tuple((p.data_ptr(), p._version) for p in ws + [q for q in bs if q is not None])
+            hit = self.__dict__.get("_rn_cat_cache")
+            if hit is not None and hit[0] == key:
+                return hit[1], hit[2]
+        w = torch.cat(ws, 0)
+        b = torch.cat(bs, 0) if bs[0] is not None else None
+        if key is not None:
+            self.__dict__["_rn_cat_cache"] = (key, w, b)
         return w, b
 
     def _out(self, z: Tensor) -> Tensor:
@@ -187,7 +243,7 @@ class MultiheadCrossAttention(_MultiheadAttention):
                 return_kv: bool = False):
         H = self.n_heads
         split = self.embedding_size // H
-        wq, bq = self._cat_weights(["_query"])
+        wq, bq = self._cat_weights()
         q = ops.linear(x, wq, bq)
         kk = k[..., : H * split]
         vv = v[..., : H * split]
@@ -213,9 +269,10 @@ class MultiheadSelfAttention(_MultiheadAttention):
     """Multi-head self attention (reference ``:175-192``), fused QKV + fused attention."""
 
     AttentionHead = SelfAttentionHead
+    _FUSED = ("_query", "_key", "_value")
 
     def fused_qkv(self, x: Tensor) -> Tensor:
-        w, b = self._cat_weights(["_query", "_key", "_value"])
+        w, b = self._cat_weights()
         return ops.linear(x, w, b)
 
     def forward(self, x: Tensor, /, mask: Tensor | None = None, *, return_kv: bool = False):

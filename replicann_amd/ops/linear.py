@@ -126,7 +126,13 @@ def _direct_grad(p):
 
 def _notify(p):
     """Tell the flat buffer (and thus DDP's bucketing) that ``p``'s gradient is
-    final — for a multi-use parameter, after its last contribution."""
+    final — for a multi-use parameter, after its last contribution.  A fused-view parameter
+    (nn/attention.py ``_fused_param``) stands for its members: each of them is final."""
+    members = getattr(p, "_rn_members", None)
+    if members is not None:
+        for m in members:
+            p._rn_flat.mark_ready(m)
+        return
     uses = getattr(p, "_rn_direct_uses", 1)
     if uses > 1:
         left = getattr(p, "_rn_pending", uses) - 1

@@ -12,8 +12,11 @@ caller's stream, ``synchronize`` blocks the host):
 * :class:`TorchComm` — ``torch.distributed`` async collectives (``nccl`` = RCCL on a
   GPU, ``gloo`` on the CPU).  The CPU tests and gloo rehearsals run this one.
 
-``make_comm("auto")`` picks native for GPU tensors on an ``nccl`` process group and
-torch otherwise.  The reference has no collective code (``/root/reference/poetry.lock:1222``
+``make_comm("auto")`` picks native for a ONE-rank ``nccl`` group (the one-GPU rehearsal,
+where it is hardware-tested and hipGraph-capturable) and torch otherwise: at world > 1 the
+native communicator has not yet been run on a multi-GPU node, so ProcessGroupNCCL (also RCCL,
+on its own internal stream) stays the default there until a multi-GPU parity run of the native
+path exists; ``REPLICANN_COMM=native`` (or ``comm="native"``) opts in.  The reference has no collective code (``/root/reference/poetry.lock:1222``
 is its only NCCL touchpoint).
 """
 
@@ -72,7 +75,7 @@ class NativeComm:
 
     name = "native"
 
-    def __init__(self, group=None, device=None, timeout_s: float = 600.0):
+    def __init__(self, group=None, device=None, timeout_s: float = 600.0, proxy: bool = False):
         from .. import _ext
 
         self.ops = _ext.ops()
@@ -82,6 +85,22 @@ class NativeComm:
         else:
             self.rank, self.world = 0, 1
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.proxy = proxy
+        if proxy:
+            # one-GPU stand-in for an N-GPU RCCL collective's footprint (csrc/kernels/comm_proxy.hip):
+            # REPLICANN_PROXY_WORLD emulated ranks, REPLICANN_PROXY_WGS workgroups, REPLICANN_PROXY_GBPS
+            # per-GPU bus bandwidth of the emulated xGMI ring
+            assert self.world == 1, "the comm proxy stands in for collectives on a one-rank group"
+            self.name = "proxy"
+            self.proxy_world = int(os.environ.get("REPLICANN_PROXY_WORLD", 8))
+            self.proxy_wgs = int(os.environ.get("REPLICANN_PROXY_WGS", 32))
+            self.proxy_gbps = float(os.environ.get("REPLICANN_PROXY_GBPS", 300.0))
+            self.handle = int(self.ops.comm_init_proxy(self.device.index, self.proxy_world, self.proxy_wgs,
+                                                       self.proxy_gbps, float(timeout_s)))
+            import atexit
+
+            atexit.register(self._quiesce)
+            return
         uid = self.ops.comm_unique_id() if self.rank == 0 else None
         if self.world > 1:  # rank 0's id over the existing rendezvous (a CPU object broadcast)
             box = [bytes(uid.numpy()) if uid is not None else None]
@@ -139,7 +158,8 @@ def make_comm(kind: str = "auto", group=None, device=None, timeout_s: float = 60
     timeout_s = float(os.environ.get("REPLICANN_COMM_TIMEOUT", timeout_s))
     dev = torch.device(device) if device is not None else None
     if kind == "auto":
-        if _is_nccl(group) and (dev is None or dev.type == "cuda"):
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if _is_nccl(group) and world == 1 and (dev is None or dev.type == "cuda"):
             try:
                 return NativeComm(group, dev, timeout_s)
             except Exception as e:  # e.g. extension built without RCCL: same collectives via torch
@@ -150,6 +170,8 @@ def make_comm(kind: str = "auto", group=None, device=None, timeout_s: float = 60
         kind = "torch"
     if kind == "native":
         return NativeComm(group, dev, timeout_s)
+    if kind == "proxy":
+        return NativeComm(group, dev, timeout_s, proxy=True)
     if kind == "torch":
         return TorchComm(group)
-    raise ValueError(f"unknown comm kind {kind!r} (auto | native | torch)")
+    raise ValueError(f"unknown comm kind {kind!r} (auto | native | torch | proxy)")

@@ -71,6 +71,7 @@ class DistributedDataParallel(nn.Module):
         self.check_unused = check_unused
         self._sync = True
         self.comm = make_comm(comm, process_group, flat.grad.device) if isinstance(comm, str) else comm
+        self._reserve_cus()
         if broadcast and self.world > 1:
             self._broadcast_state()
         self.reduce_dtype = reduce_dtype
@@ -98,10 +99,10 @@ class DistributedDataParallel(nn.Module):
         for p, off, n in reversed(segs):
             if id(p) in self.split:
                 continue
-            end = off + ((n + 63) // 64) * 64
+            end = flat.span(p)[1]
             if cur_hi is None:
                 cur_hi, cur_lo, cur_n = end, off, 0
-            elif (cur_hi - off > cap or cur_lo != off + ((n + 63) // 64) * 64) and cur_n > 0:
+            elif (cur_hi - off > cap or cur_lo != end) and cur_n > 0:
                 # a split parameter between two neighbours breaks contiguity: close the bucket
                 self.buckets.append([cur_lo, cur_hi, cur_n])
                 cur_hi, cur_lo, cur_n = end, off, 0
@@ -116,6 +117,22 @@ class DistributedDataParallel(nn.Module):
         flat.ready_hooks.append(self._hook)  # parameters whose grads are accumulated directly by kernels
         flat.contribution_hooks.append(self._contribution)
         self.comm_wait_ms = 0.0  # host time spent in finish() (last step): the exposed all-reduce tail
+
+    def _reserve_cus(self):
+        """While collectives can run beside the backward (world > 1, or the one-GPU comm proxy),
+        the persistent GEMM leaves ``REPLICANN_GEMM_RESERVE`` CUs (default 8: one per dispatch
+        group) free, so a bucket's RCCL workgroups start when the bucket is ready instead of when
+        the running GEMM drains; the GEMM's dynamic tile queue absorbs whatever CUs they hold."""
+        import os
+
+        dev = self.flat.grad.device
+        if dev.type != "cuda" or not (self.world > 1 or getattr(self.comm, "proxy", False)):
+            return
+        from .. import _ext
+
+        r = int(os.environ.get("REPLICANN_GEMM_RESERVE", 8))
+        _ext.ops().gemm_set_reserve(r)
+        self.gemm_reserve = _ext.ops().gemm_get_reserve()
 
     # ------------------------------------------------------------------
     def _broadcast_state(self):

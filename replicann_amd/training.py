@@ -130,6 +130,9 @@ class Trainer:
         if self.ddp is not None:
             self.opt.grad_source = self.ddp.grad_source  # fp32 all-reduced gradients
         self.fp8_cache = None
+        if self.device.type == "cuda":  # the committed per-shape GEMM configs of this model (tuning/)
+            from .tuning import load_committed
+            self.gemm_table_entries = load_committed(cfg.model)
         if self.device.type == "cuda":  # fp8 layers read e4m3 weights the optimizer step writes
             from .ops.fp8 import attach_weight_cache
             self.fp8_cache = attach_weight_cache(self.model, self.flat, self.opt)
@@ -265,7 +268,7 @@ class Trainer:
         # models capture too; multi-rank steps run eager: N=1 eager vs graph measured within 0.3 %,
         # profiles/graph_vs_eager_r2.txt).  A one-rank DDP rehearsal captures only with the
         # native communicator (its fork/join is capturable; torch's async works are not).
-        return self.world == 1 and (self.ddp is None or self.ddp.comm.name == "native")
+        return self.world == 1 and (self.ddp is None or self.ddp.comm.name in ("native", "proxy"))
 
     def _capture(self):
         """Capture zero_grad → fwd → bwd → (all-reduce) → optimizer as ONE hipGraph.
@@ -377,29 +380,39 @@ def train(config: TrainConfig | None = None, model=None, **kw):
 def evaluate(model, data, steps=10):
     """Mean loss (and accuracy for classifiers) over ``steps`` batches per rank; under
     data parallelism the sums are all-reduced, so every rank returns the mean over ALL
-    ranks' batches (each rank reads its own round-robin share of the eval stream)."""
+    ranks' batches (each rank reads its own round-robin share of the eval stream).
+
+    Language models are scored through their own loss path (``model(x, targets)``: on a GPU the
+    fused LM-head + cross-entropy kernels, bf16 logits consumed in place — no fp32 copy of the
+    logits); classifiers through the native cross-entropy kernel."""
+    from . import ops
+
     was = model.training
     model.eval()
     dev = next(model.parameters()).device
     sums = torch.zeros(3, dtype=torch.float64, device=dev)  # Σ loss·n, Σ correct, Σ n
+    lm = _is_lm(model)
     for _ in range(steps):
         x, y = next(data)
-        out = model(x)
-        if out.dim() == 3:  # LM logits
-            lf = out.float().reshape(-1, out.shape[-1])
-            yy = y.reshape(-1)
-            sums[0] += torch.nn.functional.cross_entropy(lf, yy, reduction="sum").double()
-            sums[2] += yy.numel()
-        else:
-            sums[0] += torch.nn.functional.cross_entropy(out.float(), y, reduction="sum").double()
-            sums[1] += (out.argmax(-1) == y).sum().double()
+        if lm:  # mean token loss of the batch, from the model's own fused loss path
+            sums[0] += model(x, y).double() * y.numel()
             sums[2] += y.numel()
+            continue
+        out = model(x)
+        sums[0] += ops.cross_entropy(out, y).double() * y.numel()
+        sums[1] += (out.argmax(-1) == y).sum().double()
+        sums[2] += y.numel()
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(sums)
     model.train(was)
     tot, cor, n = (float(v) for v in sums.cpu())
     return {"loss": tot / max(n, 1), "accuracy": cor / max(n, 1)}
+
+
+def _is_lm(model) -> bool:
+    """Token models (GPT-2, the reference-block LM): a vocabulary config and a targets-taking forward."""
+    return hasattr(getattr(model, "config", None), "vocab_size") or hasattr(model, "vocab_size")
 
 
 def eval_main(argv=None):

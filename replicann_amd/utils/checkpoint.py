@@ -55,6 +55,7 @@ def save_checkpoint(path, model, optimizer=None, step=0, config=None, extra=None
             "config": dict(config or {}),
             "rng_cpu": mine["rng_cpu"],
             "ranks": ranks,
+            "world_size": len(ranks),
         }
         if optimizer is not None:
             sd["optim"] = {k: (v.detach().cpu() if torch.is_tensor(v) else v)
@@ -68,14 +69,30 @@ def save_checkpoint(path, model, optimizer=None, step=0, config=None, extra=None
         dist.barrier()
 
 
-def load_checkpoint(path, model, optimizer=None, strict=True, map_location="cpu", restore_rng=True):
-    """Returns (step, config, this rank's resume state or None)."""
+def load_checkpoint(path, model, optimizer=None, strict=True, map_location="cpu", restore_rng=True,
+                    allow_world_change=False):
+    """Returns (step, config, this rank's resume state or None).
+
+    The per-rank resume states (RNGs, data cursor) are only meaningful for the world size that
+    saved them: resuming with another world size raises, unless ``allow_world_change`` — then
+    the model / optimizer state is restored, a warning is issued, and every rank starts fresh
+    per-rank streams (returned state None: the caller reseeds them deterministically by rank)."""
     sd = torch.load(path, map_location=map_location, weights_only=True)
     model.load_state_dict(sd["model"], strict=strict)
     if optimizer is not None and "optim" in sd:
         optimizer.load_state_dict(sd["optim"])
     r = dist.get_rank() if _dist() else 0
+    world = dist.get_world_size() if _dist() else 1
     ranks = sd.get("ranks") or []
+    saved_world = int(sd.get("world_size", len(ranks) or 1))
+    if ranks and saved_world != world:
+        msg = (f"checkpoint {path} was saved by {saved_world} rank(s) but is resumed by {world}: the per-rank "
+               "RNG states and data cursors do not map onto this world size")
+        if not allow_world_change:
+            raise RuntimeError(msg + " (pass allow_world_change=True to restore only model/optimizer state)")
+        import warnings
+        warnings.warn(msg + "; restoring model/optimizer state only, per-rank streams start fresh")
+        return sd.get("step", 0), sd.get("config", {}), None
     mine = ranks[r] if r < len(ranks) else None
     if restore_rng:
         cpu = mine["rng_cpu"] if mine is not None else sd.get("rng_cpu")

@@ -13,6 +13,13 @@ Consequences that the rest of the framework is built on:
 
 Parameters are laid out in registration order; backward produces gradients
 roughly in reverse of that, which is what the DDP bucketing exploits.
+
+Fusion groups: a module may declare ``_rn_fuse_groups()`` → lists of parameters that
+one kernel consumes as ONE tensor (the reference blocks' per-head Q/K/V ``nn.Linear``
+weights, reference ``nn/attention.py:131-137``, are a fused QKV projection here).  A
+group is packed back to back, in the listed order, at the position of its first
+member, so the fused weight (and its gradient) is a zero-copy view of the flat buffers
+(:meth:`fused_view`) — no ``torch.cat`` per forward, no split of the gradient.
 """
 
 from __future__ import annotations
@@ -35,11 +42,37 @@ class FlatParams:
         dtype = dtype or self.params[0].dtype
         device = torch.device(device) if device is not None else self.params[0].device
         grad_dtype = grad_dtype or dtype
-        self.offsets = []
-        off = 0
+        trainable = {id(p) for p in self.params}
+        group_of = {}
+        for m in module.modules():
+            fg = getattr(m, "_rn_fuse_groups", None)
+            if not callable(fg):
+                continue
+            for g in fg():
+                g = list(g)
+                if (len(g) > 1 and all(id(p) in trainable and id(p) not in group_of for p in g)
+                        and len({id(p) for p in g}) == len(g) and len({p.dtype for p in g}) == 1):
+                    for p in g:
+                        group_of[id(p)] = g
+        order, seen = [], set()
         for p in self.params:
+            if id(p) in seen:
+                continue
+            for q in group_of.get(id(p), [p]):
+                order.append(q)
+                seen.add(id(q))
+        self.params = order
+        self.offsets = []
+        self.ends = []  # allocation end of each parameter (packed group members: the next member's start)
+        off = 0
+        for i, p in enumerate(self.params):
             self.offsets.append(off)
-            off += _round(p.numel())
+            g = group_of.get(id(p))
+            packed_next = g is not None and p is not g[-1]
+            off = off + p.numel() if packed_next else _round(off + p.numel())
+            self.ends.append(off)
+        self._group_of = group_of
+        self._index = {id(p): i for i, p in enumerate(self.params)}
         self.numel = off
         self.data = torch.zeros(off, dtype=dtype, device=device)
         self.grad = torch.zeros(off, dtype=grad_dtype, device=device)
@@ -63,9 +96,9 @@ class FlatParams:
             p._rn_flat = self
         # per-64-element-granule weight-decay flag (matrices decay; vectors don't)
         wd = torch.zeros(off // ALIGN, dtype=torch.uint8)
-        for p, o in zip(self.params, self.offsets):
-            if p.dim() >= 2:
-                wd[o // ALIGN:(o + _round(p.numel())) // ALIGN] = 1
+        for p, o, e in zip(self.params, self.offsets, self.ends):
+            if p.dim() >= 2:  # (a packed group is all matrices or all vectors)
+                wd[o // ALIGN:_round(e) // ALIGN] = 1
         self.wd_mask = wd.to(device)
 
     def zero_grad(self):
@@ -89,3 +122,18 @@ class FlatParams:
     def segments(self):
         """[(param, offset, numel)] in layout order."""
         return [(p, o, p.numel()) for p, o in zip(self.params, self.offsets)]
+
+    def span(self, p):
+        """(offset, allocation end) of parameter ``p`` in the flat buffers."""
+        i = self._index[id(p)]
+        return self.offsets[i], self.ends[i]
+
+    def fused_view(self, members, shape):
+        """(data view, grad view) of a packed fusion group, in ``shape``, or None when ``members``
+        is not one of this buffer's groups (packed back to back in exactly this order)."""
+        g = self._group_of.get(id(members[0]))
+        if g is None or len(g) != len(members) or any(a is not b for a, b in zip(g, members)):
+            return None
+        lo = self.offsets[self._index[id(g[0])]]
+        n = sum(p.numel() for p in g)
+        return self.data[lo:lo + n].view(shape), self.grad[lo:lo + n].view(shape)

@@ -159,3 +159,41 @@ def test_ddp_pre_step_tuning_pass_is_invisible(one_rank_pg):
     a_l, a_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"))
     b_l, b_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"), skip_tune=True)
     assert a_l == b_l and torch.equal(a_w, b_w)
+
+
+def test_proxy_comm_keeps_data_and_orders_streams():
+    """REPLICANN_COMM=proxy: the collectives move the emulated ring volume through HBM on the comm
+    stream (values unchanged at world 1), stream-ordered like the real ones, and capturable."""
+    from replicann_amd.parallel.comm import NativeComm
+
+    c = NativeComm(device="cuda:0", proxy=True)
+    try:
+        assert c.name == "proxy" and c.proxy_world >= 2
+        a = torch.randn(4 << 20, device="cuda")
+        for _ in range(3):
+            y = a * 2.0
+            c.all_reduce(y)
+            c.wait()
+            z = y + 1.0
+        b = torch.randn(4096, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty_like(b)
+        c.all_gather(b, out)
+        c.broadcast(b, 0)
+        c.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(z, a * 2.0 + 1.0) and torch.equal(out, b)
+        assert c.info()["collectives"] == 5
+    finally:
+        c.close()
+
+
+def test_ddp_step_proxy_matches_native_and_reserves_cus(one_rank_pg):
+    nat_l, nat_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"))
+    assert torch.ops.replicann.gemm_get_reserve() == 0  # a one-rank real group runs no collective beside GEMMs
+    px_l, px_w, px_g, px_c, _ = _run(dict(graph="auto", ddp="on", comm="proxy"))
+    try:
+        assert px_c == "proxy" and px_g  # capturable like the native communicator
+        assert torch.ops.replicann.gemm_get_reserve() == 8
+        assert px_l == nat_l and torch.equal(px_w, nat_w)
+    finally:
+        torch.ops.replicann.gemm_set_reserve(0)

@@ -88,3 +88,24 @@ def test_eval_starts_at_window_zero_after_checkpoint(tmp_path):
     # and the TRAIN resume continues the saved cursor (any grad_accum)
     tr2 = Trainer(TrainConfig(steps=3, resume=ck, grad_accum=2, **base))
     assert tr2.data.batch_index == tr.data.batch_index
+
+
+def test_resume_with_other_world_size_is_refused(tmp_path):
+    import pytest
+    import torch
+
+    from replicann_amd.models import MLP
+    from replicann_amd.utils.checkpoint import load_checkpoint, rank_state, save_checkpoint
+
+    m = MLP()
+    ck = str(tmp_path / "w2.pt")
+    save_checkpoint(ck, m, step=3)
+    sd = torch.load(ck, weights_only=True)
+    sd["ranks"] = [rank_state(), rank_state()]  # as if two ranks had saved it
+    sd["world_size"] = 2
+    torch.save(sd, ck)
+    with pytest.raises(RuntimeError, match="saved by 2 rank"):
+        load_checkpoint(ck, MLP())
+    with pytest.warns(UserWarning, match="per-rank streams start fresh"):
+        step, _, mine = load_checkpoint(ck, MLP(), allow_world_change=True)
+    assert step == 3 and mine is None
