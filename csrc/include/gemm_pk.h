@@ -40,17 +40,23 @@
 // static list (bid + s·grid) but DEQUEUES its work, so a workgroup that starts late — because an
 // RCCL kernel on the comm stream held its CU when the GEMM launched — simply takes fewer tiles
 // instead of delaying the whole GEMM by the collective's duration.
-//   * work unit = C consecutive items (tile × split-K slice), C·nk ≥ 5 K-tiles, so one dequeue
-//     has ≥ 20 phases to come back before the DMA cursor needs the next unit;
+//   * the unit of work is one item (tile × split-K slice) of ≥ 5 K-tiles (shorter items — K per
+//     slice < 320 — keep the static walk), so one dequeue (+ one retry) has 3.5 K-tiles to come
+//     back before the DMA cursor needs the next item, and the cursor is never more than one item
+//     ahead of the compute side;
 //   * one queue per dispatch group (blockIdx & 7: the blocks that share an XCD and its L2) over
 //     exactly the units the static walk would give that group in all but its last round, plus
 //     one shared tail queue over the rest: the same L2 locality as the static walk, balanced at
 //     the end;
-//   * wave 0 lane 0 issues the returning atomic (a range-checked buffer atomic: the other lanes'
-//     offsets are out of range, so exec stays full) right after a phase's DMA issue; it is
-//     COUNTED like a DMA: wave 0's waits allow one more outstanding op for the next 4 phases and
-//     the 5th retires it (vmcnt is in order), then the unit id goes to a 4-slot LDS ring past the
-//     operand ring, read by every wave ≥ 1 phase later (the DMA placement rule);
+//   * wave 0 issues ONE returning buffer atomic per K-tile, at q0 right after q0's wait and BEFORE
+//     q0's DMA: lane 0 is in range only when a dequeue is wanted (at an item's first K-tile, or to
+//     retry on the shared tail), otherwise every lane is out of range and the atomic is a no-op.
+//     It is older than q0's DMA, so the next K-tile's q0 wait retires it (vmcnt is in order) and
+//     in between (q1-q3) wave 0's waits allow exactly one more op than the other waves'.  The
+//     value is consumed at the next q0, right before the next atomic redefines the register: it
+//     is never live across a second definition, so the register allocator has no reason to copy
+//     a register the hardware has not written yet.  The unit id goes to a 4-slot LDS ring past
+//     the operand ring, read by every wave ≥ 1 phase later (the DMA placement rule);
 //   * the counters (home 0-7, tail, exit; one 128-B line each) reset themselves: the last block
 //     to finish zeroes them, so a slot is reusable by the next launch on the stream and graph
 //     replays need no memset node.
@@ -194,8 +200,9 @@ constexpr int pk_epi_stores() {
 // DBG (timing-only ablation builds: gemm_pk_dbg.hip, cfg 90 + DBG; outputs are wrong): bit 0
 // skips the main-loop operand DMA, bit 1 the counted vmcnt waits, bit 2 the epilogue body, bit 3
 // issues the DMA between the two k-steps' MFMAs, bit 4 issues every main-loop DMA instruction with
-// an out-of-range offset (same instructions, no memory traffic, no LDS writes), bit 5 issues each
-// half-tile's DMA with the SAME descriptor every phase (no per-phase descriptor rebuild).
+// an out-of-range offset (same instructions, no memory traffic, no LDS writes), bit 5 (32) issues
+// the bf16 epilogue's stores with an out-of-range offset (same instructions, no traffic), bit 6
+// (64) drops them (the values stay live; the counted waits drop their allowance too).
 // FP8: e4m3 operands, both K-contiguous (the forward x·Wᵀ), staged as "bf16 pairs" (K, lda, ldb
 // in 2-byte units, so the DMA stream, the LDS images and the fragment reads are byte-identical to
 // the bf16 kernel's); each phase's two k-step fragments of a row (16 B each) are concatenated into
@@ -214,12 +221,16 @@ RN_DEV i32x8 pk_cat8(const s16x8 a, const s16x8 b) {
 // that retires it.
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-RN_DEV uint32_t pk_deq_issue(const int* ctr, int lane) {
-    const u32x4 rs = pk_rsrc_u(ctr, 4u);
-    uint32_t v = 1u;
-    const uint32_t off = lane == 0 ? 0u : 0xFFFFFFF0u;
+RN_DEV void pk_deq_issue(uint32_t& v, const int* ctr, bool live) {
+    const u32x4 rs = pk_rsrc_u(ctr, ctr ? 4u : 0u);
+    const uint32_t off = live ? 0u : 0xFFFFFFF0u;
+    v = 1u;
     asm volatile("buffer_atomic_add %0, %1, %2, 0 offen sc0 ; rn_deq_issue" : "+v"(v) : "v"(off), "s"(rs) : "memory");
-    return v;
+}
+// the static-walk form without a return (no register written asynchronously; still counted)
+RN_DEV void pk_deq_noop() {
+    const u32x4 rs = pk_rsrc_u(nullptr, 0u);
+    asm volatile("buffer_atomic_add %0, %1, %2, 0 offen ; rn_deq_noop" ::"v"(1u), "v"(0xFFFFFFF0u), "s"(rs) : "memory");
 }
 RN_DEV int pk_deq_take(uint32_t v) {
     asm volatile("; rn_deq_take %0" : "+v"(v));
@@ -231,7 +242,7 @@ template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     static_assert(!FP8 || (AK && BKC && !(DBG & 8)), "fp8: K-contiguous operands only");
     constexpr int BM = 256, BN = 256;
-    constexpr int S_EPI = pk_epi_stores<ACT, SPLIT, F32>();
+    constexpr int S_EPI = (DBG & 64) ? 0 : pk_epi_stores<ACT, SPLIT, F32>();
     static_assert(7 + S_EPI <= 63, "vmcnt range");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
@@ -244,27 +255,31 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     const int bid = xcd_remap(blockIdx.x, grid);
     const int nk = p.k_per_split / BK;
 
-    // ---- tile schedule (see the header): units of C items, static walk or dynamic queue ----
-    const bool dyn = p.sched != nullptr && DBG == 0;
-    const int C = dyn ? (nk >= 5 ? 1 : (4 + nk) / nk) : 1;
-    const int units = (items + C - 1) / C;
-    const int per = (grid & 7) == 0 ? grid >> 3 : 0;              // blocks per dispatch group
-    const int rounds_home = per ? max(0, units / grid - 1) : 0;
-    const int home_size = rounds_home * per;                       // units per group queue
-    const int tail_base = rounds_home * grid;
-    const int xq = blockIdx.x & 7;
-    int* const cnt = p.sched;
+    // ---- tile schedule (see the header): static walk or dynamic queue over the items ----
+    // (not for fp8: its register pressure makes hipcc reuse the schedule op's register as a
+    // temporary between issue and retire — tests/test_gemm_isa.py checks every instantiation)
+    const bool dyn = p.sched != nullptr && DBG == 0 && !FP8 && nk >= 5;
     int* const ring = reinterpret_cast<int*>(smem + PK_RING);
-    // the unit a group queue's v-th dequeue stands for: the static walk's unit of that slot
-    auto home_unit = [&](int v) { return (v / per) * grid + xq * per + (v % per); };
     auto unit_of = [&](int s) -> int {
         if (!dyn) {
             const int u = bid + s * grid;
-            return u < units ? u : -1;
+            return u < items ? u : -1;
         }
         return __builtin_amdgcn_readfirstlane(*(volatile int*)(ring + (s & 3)));
     };
-    auto unit_items = [&](int u) { return min(C, items - u * C); };
+    // the item of the v-th dequeue from queue q (0-7: dispatch group q's share of the static walk's
+    // first rounds, grid a multiple of 8 with a power-of-two share; 8: the shared tail), -2 = group
+    // queue drained, -1 = no work left
+    auto deq_map = [&](int q, int v) -> int {
+        const int per = grid >> 3;
+        const bool home = (grid & 7) == 0 && (per & (per - 1)) == 0;
+        const int rh = home ? max(0, items / grid - 1) : 0;
+        if (q < 8) {
+            const int sh = 31 - __builtin_clz(per | 1);
+            return (unsigned)v < (unsigned)(rh * per) ? (v >> sh) * grid + q * per + (v & (per - 1)) : -2;
+        }
+        return (unsigned)v < (unsigned)(items - rh * grid) ? rh * grid + v : -1;
+    };
 
     float alpha = 1.f;
     if (p.alpha) alpha = *p.alpha;
@@ -312,7 +327,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     const bf16* ca = p.A;
     const bf16* cb = p.B;
     int cml = 0, cnl = 0, ckl = 0, ckt = 0, ct = 0;
-    int cs = 0, cu = -1, ci = 0, cnit = 0;  // cursor: unit sequence no., unit id, item in unit, items
+    int cu = -1, cs = 0;  // cursor: the item being issued, its sequence number (ring slot)
     // bit H: half-tile H of the K-tile being issued is interior (no per-lane range checks);
     // recomputed once per K-tile instead of in every phase's DMA issue
     uint32_t intr = 0;
@@ -324,7 +339,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     bool in_loop = false;
     auto cur_set = [&]() {
         int m0, n0, kb, ke, tm;
-        item_coords(cu * C + ci, m0, n0, kb, ke, tm);
+        item_coords(cu, m0, n0, kb, ke, tm);
         ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + m0;
         cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + n0;
         cml = p.M - m0;
@@ -343,14 +358,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             return;
         }
         ckt = 0;
-        if (++ci < cnit) {
-            cur_set();
-            return;
-        }
         cu = unit_of(++cs);
         if (cu >= 0) {
-            ci = 0;
-            cnit = unit_items(cu);
             cur_set();
         } else {
             cml = cnl = ckl = 0;
@@ -557,7 +566,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                         }
                         const u32x4 ou = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
                                           pk_pack2(v[6], v[7])};
-                        pk_st16(ou, crs_u, o);
+                        if constexpr (DBG & 64) asm volatile("" ::"v"(ou));         // ablation: no stores
+                        else pk_st16(ou, crs_u, (DBG & 32) ? 0xFFFFFFF0u : o);   // ablation: no traffic
                     }
                 }
         }
@@ -591,45 +601,33 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         }
     };
 
-    // ---- dynamic schedule: wave 0's dequeue state machine (see the header) ----
-    int deq_state = 0;  // 0 idle, 1 issue at this phase's end, 2 in flight
-    int deq_age = 0, deq_slot = 0;
-    bool deq_home = false, home_ok = home_size > 0, deq_done = false;
+    // ---- dynamic schedule: wave 0's dequeue state (see the header) ----
+    // bits 0-3: queue of the next dequeue (0-7 dispatch group, 8 tail); 4: requested; 5: the
+    // atomic in flight is a real dequeue; 6: no work left
+    int deq = blockIdx.x & 7;
     uint32_t deq_v = 0u;
-    auto publish = [&](int u) {
-        if (lane == 0) *(volatile int*)(ring + (deq_slot & 3)) = u;
-        deq_state = 0;
-        deq_done = u < 0;
-    };
 
-    // ---- prologue: the first unit, then σ = 0..5 in flight (K-tile 0, halves 0/1 of K-tile 1) ----
+    // ---- prologue: the first item, then σ = 0..5 in flight (K-tile 0, halves 0/1 of K-tile 1) ----
     if (dyn) {
-        if (wave == 0) {  // nothing is in flight yet: plain atomics, compiler-managed waits
-            int u = -1;
-            if (lane == 0) {
-                bool hk = home_size > 0;
-                if (hk) {
-                    const int v = __hip_atomic_fetch_add(cnt + xq * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    if ((unsigned)v < (unsigned)home_size) u = home_unit(v);
-                    else hk = false;
-                }
-                if (!hk) {
-                    const int v = __hip_atomic_fetch_add(cnt + 8 * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    u = (unsigned)v < (unsigned)(units - tail_base) ? tail_base + v : -1;
-                }
-                ring[0] = u;
-                ring[1] = hk ? 1 : 0;
+        if (wave == 0 && lane == 0) {  // nothing is in flight yet: plain atomics, compiler-managed waits
+            int q = blockIdx.x & 7;
+            int u = deq_map(q, __hip_atomic_fetch_add(p.sched + q * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+            if (u == -2) {  // this group's queue is empty: the shared tail
+                q = 8;
+                u = deq_map(8, __hip_atomic_fetch_add(p.sched + 8 * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
             }
+            ring[0] = u;
+            ring[1] = q | (u < 0 ? 64 : 0);
         }
         __syncthreads();  // no DMA in flight yet: a plain barrier drains nothing
-        home_ok = ring[1] != 0;
-        deq_done = unit_of(0) < 0;
+        deq = __builtin_amdgcn_readfirstlane(ring[1]);
     }
-    cu = unit_of(0);
+    int c_s = 0;  // compute side: sequence number of its item (ring slot), and the item
+    int c_u = unit_of(0);  // (dynamic: the cursor is never more than one item ahead, nk >= 5)
+    cu = c_u;
     if (cu >= 0) {
-        cnit = unit_items(cu);
         cur_set();
         issue_h(H0{});
         issue_h(H1{});
@@ -638,54 +636,57 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         cur_adv();
         issue_h(H0{});
         issue_h(H1{});
-        vm_wait<8>();
     }
+    vm_wait<8>();
     asm volatile("s_barrier" ::: "memory");
     if (wr == 1) asm volatile("s_barrier" ::: "memory");  // stagger: waves 4-7 one barrier behind
     in_loop = true;
     __builtin_amdgcn_sched_barrier(0);
 
-    int c_m0 = 0, c_n0 = 0, c_kb = 0, c_ke = 0, c_tm = 0, c_sid = 0;
-    int c_s = 0, c_u = unit_of(0), c_i = 0, c_nit = c_u >= 0 ? unit_items(c_u) : 0, c_kt = 0;
+    int c_m0 = 0, c_n0 = 0, c_kb = 0, c_ke = 0, c_tm = 0, c_sid = 0, c_kt = 0;
     if (c_u >= 0) {
-        item_coords(c_u * C, c_m0, c_n0, c_kb, c_ke, c_tm);
-        c_sid = (c_u * C) / tiles;
+        item_coords(c_u, c_m0, c_n0, c_kb, c_ke, c_tm);
+        c_sid = c_u / tiles;
     }
     int since_epi = 4;
 
     // phase wait: σ ≤ φ+2 must have landed (this wave's DMA); younger = the 3 half-tiles
     // issued in the previous 3 phases (6 ops) plus, within 4 phases of an epilogue, its stores,
-    // plus (wave 0) a schedule atomic issued within the last 4 phases
-    auto phase_wait = [&]() {
+    // plus in q1-q3 (XW) wave 0's schedule atomic of this K-tile
+    auto phase_wait = [&](auto xw) {
         if constexpr (DBG & 2) return;
-        bool xtra = false;
-        if (dyn && wave == 0 && deq_state == 2) xtra = ++deq_age <= 4;
+        constexpr bool XW = decltype(xw)::value;
         if (since_epi < 4) {
-            if (xtra) vm_wait<7 + S_EPI>();
+            if (XW && wave == 0) vm_wait<7 + S_EPI>();
             else vm_wait<6 + S_EPI>();
         } else {
-            if (xtra) vm_wait<7>();
+            if (XW && wave == 0) vm_wait<7>();
             else vm_wait<6>();
         }
         ++since_epi;
-        if (dyn && wave == 0 && deq_state == 2 && deq_age >= 5) {  // retired by the wait above
-            const int v = pk_deq_take(deq_v);
-            // (unsigned compares: a corrupted counter can only end the block's work, never index past it)
-            if (!deq_home) publish((unsigned)v < (unsigned)(units - tail_base) ? tail_base + v : -1);
-            else if ((unsigned)v < (unsigned)home_size) publish(home_unit(v));
-            else {  // this group's queue is drained: the shared tail next
-                home_ok = false;
-                deq_state = 1;
-            }
-        }
     };
-    // after a phase's DMA issue: wave 0 sends a pending dequeue
-    auto deq_issue = [&]() {
-        if (dyn && wave == 0 && deq_state == 1) {
-            deq_home = home_ok;
-            deq_v = pk_deq_issue(cnt + (home_ok ? xq : 8) * PK_CTR_STRIDE, lane);
-            deq_state = 2;
-            deq_age = 0;
+    // q0, after its wait, before its DMA: wave 0 consumes the previous K-tile's atomic (retired by
+    // that wait) and sends this K-tile's (a dequeue if one is wanted, else a no-op).  Real dequeues
+    // are sent at an item's K-tile 0 or 1 only and consumed by K-tile 2 (nk >= 5); the no-op of an
+    // item's last K-tile is retired before the epilogue (vm_wait<8> there), so no asynchronous
+    // register write can land while the epilogue reuses registers
+    auto deq_step = [&]() {
+        if (wave == 0) {
+            if (deq & 32) {
+                const int u = deq_map(deq & 15, pk_deq_take(deq_v));
+                if (u == -2) {
+                    deq = (deq & 64) | 8 | 16;  // this group's queue is drained: the shared tail
+                } else {
+                    if (lane == 0) *(volatile int*)(ring + ((c_s + 1) & 3)) = u;
+                    deq = (deq & ~32) | (u < 0 ? 64 : 0);
+                }
+            }
+            // ONE asm on both paths (a branch per path made hipcc merge two registers by copies
+            // issued before the hardware had written the value)
+            const bool want = (deq & 16) != 0;
+            if constexpr (FP8) pk_deq_noop();
+            else pk_deq_issue(deq_v, dyn ? p.sched + (deq & 15) * PK_CTR_STRIDE : nullptr, lane == 0 && want);
+            deq = (deq & ~48) | (want ? 32 : 0);
         }
     };
     auto sync_mma_begin = [&]() {
@@ -720,11 +721,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j_][S], Af[i_][S], acc[MH][NH][i_][j_], 0, 0, 0);
     // one phase: counted wait, this phase's fragment reads, the DMA of one half-tile (in the read
     // segment, or between the two k-steps' MFMAs with DBG bit 3), barrier, 16 MFMAs, barrier
-#define RN_PK_PHASE(READS, ISSUE, MH, NH, BF)                                                          \
-    phase_wait();                                                                                      \
+#define RN_PK_PHASE(XW, READS, ISSUE, MH, NH, BF)                                                      \
+    phase_wait(std::integral_constant<bool, XW>{});                                                    \
     READS                                                                                              \
     if constexpr (!(DBG & 8)) { ISSUE }                                                                \
-    deq_issue();                                                                                       \
     sync_mma_begin();                                                                                  \
     if constexpr (DBG & 8) {                                                                           \
         RN_PK_MMA_S(MH, NH, BF, 0)                                                                     \
@@ -740,31 +740,32 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll 1
     for (int u = 0; c_u >= 0; ++u) {
         const char* sl = smem + (u & 1) * (4 * PK_HALF);
-        // a unit's first K-tile: wave 0 asks for the unit after it (sent after q0's DMA)
-        if (dyn && wave == 0 && c_kt == 0 && c_i == 0 && !deq_done) {
-            deq_state = 1;
-            deq_slot = c_s + 1;
-        }
+        // an item's first K-tile: wave 0 asks for the item after it (sent after q0's DMA)
+        if (dyn && wave == 0 && c_kt == 0 && !(deq & 64)) deq |= 16;
         // q0: At + Bl  (fragment reads first: their latency runs under the DMA issue)
-        RN_PK_PHASE(
+        RN_PK_PHASE(false,
+            deq_step();
             _Pragma("unroll") for (int s = 0; s < 2; ++s) {
                 _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl, wr * 64 + i * 16, s, lane);
                 _Pragma("unroll") for (int j = 0; j < 2; ++j) Bl[j][s] = pk_frag_b<BKC>(sl + PK_HALF, wc * 32, j, s, lane);
             },
             issue_h(H2{});, 0, 0, Bl)
         // q1: At + Br
-        RN_PK_PHASE(
+        RN_PK_PHASE(true,
             _Pragma("unroll") for (int s = 0; s < 2; ++s)
                 _Pragma("unroll") for (int j = 0; j < 2; ++j) Br[j][s] = pk_frag_b<BKC>(sl + 2 * PK_HALF, wc * 32, j, s, lane);,
             issue_h(H3{});, 0, 1, Br)
         // q2: Ab + Br (the cursor moves on to K-tile u + 2)
-        RN_PK_PHASE(
+        RN_PK_PHASE(true,
             _Pragma("unroll") for (int s = 0; s < 2; ++s)
                 _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl + 3 * PK_HALF, wr * 64 + i * 16, s, lane);,
             cur_adv(); issue_h(H0{});, 1, 1, Br)
         // q3: Ab + Bl (all fragments already in registers)
-        RN_PK_PHASE(, issue_h(H1{});, 1, 0, Bl)
+        RN_PK_PHASE(true, , issue_h(H1{});, 1, 0, Bl)
         if (++c_kt == nk) {
+            // retire wave 0's schedule op of this K-tile (issued before q0's DMA: 8 younger ops);
+            // every other op this waits for, the next q0 wait would wait for anyway
+            vm_wait<8>();
             if constexpr (!(DBG & 4)) {
                 epilogue(c_m0, c_n0, c_tm, c_sid);
             } else {  // keep the accumulators (and the MFMAs feeding them) alive
@@ -787,14 +788,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
             c_kt = 0;
-            if (++c_i == c_nit) {
-                c_u = unit_of(++c_s);
-                c_i = 0;
-                c_nit = c_u >= 0 ? unit_items(c_u) : 0;
-            }
+            c_u = unit_of(++c_s);
             if (c_u >= 0) {
-                item_coords(c_u * C + c_i, c_m0, c_n0, c_kb, c_ke, c_tm);
-                c_sid = (c_u * C + c_i) / tiles;
+                item_coords(c_u, c_m0, c_n0, c_kb, c_ke, c_tm);
+                c_sid = c_u / tiles;
             }
         }
     }
@@ -803,6 +800,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #undef RN_PK_PHASE
     if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger barrier
     if (dyn && wave == 0 && lane == 0) {  // the last block out resets the counters for the next launch
+        int* const cnt = p.sched;
         if (__hip_atomic_fetch_add(cnt + 9 * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1) {
 #pragma unroll
             for (int i = 0; i < 10; ++i) __hip_atomic_store(cnt + i * PK_CTR_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -847,10 +845,7 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
     const int reserve = rn_gemm_get_reserve();
     if (reserve > 0 && reserve < cus) cus -= reserve;
     a.sched = DBG == 0 ? rn_gemm_sched_slot(dev, st) : nullptr;
-    const int nk = a.k_per_split / BK;
-    const int C = a.sched ? (nk >= 5 ? 1 : (4 + nk) / nk) : 1;
-    const int units = (items + C - 1) / C;
-    const int grid = units < cus ? units : cus;
+    const int grid = items < cus ? items : cus;
     kern<<<grid, 512, PK_LDS, st>>>(a);
 }
 

@@ -21,6 +21,8 @@ int rn_gemm_launch_pk_dbg(GemmArgs& a, bool ak, bool bk, int dbg, hipStream_t st
         case 8: launch_dbg<8>(a, ak, bk, st); break;
         case 9: launch_dbg<9>(a, ak, bk, st); break;
         case 16: launch_dbg<16>(a, ak, bk, st); break;
+        case 32: launch_dbg<32>(a, ak, bk, st); break;
+        case 64: launch_dbg<64>(a, ak, bk, st); break;
         default: return -1;
     }
     return 0;

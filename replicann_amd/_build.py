@@ -27,7 +27,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "objs"
-OUT = Path(__file__).resolve().parent / "_C.so"
+# REPLICANN_BUILD_OUT: write the library elsewhere (developer A/B builds, e.g. REPLICANN_DEV=1 ablations
+# loaded with REPLICANN_SO), leaving the tree's production _C.so untouched
+OUT = Path(os.environ.get("REPLICANN_BUILD_OUT") or Path(__file__).resolve().parent / "_C.so")
 ARCH = os.environ.get("REPLICANN_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 

@@ -40,8 +40,16 @@ class Linear(nn.Module):
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
         self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
         self.fp8 = fp8
-        self.fp8_state = ops.Fp8State() if fp8 else None
+        self.fp8_state = None
+        if fp8:  # delayed-scaling state [activation, weight] x [scale, amax, -, -]: a checkpointed buffer
+            self.register_buffer("fp8_scales", torch.zeros(2, 4))
+            self.fp8_state = ops.Fp8State(owner=self)
         nn.init.normal_(self.weight, std=std)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+        if self.fp8_state is not None:  # a loaded slot holds a scale: continue with delayed scaling
+            self.fp8_state.sync_ready()
 
     def forward(self, x, act=None, residual=None):
         return ops.linear(x, self.weight, self.bias, act=act, residual=residual, fp8=self.fp8_state)

@@ -45,14 +45,40 @@ class Fp8State:
     single pass with delayed scaling: the scale comes from the previous quantisation's
     amax (x2 headroom, saturating beyond it) and the pass records the new amax
     (``fp8_quantize_delayed``) — the Transformer-Engine recipe with a history of one.
-    Everything is on device, so a captured step graph replays it unchanged."""
+    Everything is on device, so a captured step graph replays it unchanged.
 
-    def __init__(self):
-        self.t = None
+    Persistence: with an ``owner`` module the (2, 4) state tensor is that module's registered
+    buffer (``fp8_scales``): it moves with ``.to()``, is saved / loaded with the state_dict (so a
+    resumed run continues with the same delayed scales), and is part of ``model.buffers()``, which
+    the trainer snapshots around its autotuning pass and graph-capture warm-ups.  The host-side
+    ``ready`` flags (whether a slot holds a scale yet) follow the tensor: they are re-derived when a
+    state_dict is loaded (:func:`sync_ready_from_tensors`) and snapshotted with it
+    (:func:`ready_snapshot` / :func:`ready_restore`)."""
+
+    def __init__(self, owner=None, name="fp8_scales"):
+        self._owner = owner
+        self._name = name
+        self._t = None
         self.ready = [False, False]
         self._offer = None  # (activation tensor, its e4m3 copy) written by the producer kernel
         self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
         self.wcache = None  # Fp8WeightCache holding this GEMM's e4m3 weight (refreshed by the optimizer)
+
+    @property
+    def t(self):
+        return getattr(self._owner, self._name) if self._owner is not None else self._t
+
+    @t.setter
+    def t(self, value):
+        if self._owner is not None:
+            self._owner._buffers[self._name] = value
+        else:
+            self._t = value
+
+    def sync_ready(self):
+        """ready[i] = slot i holds a scale (host sync: call at load time, never inside a step)."""
+        t = self.t
+        self.ready = [bool(t is not None and float(t[i, 0]) > 0) for i in range(2)]
 
     def producer_ready(self, device) -> bool:
         """True once the activation slot has a delayed scale, so a producer kernel (LayerNorm)
@@ -85,6 +111,25 @@ class Fp8State:
             self.ready[i] = True
             return q, st
         return _ext.ops().fp8_quantize_delayed(x, st), st
+
+
+def fp8_states(model):
+    """Every Fp8State of ``model`` (layers with ``fp8_state``), in module order."""
+    return [m.fp8_state for m in model.modules() if getattr(m, "fp8_state", None) is not None]
+
+
+def ready_snapshot(model):
+    return [list(st.ready) for st in fp8_states(model)]
+
+
+def ready_restore(model, snap):
+    for st, r in zip(fp8_states(model), snap):
+        st.ready = list(r)
+
+
+def sync_ready_from_tensors(model):
+    for st in fp8_states(model):
+        st.sync_ready()
 
 
 def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State, out8: Fp8State | None = None):

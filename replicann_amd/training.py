@@ -239,17 +239,20 @@ class Trainer:
         if self.device.type != "cuda" or self.ddp is None:
             return
         from .ops import rng as dev_rng
+        from .ops.fp8 import ready_restore, ready_snapshot
         probe = self._make_data()
         x, y = next(probe)
         del probe
         state = self.opt.state_tensors() + list(self.model.buffers()) + dev_rng.state_tensors(self.device)
         snap = [t.clone() for t in state]
+        ready = ready_snapshot(self.model)  # fp8 delayed-scaling slots: tensors above, flags here
         with self.ddp.no_sync(), self.timer.paused():
             self.opt.zero_grad()
             self.net(x, y).backward()
         self.opt.zero_grad()
         for t, v in zip(state, snap):
             t.copy_(v)
+        ready_restore(self.model, ready)
         torch.cuda.synchronize(self.device)
         if self.world > 1:  # every rank adopts rank 0's picks: the same kernels on every GPU
             import torch.distributed as dist
@@ -282,7 +285,10 @@ class Trainer:
         c = self.cfg
         self._static = [tuple(t.clone() for t in next(self.data)) for _ in range(c.grad_accum)]
         from .ops import rng as dev_rng
-        state = self.opt.state_tensors() + [b for b in self.model.buffers()] + dev_rng.state_tensors(self.device)
+        # fp8 delayed-scaling slots are NOT rolled back: the warm-ups seed them, so the captured step
+        # is the steady-state (delayed-scaling) step, not a first step frozen into every replay
+        bufs = [b for n, b in self.model.named_buffers() if not n.endswith("fp8_scales")]
+        state = self.opt.state_tensors() + bufs + dev_rng.state_tensors(self.device)
         snap = [t.clone() for t in state]
         count = self.opt.step_count
         s = torch.cuda.Stream()

@@ -14,7 +14,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from replicann_amd import ops  # noqa: E402
+from replicann_amd import _ext, ops  # noqa: E402
 
 # (name, M, N, K, layout, act, split)
 SHAPES = [
@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--reserve", type=int, nargs="*", default=[8])
     ap.add_argument("--only", default=None)
     a = ap.parse_args()
-    R = torch.ops.replicann
+    R = _ext.ops()  # loads the native library (fails loudly if missing or stale)
     arms = [("static", 0, 0), ("dynamic", 1, 0)] + [(f"dynamic_r{r}", 1, r) for r in a.reserve]
     for name, M, N, K, lay, act, split in SHAPES:
         if a.only and a.only not in name:

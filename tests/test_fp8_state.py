@@ -1,0 +1,46 @@
+"""fp8 delayed-scaling state is persistent: the per-layer scale / amax slots are module
+buffers — saved and loaded with the state_dict, rolled back by the trainer's autotuning pass — and
+the host-side ready flags follow the loaded tensors."""
+
+import pytest
+import torch
+
+import replicann_amd as R
+from replicann_amd.ops.fp8 import fp8_states
+
+
+def _model():
+    torch.manual_seed(0)
+    return R.GPT2(R.GPT2Config.tiny(fp8=True))
+
+
+def test_fp8_scales_are_state_dict_buffers():
+    m = _model()
+    keys = [k for k in m.state_dict() if k.endswith("fp8_scales")]
+    assert len(keys) == 3 * m.config.n_layer  # c_attn, c_fc, mlp c_proj per block
+    ids = torch.randint(0, 1000, (2, 32))
+    m(ids, ids)  # first quantisation: current scaling fills the slots
+    sts = fp8_states(m)
+    assert all(st.ready == [True, True] for st in sts)
+    m2 = _model()
+    assert not any(any(st.ready) for st in fp8_states(m2))
+    m2.load_state_dict(m.state_dict())
+    for a, b in zip(fp8_states(m), fp8_states(m2)):
+        assert torch.equal(a.t, b.t) and b.ready == [True, True]
+
+
+@pytest.mark.gpu
+def test_fp8_resume_bitwise_gpu(cuda, tmp_path):
+    from replicann_amd.training import TrainConfig, Trainer
+
+    kw = dict(model="gpt2-tiny", model_kwargs={"fp8": True}, batch_size=4, seq_len=128, steps=100,
+              warmup_steps=1, lr=1e-3, log_every=10**9, seed=5, graph="off")
+    a = Trainer(TrainConfig(**kw))
+    for _ in range(3):
+        a.step()
+    ck = str(tmp_path / "fp8.pt")
+    a.save(ck)
+    la = [float(a.step()) for _ in range(3)]
+    b = Trainer(TrainConfig(**kw, resume=ck))
+    lb = [float(b.step()) for _ in range(3)]
+    assert la == lb
