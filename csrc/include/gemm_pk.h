@@ -36,7 +36,9 @@
 //     the in-flight operand DMA; epilogues that read a full tile (residual, saved
 //     pre-activation, accumulate target) do wait for it.
 //
-// Tile schedule (p.sched != nullptr; the default, see rn_gemm_set_sched): the grid does not walk a
+// Tile schedule (DYN instantiations; chosen per launch while the queue is enabled — by the data-
+// parallel reducer whenever collectives can run beside the backward, rn_gemm_set_sched): the grid
+// does not walk a
 // static list (bid + s·grid) but DEQUEUES its work, so a workgroup that starts late — because an
 // RCCL kernel on the comm stream held its CU when the GEMM launched — simply takes fewer tiles
 // instead of delaying the whole GEMM by the collective's duration.
@@ -227,20 +229,16 @@ RN_DEV void pk_deq_issue(uint32_t& v, const int* ctr, bool live) {
     v = 1u;
     asm volatile("buffer_atomic_add %0, %1, %2, 0 offen sc0 ; rn_deq_issue" : "+v"(v) : "v"(off), "s"(rs) : "memory");
 }
-// the static-walk form without a return (no register written asynchronously; still counted)
-RN_DEV void pk_deq_noop() {
-    const u32x4 rs = pk_rsrc_u(nullptr, 0u);
-    asm volatile("buffer_atomic_add %0, %1, %2, 0 offen ; rn_deq_noop" ::"v"(1u), "v"(0xFFFFFFF0u), "s"(rs) : "memory");
-}
 RN_DEV int pk_deq_take(uint32_t v) {
     asm volatile("; rn_deq_take %0" : "+v"(v));
     return (int)__builtin_amdgcn_readfirstlane(v);
 }
 #pragma clang diagnostic pop
 
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false>
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false, bool DYN = false>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     static_assert(!FP8 || (AK && BKC && !(DBG & 8)), "fp8: K-contiguous operands only");
+    static_assert(!DYN || (!FP8 && DBG == 0), "dynamic schedule: bf16 production kernels only");
     constexpr int BM = 256, BN = 256;
     constexpr int S_EPI = (DBG & 64) ? 0 : pk_epi_stores<ACT, SPLIT, F32>();
     static_assert(7 + S_EPI <= 63, "vmcnt range");
@@ -256,12 +254,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     const int nk = p.k_per_split / BK;
 
     // ---- tile schedule (see the header): static walk or dynamic queue over the items ----
-    // (not for fp8: its register pressure makes hipcc reuse the schedule op's register as a
-    // temporary between issue and retire — tests/test_gemm_isa.py checks every instantiation)
-    const bool dyn = p.sched != nullptr && DBG == 0 && !FP8 && nk >= 5;
+    // DYN (a separate instantiation, so the static walk carries none of the queue's code; the
+    // host takes it only for K slices of >= 5 K-tiles with a counter slot — not for fp8, whose
+    // register pressure makes hipcc reuse the schedule op's register as a temporary between issue
+    // and retire: tests/test_gemm_isa.py checks every instantiation)
+    constexpr bool dyn = DYN;
     int* const ring = reinterpret_cast<int*>(smem + PK_RING);
     auto unit_of = [&](int s) -> int {
-        if (!dyn) {
+        if constexpr (!DYN) {
             const int u = bid + s * grid;
             return u < items ? u : -1;
         }
@@ -608,7 +608,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     uint32_t deq_v = 0u;
 
     // ---- prologue: the first item, then σ = 0..5 in flight (K-tile 0, halves 0/1 of K-tile 1) ----
-    if (dyn) {
+    if constexpr (DYN) {
         if (wave == 0 && lane == 0) {  // nothing is in flight yet: plain atomics, compiler-managed waits
             int q = blockIdx.x & 7;
             int u = deq_map(q, __hip_atomic_fetch_add(p.sched + q * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED,
@@ -657,10 +657,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         if constexpr (DBG & 2) return;
         constexpr bool XW = decltype(xw)::value;
         if (since_epi < 4) {
-            if (XW && wave == 0) vm_wait<7 + S_EPI>();
+            if (DYN && XW && wave == 0) vm_wait<7 + S_EPI>();
             else vm_wait<6 + S_EPI>();
         } else {
-            if (XW && wave == 0) vm_wait<7>();
+            if (DYN && XW && wave == 0) vm_wait<7>();
             else vm_wait<6>();
         }
         ++since_epi;
@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     // item's last K-tile is retired before the epilogue (vm_wait<8> there), so no asynchronous
     // register write can land while the epilogue reuses registers
     auto deq_step = [&]() {
-        if (wave == 0) {
+        if (DYN && wave == 0) {
             if (deq & 32) {
                 const int u = deq_map(deq & 15, pk_deq_take(deq_v));
                 if (u == -2) {
@@ -684,8 +684,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             // ONE asm on both paths (a branch per path made hipcc merge two registers by copies
             // issued before the hardware had written the value)
             const bool want = (deq & 16) != 0;
-            if constexpr (FP8) pk_deq_noop();
-            else pk_deq_issue(deq_v, dyn ? p.sched + (deq & 15) * PK_CTR_STRIDE : nullptr, lane == 0 && want);
+            pk_deq_issue(deq_v, p.sched + (deq & 15) * PK_CTR_STRIDE, lane == 0 && want);
             deq = (deq & ~48) | (want ? 32 : 0);
         }
     };
@@ -737,8 +736,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     }                                                                                                  \
     sync_mma_end();
 
+    // static walk: the block's item count is known (bid + s·grid < items)
+    const int n_static = DYN ? 0 : ((items - bid + grid - 1) / grid) * nk;
 #pragma unroll 1
-    for (int u = 0; c_u >= 0; ++u) {
+    for (int u = 0; DYN ? (c_u >= 0) : (u < n_static); ++u) {
         const char* sl = smem + (u & 1) * (4 * PK_HALF);
         // an item's first K-tile: wave 0 asks for the item after it (sent after q0's DMA)
         if (dyn && wave == 0 && c_kt == 0 && !(deq & 64)) deq |= 16;
@@ -765,7 +766,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         if (++c_kt == nk) {
             // retire wave 0's schedule op of this K-tile (issued before q0's DMA: 8 younger ops);
             // every other op this waits for, the next q0 wait would wait for anyway
-            vm_wait<8>();
+            if constexpr (DYN) vm_wait<8>();
             if constexpr (!(DBG & 4)) {
                 epilogue(c_m0, c_n0, c_tm, c_sid);
             } else {  // keep the accumulators (and the MFMAs feeding them) alive
@@ -799,7 +800,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #undef RN_PK_MMA_S
 #undef RN_PK_PHASE
     if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger barrier
-    if (dyn && wave == 0 && lane == 0) {  // the last block out resets the counters for the next launch
+    if (DYN && wave == 0 && lane == 0) {  // the last block out resets the counters for the next launch
         int* const cnt = p.sched;
         if (__hip_atomic_fetch_add(cnt + 9 * PK_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1) {
 #pragma unroll
@@ -821,9 +822,18 @@ extern "C" int* rn_gemm_sched_slot(int dev, hipStream_t st);
 extern "C" int rn_gemm_get_reserve();
 namespace rn_gemm_detail {
 
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false>
+// the host side of the schedule choice: a counter slot for a dynamic launch (needs K slices of
+// >= 5 K-tiles and the queue enabled), else nullptr (static walk)
+inline int* pk_sched_slot(const GemmArgs& a, hipStream_t st) {
+    if (a.k_per_split / BK < 5) return nullptr;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return rn_gemm_sched_slot(dev, st);
+}
+
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false, bool DYN = false>
 void launch_pk_t(GemmArgs& a, hipStream_t st) {
-    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8>;
+    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8, DYN>;
     static int attr_dev = -1;  // the >64 KiB LDS opt-in, per device the process launches on
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -844,7 +854,7 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
     }
     const int reserve = rn_gemm_get_reserve();
     if (reserve > 0 && reserve < cus) cus -= reserve;
-    a.sched = DBG == 0 ? rn_gemm_sched_slot(dev, st) : nullptr;
+    if (!DYN) a.sched = nullptr;
     const int grid = items < cus ? items : cus;
     kern<<<grid, 512, PK_LDS, st>>>(a);
 }

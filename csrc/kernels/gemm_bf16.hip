@@ -110,17 +110,18 @@ inline Choice pick(int M, int N, int K, int split_req) {
 extern "C" {
 
 // ---- persistent-GEMM schedule knobs (gemm_pk.h) ----
-// sched: 1 = dynamic tile queue (default), 0 = static walk.  reserve: CUs a cfg-9 launch leaves
-// free for a concurrent collective.  Host-side state read at launch (captured graphs keep the
-// values of their capture).
+// sched: 1 = dynamic tile queue, 0 = static walk (default: the queue costs ~1-3 % per GEMM on an
+// otherwise idle GPU; the data-parallel reducer turns it on while collectives can overlap the
+// backward).  reserve: CUs a cfg-9 launch leaves free for a concurrent collective.  Host-side
+// state read at launch (captured graphs keep the values of their capture).
 static std::atomic<int> g_sched{-1};
 static std::atomic<int> g_reserve{0};
 void rn_gemm_set_sched(int m) { g_sched = m ? 1 : 0; }
 int rn_gemm_get_sched() {
     int v = g_sched.load();
-    if (v < 0) {  // REPLICANN_GEMM_SCHED=static selects the static walk process-wide
+    if (v < 0) {  // REPLICANN_GEMM_SCHED=dynamic|static: the process-wide initial setting
         const char* e = std::getenv("REPLICANN_GEMM_SCHED");
-        v = (e && e[0] == 's') ? 0 : 1;
+        v = (e && e[0] == 'd') ? 1 : 0;
         g_sched = v;
     }
     return v;

@@ -119,10 +119,15 @@ class DistributedDataParallel(nn.Module):
         self.comm_wait_ms = 0.0  # host time spent in finish() (last step): the exposed all-reduce tail
 
     def _reserve_cus(self):
-        """While collectives can run beside the backward (world > 1, or the one-GPU comm proxy),
-        the persistent GEMM leaves ``REPLICANN_GEMM_RESERVE`` CUs (default 8: one per dispatch
-        group) free, so a bucket's RCCL workgroups start when the bucket is ready instead of when
-        the running GEMM drains; the GEMM's dynamic tile queue absorbs whatever CUs they hold."""
+        """GEMM schedule knobs for steps whose collectives run beside the backward (world > 1,
+        or the one-GPU comm proxy).  ``REPLICANN_GEMM_SCHED=dynamic`` makes the persistent GEMM
+        dequeue its tiles (csrc/include/gemm_pk.h, "Tile schedule"): a workgroup that starts
+        late because RCCL holds its CU takes fewer tiles instead of stalling the whole GEMM.
+        It is opt-in: on GPT-2-small under the proxy the queue's per-K-tile atomic costs more
+        than it recovers (68.2 ms static vs 70.6 ms dynamic per step, profiles/
+        gemm_sched_proxy_r3f.txt).  ``REPLICANN_GEMM_RESERVE`` CUs (default 0) can additionally
+        be left free for the collectives' workgroups (measured: a reservation costs more in
+        wave quantisation than it saves, profiles/gemm_sched_ab_r3d.txt)."""
         import os
 
         dev = self.flat.grad.device
@@ -130,9 +135,12 @@ class DistributedDataParallel(nn.Module):
             return
         from .. import _ext
 
-        r = int(os.environ.get("REPLICANN_GEMM_RESERVE", 8))
-        _ext.ops().gemm_set_reserve(r)
-        self.gemm_reserve = _ext.ops().gemm_get_reserve()
+        ops = _ext.ops()
+        if os.environ.get("REPLICANN_GEMM_SCHED", "static") == "dynamic":
+            ops.gemm_set_sched(1)
+        ops.gemm_set_reserve(int(os.environ.get("REPLICANN_GEMM_RESERVE", 0)))
+        self.gemm_reserve = ops.gemm_get_reserve()
+        self.gemm_sched = ops.gemm_get_sched()
 
     # ------------------------------------------------------------------
     def _broadcast_state(self):

@@ -187,13 +187,16 @@ def test_proxy_comm_keeps_data_and_orders_streams():
         c.close()
 
 
-def test_ddp_step_proxy_matches_native_and_reserves_cus(one_rank_pg):
+def test_ddp_step_proxy_matches_native_and_enables_queue(one_rank_pg, monkeypatch):
+    torch.ops.replicann.gemm_set_sched(0)
+    monkeypatch.setenv("REPLICANN_GEMM_SCHED", "dynamic")  # opt-in (static is the measured default)
     nat_l, nat_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"))
-    assert torch.ops.replicann.gemm_get_reserve() == 0  # a one-rank real group runs no collective beside GEMMs
+    assert torch.ops.replicann.gemm_get_sched() == 0  # a one-rank real group runs no collective beside GEMMs
     px_l, px_w, px_g, px_c, _ = _run(dict(graph="auto", ddp="on", comm="proxy"))
     try:
         assert px_c == "proxy" and px_g  # capturable like the native communicator
-        assert torch.ops.replicann.gemm_get_reserve() == 8
-        assert px_l == nat_l and torch.equal(px_w, nat_w)
+        assert torch.ops.replicann.gemm_get_sched() == 1  # dynamic tile queue while collectives overlap (opt-in)
+        assert px_l == nat_l and torch.equal(px_w, nat_w)  # (the queue changes no output bit)
     finally:
+        torch.ops.replicann.gemm_set_sched(0)
         torch.ops.replicann.gemm_set_reserve(0)

@@ -17,7 +17,7 @@ import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-TUS = ["gemm_pk_tt", "gemm_pk_tf", "gemm_pk_ff", "gemm_pk_ft", "gemm_pk_fp8"]
+TUS = ["gemm_pk_tt_dyn", "gemm_pk_tf_dyn", "gemm_pk_ff_dyn", "gemm_pk_ft_dyn"]
 
 
 @pytest.mark.skipif(not Path(HIPCC).exists(), reason="hipcc not available")
@@ -35,4 +35,4 @@ def test_schedule_register_never_touched_in_flight(tmp_path):
     r = subprocess.run([sys.executable, str(ROOT / "tests" / "tools" / "gemm_deq_check.py"), *map(str, outs)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-4000:]
-    assert r.stdout.count(" OK") >= 20  # every bf16 instantiation has the queue and passed
+    assert r.stdout.count(" OK") >= 20  # every dynamic instantiation was checked and passed
