@@ -118,6 +118,8 @@ class DistributedDataParallel(nn.Module):
         flat.contribution_hooks.append(self._contribution)
         self.comm_wait_ms = 0.0  # host time spent in finish() (last step): the exposed all-reduce tail
 
+    _sched_ops = None  # set in "overlap" schedule mode
+
     def _reserve_cus(self):
         """GEMM schedule knobs for steps whose collectives run beside the backward (world > 1,
         or the one-GPU comm proxy).  ``REPLICANN_GEMM_SCHED=dynamic`` makes the persistent GEMM
@@ -136,8 +138,12 @@ class DistributedDataParallel(nn.Module):
         from .. import _ext
 
         ops = _ext.ops()
-        if os.environ.get("REPLICANN_GEMM_SCHED", "static") == "dynamic":
+        mode = os.environ.get("REPLICANN_GEMM_SCHED", "static")
+        if mode == "dynamic":
             ops.gemm_set_sched(1)
+        elif mode == "overlap":  # queue only for the GEMMs launched while a collective is in flight
+            ops.gemm_sched_init(dev.index if dev.index is not None else torch.cuda.current_device())
+            self._sched_ops = ops
         ops.gemm_set_reserve(int(os.environ.get("REPLICANN_GEMM_RESERVE", 0)))
         self.gemm_reserve = ops.gemm_get_reserve()
         self.gemm_sched = ops.gemm_get_sched()
@@ -167,6 +173,8 @@ class DistributedDataParallel(nn.Module):
         if dst.data_ptr() != g.data_ptr():
             dst.copy_(g)  # stream-ordered after the kernels that produced the gradient
         self.comm.all_reduce(dst)
+        if self._sched_ops is not None:
+            self._sched_ops.gemm_set_sched(1)  # later GEMMs of this backward share the CUs with RCCL
 
     def _launch_ready(self, from_hook=False):
         while self._next < len(self.buckets) and self._ready[self._next]:
@@ -256,6 +264,8 @@ class DistributedDataParallel(nn.Module):
                     s_.zero_()
             self._split_done[pid] = uses
         self.comm.wait()  # native: the compute stream joins the comm stream (no host sync)
+        if self._sched_ops is not None:
+            self._sched_ops.gemm_set_sched(0)
         for pid, (lo, hi, uses, sides) in self.split.items():
             for s in sides:
                 self.reduce_buf[lo:hi].add_(s)

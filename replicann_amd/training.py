@@ -81,6 +81,7 @@ class TrainConfig:
     grad_accum: int = 1
     max_grad_norm: float = 1.0
     bucket_mb: float = 64.0
+    reduce_dtype: str = "fp32"    # DDP cross-rank sum: fp32 (exact widening) | bf16 (in place, half the bytes)
     ddp: str = "auto"             # auto (world > 1) | on (also at world 1: one-GPU rehearsal of the DDP step)
     comm: str = "auto"            # auto (native RCCL communicator on GPUs, torch.distributed otherwise) | native | torch
     graph: str = "auto"           # auto | on | off — capture the whole step in one hipGraph
@@ -117,7 +118,9 @@ class Trainer:
             p.data = p.data.to(dtype)
         self.flat = FlatParams(self.model)
         use_ddp = self.world > 1 or cfg.ddp == "on"
-        self.ddp = (DistributedDataParallel(self.model, self.flat, cfg.bucket_mb, comm=cfg.comm, force=True)
+        self.ddp = (DistributedDataParallel(
+            self.model, self.flat, cfg.bucket_mb, comm=cfg.comm, force=True,
+            reduce_dtype=torch.bfloat16 if cfg.reduce_dtype == "bf16" else torch.float32)
                     if use_ddp else None)
         gs = 1.0 / self.world
         if cfg.optimizer == "adamw":
