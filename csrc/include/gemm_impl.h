@@ -64,6 +64,10 @@ struct GemmArgs {
     // persistent kernel (cfg 9) only: dynamic tile queue counters (gemm_pk.h, "Tile schedule"),
     // nullptr = static walk
     int* sched;
+    // persistent kernel only: store the bf16 output with the non-temporal policy (set by the host
+    // for outputs larger than the 256 MiB Infinity Cache, e.g. the LM-head logits: such a stream
+    // cannot stay resident and would only evict the operand panels the main loop re-reads)
+    int st_nt;
 };
 
 template <int BN, int NT>

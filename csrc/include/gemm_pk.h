@@ -36,6 +36,13 @@
 //     the in-flight operand DMA; epilogues that read a full tile (residual, saved
 //     pre-activation, accumulate target) do wait for it.
 //
+// Epilogue operand reads (residual, saved activation): the full-tile read at the end of an item
+// waits behind a vmcnt(0) that also drains the next item's in-flight operand DMA (≈ 15-20 % of a
+// K = 768 tile, profiles/gemm_epilogue_aux_r3k.txt).  An L2 prefetch of that tile during the
+// item's last K-tiles (extra LDS-DMA into scratch LDS) changed nothing — the drain, not the
+// latency of the aux bytes, is the cost — and holding the tile in registers ahead of time does
+// not fit the 256-VGPR budget (it spills).
+//
 // Tile schedule (DYN instantiations; chosen per launch while the queue is enabled — by the data-
 // parallel reducer whenever collectives can run beside the backward, rn_gemm_set_sched): the grid
 // does not walk a
@@ -172,8 +179,18 @@ RN_DEV u32x4 pk_rsrc_u(const void* base, uint32_t bytes) {
 // store data registers would drain it); s_nop 1 covers the store-data read hazard (guide §5.7).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+#if defined(RN_PK_ST_NT)  // A/B builds (REPLICANN_EXTRA_DEFS): epilogue store cache policy
+#define RN_PK_ST_POLICY "nt"
+#elif defined(RN_PK_ST_SC)
+#define RN_PK_ST_POLICY "sc0 sc1"
+#else
+#define RN_PK_ST_POLICY ""
+#endif
 RN_DEV void pk_st16(const u32x4 v, const u32x4& rs, uint32_t voff) {
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen " RN_PK_ST_POLICY "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+RN_DEV void pk_st16_nt(const u32x4 v, const u32x4& rs, uint32_t voff) {
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
 #pragma clang diagnostic pop
 
@@ -241,7 +258,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     static_assert(!DYN || (!FP8 && DBG == 0), "dynamic schedule: bf16 production kernels only");
     constexpr int BM = 256, BN = 256;
     constexpr int S_EPI = (DBG & 64) ? 0 : pk_epi_stores<ACT, SPLIT, F32>();
-    static_assert(7 + S_EPI <= 63, "vmcnt range");
+    constexpr int WY = 6;  // ops younger than a phase's target half-tile: 3 half-tiles × 2 DMA
+    static_assert(WY + 1 + S_EPI <= 63, "vmcnt range");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -456,7 +474,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         // or the accumulate target (bf16 out)
         const bf16* auxp = SPLIT ? nullptr
                                  : (act_bwd(ACT) ? p.pre : (p.res ? p.res : ((p.accumulate && !F32) ? (const bf16*)p.C : nullptr)));
-        // (loaded one 128-row half at a time: 32 VGPRs, all 8 loads of a half in flight together)
+        // (loaded one 128-row half at a time: 32 VGPRs, all 8 loads of a half in flight together;
+        // both halves at once spill: the kernel is at the 256-VGPR limit)
         u32x4 aux[4][2];
         const __amdgpu_buffer_rsrc_t ars = pk_rsrc(auxp ? auxp + (long)m0 * p.ldc + n0 : nullptr, 0x7FFFFFF0u);
         const u32x4 prs = pk_rsrc_u(act_fwd(ACT) && p.pre ? (void*)(p.pre + (long)m0 * p.ldc + n0) : nullptr,
@@ -472,13 +491,20 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int nh = 0; nh < 2; ++nh)
+                    for (int nh = 0; nh < 2; ++nh) {
+#ifdef RN_PK_NO_AUX  // A/B only: no aux traffic and no wait (wrong outputs)
+                        aux[i][nh] = (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+#else
                         aux[i][nh] = __builtin_amdgcn_raw_buffer_load_b128(ars, off(mh, i, nh, 2), 0, 0);
+#endif
+                    }
                 // retire them HERE, in the branch that issued them (vmcnt(0); this epilogue drains the
                 // operand DMA anyway): with the wait left to the separately-branched consumers below,
                 // the compiler's wait insertion assumed the loads could still be pending at the main
                 // loop's head and put vmcnt(2) + vmcnt(0) into every K-tile's first phase
+#ifndef RN_PK_NO_AUX
                 __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -567,6 +593,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                         const u32x4 ou = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
                                           pk_pack2(v[6], v[7])};
                         if constexpr (DBG & 64) asm volatile("" ::"v"(ou));         // ablation: no stores
+                        else if (p.st_nt) pk_st16_nt(ou, crs_u, o);                // wave-uniform choice
                         else pk_st16(ou, crs_u, (DBG & 32) ? 0xFFFFFFF0u : o);   // ablation: no traffic
                     }
                 }
@@ -657,11 +684,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         if constexpr (DBG & 2) return;
         constexpr bool XW = decltype(xw)::value;
         if (since_epi < 4) {
-            if (DYN && XW && wave == 0) vm_wait<7 + S_EPI>();
-            else vm_wait<6 + S_EPI>();
+            if (DYN && XW && wave == 0) vm_wait<WY + 1 + S_EPI>();
+            else vm_wait<WY + S_EPI>();
         } else {
-            if (DYN && XW && wave == 0) vm_wait<7>();
-            else vm_wait<6>();
+            if (DYN && XW && wave == 0) vm_wait<WY + 1>();
+            else vm_wait<WY>();
         }
         ++since_epi;
     };
@@ -821,6 +848,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 extern "C" int* rn_gemm_sched_slot(int dev, hipStream_t st);
 extern "C" int rn_gemm_get_reserve();
 namespace rn_gemm_detail {
+// non-temporal output stores: plain bf16 outputs over 256 MiB (REPLICANN_GEMM_ST_NT=0 disables)
+inline int rn_gemm_st_nt(const GemmArgs& a) {
+    static const bool on = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT"); return !(e && e[0] == '0'); }();
+    return (on && a.split <= 1 && (long)a.M * a.N * 2 > (256L << 20)) ? 1 : 0;
+}
+}  // namespace rn_gemm_detail
+namespace rn_gemm_detail {
 
 // the host side of the schedule choice: a counter slot for a dynamic launch (needs K slices of
 // >= 5 K-tiles and the queue enabled), else nullptr (static walk)
@@ -852,6 +886,7 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
         }
         cus = cu_n;
     }
+    a.st_nt = rn_gemm_st_nt(a);
     const int reserve = rn_gemm_get_reserve();
     if (reserve > 0 && reserve < cus) cus -= reserve;
     if (!DYN) a.sched = nullptr;

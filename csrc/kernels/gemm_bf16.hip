@@ -110,9 +110,10 @@ inline Choice pick(int M, int N, int K, int split_req) {
 extern "C" {
 
 // ---- persistent-GEMM schedule knobs (gemm_pk.h) ----
-// sched: 1 = dynamic tile queue, 0 = static walk (default: the queue costs ~1-3 % per GEMM on an
-// otherwise idle GPU; the data-parallel reducer turns it on while collectives can overlap the
-// backward).  reserve: CUs a cfg-9 launch leaves free for a concurrent collective.  Host-side
+// sched: 1 = dynamic tile queue, 0 = static walk (default: the queue costs 3-12 % per GEMM on an
+// otherwise idle GPU, profiles/gemm_sched_proxy_r3f.txt; REPLICANN_GEMM_SCHED=dynamic turns it on
+// for the process, =overlap lets the data-parallel reducer turn it on while collectives are in
+// flight).  reserve: CUs a cfg-9 launch leaves free for a concurrent collective.  Host-side
 // state read at launch (captured graphs keep the values of their capture).
 static std::atomic<int> g_sched{-1};
 static std::atomic<int> g_reserve{0};

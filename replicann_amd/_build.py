@@ -50,6 +50,9 @@ DEV = os.environ.get("REPLICANN_DEV", "0") == "1"
 if DEV:
     HIP_FLAGS.append("-DREPLICANN_DEV=1")
 DEV_ONLY = {"gemm_pk_dbg"}
+# A/B experiments: extra preprocessor definitions (space-separated NAME[=VALUE]), dev builds only
+if DEV:
+    HIP_FLAGS += [f"-D{d}" for d in os.environ.get("REPLICANN_EXTRA_DEFS", "").split()]
 
 # Per-translation-unit extra flags.  The attention kernels run VALU-bound beside their MFMAs;
 # SLP vectorisation packs adjacent f32 adds/muls into v_pk_add/v_pk_mul_f32, which cost ~22-26

@@ -76,6 +76,26 @@ def test_gemm_persistent_act_backward_multi_tile(cuda):
     assert rel_err(bg.float(), out.float().sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("act", [3, 4, 6])
+@pytest.mark.parametrize("M,N,K", [(9000, 3000, 768), (9000, 3000, 128), (600, 5000, 320)])
+def test_gemm_persistent_act_backward_prefetch(cuda, act, M, N, K):
+    """Act-backward epilogues with the saved-activation L2 prefetch (gemm_pk.h, PF): several items
+    per workgroup, ragged M/N edges, K slices shorter than the 4-K-tile prefetch window."""
+    torch.manual_seed(13)
+    dy, w, pre = bf(M, K), bf(K, N, scale=0.05), bf(M, N)
+    bg = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+    out = torch.ops.replicann.gemm(dy, w, False, False, None, None, act, pre, None, False, 0, False, None, 9, bg)
+    du = (dy.float() @ w.float()).bfloat16().float()
+    if act == 6:
+        ref = du * pre.float()
+    else:
+        pf = pre.float().requires_grad_()
+        y = F.relu(pf) if act == 3 else F.gelu(pf, approximate="tanh")
+        (ref,) = torch.autograd.grad(y, pf, du)
+    assert rel_err(out, ref) < 1e-2
+    assert rel_err(bg.float(), out.float().sum(0)) < 2e-2
+
+
 def test_gemm_alpha(cuda):
     a, b = bf(300, 128), bf(200, 128)
     alpha = torch.tensor([0.25], device="cuda")
