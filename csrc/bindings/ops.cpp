@@ -90,7 +90,7 @@ int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*
 long rn_bn_ws_floats(int, int);
 int rn_bn_supported(int);
 void rn_bn_fwd(const void*, const void*, const void*, float*, float*, void*, float*, float*, float*, int, int, float,
-               float, int, const void*, const float*, int, hipStream_t);
+               float, int, const void*, const float*, int, void*, hipStream_t);
 void rn_bn_eval(const void*, const void*, const void*, const float*, const float*, void*, int, int, float, int,
                 const void*, hipStream_t);
 void rn_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
@@ -856,7 +856,8 @@ static void check_bn(const Tensor& x, const optional<Tensor>& res) {
         TORCH_CHECK(res->sizes() == x.sizes(), "batchnorm residual shape");
     }
 }
-std::tuple<Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
+// returns (y, mean, rstd, mask): mask = relu'(y) bits, [M·C/8] bytes (empty without relu)
+std::tuple<Tensor, Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
                                                  const Tensor& rmean, const Tensor& rvar, double mom, double eps,
                                                  bool relu, const optional<Tensor>& res,
                                                  const optional<Tensor>& partials) {
@@ -873,10 +874,12 @@ std::tuple<Tensor, Tensor, Tensor> batchnorm_fwd(const Tensor& x, const Tensor& 
     Tensor mean = at::empty({C}, x.options().dtype(at::kFloat));
     Tensor rstd = at::empty({C}, x.options().dtype(at::kFloat));
     Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
+    Tensor mask = at::empty({relu ? (int64_t)M * C / 8 : 0}, x.options().dtype(at::kByte));
     rn_bn_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), y.data_ptr(),
               mean.data_ptr<float>(), rstd.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)mom, (float)eps, relu,
-              optr(res), hp ? partials->data_ptr<float>() : nullptr, hp ? (int)partials->size(0) : 0, cur_stream());
-    return {y, mean, rstd};
+              optr(res), hp ? partials->data_ptr<float>() : nullptr, hp ? (int)partials->size(0) : 0,
+              relu ? mask.data_ptr() : nullptr, cur_stream());
+    return {y, mean, rstd, mask};
 }
 Tensor batchnorm_eval(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& rmean, const Tensor& rvar,
                       double eps, bool relu, const optional<Tensor>& res) {
@@ -886,13 +889,17 @@ Tensor batchnorm_eval(const Tensor& x, const Tensor& w, const Tensor& b, const T
                x.size(0), x.size(1), (float)eps, relu, optr(res), cur_stream());
     return y;
 }
-// returns (dx, dw, db, g') with g' = dy ⊙ relu'(y) (the fused residual's gradient) when want_gres
-std::tuple<Tensor, Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor& x, const Tensor& y,
+// returns (dx, dw, db, g') with g' = dy ⊙ relu'(y) (the fused residual's gradient) when want_gres;
+// mask: batchnorm_fwd's relu'(y) bits (read only with relu)
+std::tuple<Tensor, Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const Tensor& x, const Tensor& mask,
                                                          const Tensor& w, const Tensor& mean, const Tensor& rstd,
                                                          bool relu, bool want_gres, const optional<Tensor>& dw_acc,
                                                          const optional<Tensor>& db_acc) {
     check_bn(gy, c10::nullopt); GUARD(gy);
     const int M = x.size(0), C = x.size(1);
+    if (relu)
+        TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() == (int64_t)M * C / 8 && mask.is_contiguous(),
+                    "batchnorm_bwd: relu needs the forward's [M*C/8] uint8 mask");
     Tensor dx = at::empty_like(x);
     // dw_acc / db_acc: gradient views to ADD into (direct accumulation), both or neither
     const bool acc = dw_acc && dw_acc->defined();
@@ -907,7 +914,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> batchnorm_bwd(const Tensor& gy, const
     Tensor db = acc ? *db_acc : at::empty({C}, x.options());
     Tensor gres = want_gres ? at::empty_like(x) : at::empty({0}, x.options());
     Tensor ws = at::empty({rn_bn_ws_floats(M, C)}, x.options().dtype(at::kFloat));
-    rn_bn_bwd(gy.data_ptr(), x.data_ptr(), y.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+    rn_bn_bwd(gy.data_ptr(), x.data_ptr(), relu ? mask.data_ptr() : nullptr, w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
               dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr<float>(), M, C, relu,
               want_gres ? gres.data_ptr() : nullptr, acc ? 1 : 0, cur_stream());
     return {dx, dw, db, gres};
@@ -1034,10 +1041,10 @@ TORCH_LIBRARY(replicann, m) {
     m.def("avgpool_fwd(Tensor x) -> Tensor");
     m.def("avgpool_bwd(Tensor gy, int H, int W) -> Tensor");
     m.def("batchnorm_fwd(Tensor x, Tensor w, Tensor b, Tensor(a!) rmean, Tensor(b!) rvar, float mom, float eps, bool relu, "
-          "Tensor? res=None, Tensor? partials=None) -> (Tensor, Tensor, Tensor)");
+          "Tensor? res=None, Tensor? partials=None) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("batchnorm_eval(Tensor x, Tensor w, Tensor b, Tensor rmean, Tensor rvar, float eps, bool relu, "
           "Tensor? res=None) -> Tensor");
-    m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor y, Tensor w, Tensor mean, Tensor rstd, bool relu, "
+    m.def("batchnorm_bwd(Tensor gy, Tensor x, Tensor mask, Tensor w, Tensor mean, Tensor rstd, bool relu, "
           "bool want_gres=False, Tensor(c!)? dw_acc=None, Tensor(d!)? db_acc=None) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("fp8_quantize(Tensor x) -> (Tensor, Tensor)");
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");

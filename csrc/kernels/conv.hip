@@ -257,12 +257,14 @@ __global__ void __launch_bounds__(256) avgpool_bwd_k(const bf16* __restrict__ gy
 //   bn_finalize_k turns the forward sums into mean / rstd / running statistics.
 // Apply kernels are 8 channels per thread.  An optional residual input is fused into the forward
 // apply (y = relu(BN(x) + res)); the backward then also returns g' = dy ⊙ relu'(y), the residual
-// branch's gradient.  C % 8 == 0 and C ≤ 2048 (all of ResNet-18).
+// branch's gradient.  With ReLU the training forward also writes relu'(y) as a bit mask (one byte
+// per 8 channels of a row, 1/16 of y's bytes), which both backward passes read instead of y.
+// C % 8 == 0 and C ≤ 2048 (all of ResNet-18).
 constexpr int BN_T = 256;
 
 template <int MODE>
 __global__ void __launch_bounds__(BN_T) bn_part_k(const bf16* __restrict__ a, const bf16* __restrict__ xin,
-                                                  const bf16* __restrict__ yv, const float* __restrict__ mean,
+                                                  const uint8_t* __restrict__ mk, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, float* __restrict__ part, int M,
                                                   int C, int rps, int relu) {
     __shared__ float red[2][BN_T * 8];
@@ -290,10 +292,9 @@ __global__ void __launch_bounds__(BN_T) bn_part_k(const bf16* __restrict__ a, co
                 float xv[8];
                 load8(xin + e, xv);
                 if (relu) {
-                    float yy[8];
-                    load8(yv + e, yy);
+                    const unsigned m = mk[e >> 3];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = yy[j] > 0.f ? v[j] : 0.f;
+                    for (int j = 0; j < 8; ++j) v[j] = ((m >> j) & 1u) ? v[j] : 0.f;
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] += v[j] * (xv[j] - mu[j]) * rs[j]; }
@@ -336,7 +337,8 @@ template <bool EVAL>
 __global__ void __launch_bounds__(256) bn_apply_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const bf16* __restrict__ b, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, const bf16* __restrict__ res,
-                                                  bf16* __restrict__ y, long total8, int C, float eps, int relu) {
+                                                  bf16* __restrict__ y, uint8_t* __restrict__ mk, long total8, int C,
+                                                  float eps, int relu) {
     const int CG = C / 8;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
         const int c0 = (int)(i % CG) * 8;
@@ -354,12 +356,18 @@ __global__ void __launch_bounds__(256) bn_apply_k(const bf16* __restrict__ x, co
             v[j] = relu ? fmaxf(o, 0.f) : o;
         }
         store8(y + i * 8, v);
+        if (mk) {  // relu'(y) of the stored (bf16) values
+            unsigned m = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m |= ((float)(bf16)v[j] > 0.f ? 1u : 0u) << j;
+            mk[i] = (uint8_t)m;
+        }
     }
 }
 
 // dx = w·rstd·(g' − Σg'/M − x̂·Σ(g'x̂)/M), g' = dy ⊙ relu'(y); optionally g' itself (residual branch)
 __global__ void __launch_bounds__(256) bn_bwd_apply_k(const bf16* __restrict__ gy, const bf16* __restrict__ x,
-                                                      const bf16* __restrict__ yv, const bf16* __restrict__ w,
+                                                      const uint8_t* __restrict__ mk, const bf16* __restrict__ w,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       const float* __restrict__ sums, bf16* __restrict__ dx,
                                                       bf16* __restrict__ gres, long total8, int C, int M, int relu) {
@@ -372,10 +380,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const bf16* __restrict__ g
         load8(x + i * 8, xv);
         load8(w + c0, wf);
         if (relu) {
-            float yy[8];
-            load8(yv + i * 8, yy);
+            const unsigned m = mk[i];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+            for (int j = 0; j < 8; ++j) g[j] = ((m >> j) & 1u) ? g[j] : 0.f;
         }
         if (gres) store8(gres + i * 8, g);
         float o[8];
@@ -457,7 +464,7 @@ void rn_avgpool_bwd(const void* gy, void* dx, int N, int HW, int C, hipStream_t 
 // workspace floats: partials [S][2C] + reduced sums [2C] + the column reduction's scratch
 long rn_bn_ws_floats(int M, int C) { return 2L * C * (bn_splits(M) + 1) + (long)RN_COLRED_S * 2 * C; }
 
-static void bn_stats(int mode, const void* a, const void* xin, const void* yv, const float* mean, const float* rstd,
+static void bn_stats(int mode, const void* a, const void* xin, const uint8_t* mk, const float* mean, const float* rstd,
                      float* ws, int M, int C, int relu, void* db16, void* dw16, hipStream_t st, int accum16 = 0) {
     const int S = bn_splits(M);
     const int rps = (M + S - 1) / S;
@@ -467,7 +474,7 @@ static void bn_stats(int mode, const void* a, const void* xin, const void* yv, c
     if (mode == 0)
         bn_part_k<0><<<S, BN_T, 0, st>>>((const bf16*)a, nullptr, nullptr, nullptr, nullptr, part, M, C, rps, 0);
     else
-        bn_part_k<1><<<S, BN_T, 0, st>>>((const bf16*)a, (const bf16*)xin, (const bf16*)yv, mean, rstd, part, M, C,
+        bn_part_k<1><<<S, BN_T, 0, st>>>((const bf16*)a, (const bf16*)xin, mk, mean, rstd, part, M, C,
                                          rps, relu);
     const int a16 = accum16 ? 2 : 0;  // direct gradient accumulation: add into db16/dw16, never into sums
     RnColOut o{{sums, sums + C, nullptr}, {(__bf16*)db16, (__bf16*)dw16, nullptr}, C, {a16, a16, 0}};
@@ -478,10 +485,10 @@ int rn_bn_supported(int C) { return C % 8 == 0 && C <= 2048; }
 
 // res (optional): y = relu(BN(x) + res).  partials (optional): [prows][2C] Σx | Σx² row-block partials
 // from x's producer (the implicit-conv GEMM epilogue): only their fixed-order column reduction runs,
-// not a statistics pass over x.
+// not a statistics pass over x.  mask (optional, with relu): [M·C/8] bytes of relu'(y) bits.
 void rn_bn_fwd(const void* x, const void* w, const void* b, float* rmean, float* rvar, void* y, float* mean,
                float* rstd, float* ws, int M, int C, float mom, float eps, int relu, const void* res,
-               const float* partials, int prows, hipStream_t st) {
+               const float* partials, int prows, void* mask, hipStream_t st) {
     if (partials) {
         float* sums = ws + 2L * C * bn_splits(M);
         RnColOut o{{sums, sums + C, nullptr}, {nullptr, nullptr, nullptr}, C, {0, 0, 0}};
@@ -493,26 +500,27 @@ void rn_bn_fwd(const void* x, const void* w, const void* b, float* rmean, float*
     bn_finalize_k<<<(C + 255) / 256, 256, 0, st>>>(sums, C, M, eps, mom, mean, rstd, rmean, rvar);
     const long t8 = (long)M * C / 8;
     bn_apply_k<false><<<gridn(t8), 256, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)b, mean, rstd,
-                                                  (const bf16*)res, (bf16*)y, t8, C, eps, relu);
+                                                  (const bf16*)res, (bf16*)y, relu ? (uint8_t*)mask : nullptr, t8,
+                                                  C, eps, relu);
 }
 
 void rn_bn_eval(const void* x, const void* w, const void* b, const float* rmean, const float* rvar, void* y, int M,
                 int C, float eps, int relu, const void* res, hipStream_t st) {
     const long t8 = (long)M * C / 8;
     bn_apply_k<true><<<gridn(t8), 256, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)b, rmean, rvar,
-                                                 (const bf16*)res, (bf16*)y, t8, C, eps, relu);
+                                                 (const bf16*)res, (bf16*)y, nullptr, t8, C, eps, relu);
 }
 
 // dw/db: bf16 outputs [C] (the parameter dtype, written by the reduction itself; with `accum` ADDED
 // into them: the flat gradient buffer's views, no AccumulateGrad pass); gres (optional):
-// dy ⊙ relu'(y), the gradient of a fused residual input
-void rn_bn_bwd(const void* gy, const void* x, const void* y, const void* w, const float* mean, const float* rstd,
+// dy ⊙ relu'(y), the gradient of a fused residual input; mask: the forward's relu'(y) bits (relu only)
+void rn_bn_bwd(const void* gy, const void* x, const void* mask, const void* w, const float* mean, const float* rstd,
                void* dx, void* dw, void* db, float* ws, int M, int C, int relu, void* gres, int accum,
                hipStream_t st) {
-    bn_stats(1, gy, x, y, mean, rstd, ws, M, C, relu, db, dw, st, accum);
+    bn_stats(1, gy, x, (const uint8_t*)mask, mean, rstd, ws, M, C, relu, db, dw, st, accum);
     const float* sums = ws + 2L * C * bn_splits(M);
     const long t8 = (long)M * C / 8;
-    bn_bwd_apply_k<<<gridn(t8), 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const bf16*)y, (const bf16*)w, mean,
+    bn_bwd_apply_k<<<gridn(t8), 256, 0, st>>>((const bf16*)gy, (const bf16*)x, (const uint8_t*)mask, (const bf16*)w, mean,
                                                rstd, sums, (bf16*)dx, (bf16*)gres, t8, C, M, relu);
 }
 

@@ -77,11 +77,14 @@ __global__ void __launch_bounds__(256) emb_finish_k(const int64_t* __restrict__ 
 }
 
 // Deterministic variant (REPLICANN_DETERMINISTIC=1): the same owner scheme, but the scratch
-// accumulates 64-bit FIXED-POINT values (x · 2^32, exact for a bf16 input) with integer atomics,
-// whose sum does not depend on the order the rows arrive in — unlike fp32 atomics.  Range ±2^31
-// per element, resolution 2^-32 (far below a bf16 ulp of any gradient that survives the final
-// bf16 add); twice the scratch bytes and atomic traffic of the fp32 path.
-constexpr float FX_SCALE = 4294967296.f;  // 2^32
+// accumulates 64-bit FIXED-POINT values (round(x · 2^40)) with integer atomics, whose sum does not
+// depend on the order the rows arrive in — unlike fp32 atomics.  Each contribution is rounded to the
+// nearest 2^-40 ≈ 9.1e-13 (a bf16 input is NOT represented exactly: values below 2^-41 in magnitude
+// vanish), so a per-token gradient of 1e-8 (e.g. a 1/(B·T·grad_accum) loss scale) keeps ≈ 1e-4
+// relative precision; the per-element range is |Σ| < 2^23 (int64 / 2^40), far above any embedding
+// gradient.  Twice the scratch bytes and atomic traffic of the fp32 path
+// (tests/test_determinism_gpu.py::test_embedding_scatter_deterministic_tiny_gradients).
+constexpr float FX_SCALE = 1099511627776.f;  // 2^40
 
 __global__ void __launch_bounds__(256) emb_scatter_own_fx_k(const int64_t* __restrict__ ids,
                                                             const bf16* __restrict__ dx,
@@ -112,7 +115,7 @@ __global__ void __launch_bounds__(256) emb_finish_fx_k(const int64_t* __restrict
         const long long v = (long long)d64[id * E + c];
         d64[id * E + c] = 0ull;
         bf16* q = g + id * E + c;
-        q[0] = (bf16)((float)q[0] + (float)((double)v * (1.0 / 4294967296.0)));
+        q[0] = (bf16)((float)q[0] + (float)((double)v * (1.0 / 1099511627776.0)));
     }
     if (lane == 0) owner[id] = 0xFFFFFFFFu;
 }

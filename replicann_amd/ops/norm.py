@@ -124,9 +124,10 @@ class _BatchNormFn(torch.autograd.Function):
             part = None
         if part is not None and getattr(x, "_rn_bn_version", -1) != x._version:
             part = None  # x was modified in place after the conv: recompute the statistics
-        y, mean, rstd = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
-                                                 momentum, eps, relu, r2, part)
-        ctx.save_for_backward(x2, y, weight, bias, mean, rstd)
+        # mask: relu'(y) as bits (1/16 of y's bytes) — all the backward needs of y
+        y, mean, rstd, mask = _ext.ops().batchnorm_fwd(x2, weight, bias, running_mean, running_var,
+                                                       momentum, eps, relu, r2, part)
+        ctx.save_for_backward(x2, mask, weight, bias, mean, rstd)
         ctx.params = (weight, bias)  # the Parameters themselves (direct gradient accumulation)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -136,13 +137,13 @@ class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         from .linear import _direct_grad, _notify
-        x2, y, weight, bias, mean, rstd = ctx.saved_tensors
+        x2, mask, weight, bias, mean, rstd = ctx.saved_tensors
         C = ctx.shp[-1]
         pw, pb = ctx.params
         dw_acc, db_acc = _direct_grad(pw), _direct_grad(pb)
         direct = (dw_acc is not None and db_acc is not None and dw_acc.dtype == torch.bfloat16
                   and db_acc.dtype == torch.bfloat16)
-        dx, dw, db, gres = _ext.ops().batchnorm_bwd(gy.reshape(-1, C).contiguous(), x2, y, weight, mean,
+        dx, dw, db, gres = _ext.ops().batchnorm_bwd(gy.reshape(-1, C).contiguous(), x2, mask, weight, mean,
                                                     rstd, ctx.relu, ctx.has_res,
                                                     dw_acc if direct else None, db_acc if direct else None)
         gr = gres.reshape(ctx.shp) if ctx.has_res else None

@@ -34,16 +34,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("B", type=int, nargs="?", default=64)
     ap.add_argument("--fwd", default="1,2")
-    ap.add_argument("--bwd", default="1")
+    ap.add_argument("--bwd", default="2", help="REPLICANN_ATTN_DQ values (1 or 2 query groups per wave in the dQ kernel)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--D", type=int, default=64, help="head size (H = 768 // D keeps E = 768)")
+    ap.add_argument("--noncausal", action="store_true")
     a = ap.parse_args()
     B, T, D = a.B, 1024, a.D
     H = 768 // D
     torch.manual_seed(0)
     qkv = torch.randn(B, T, 3, H, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
     go = torch.randn(B, T, H, D, device="cuda", dtype=torch.bfloat16)
-    fl_f = 4 * B * H * T * T * D / 2
+    fl_f = 4 * B * H * T * T * D / (1 if a.noncausal else 2)
     fv = [int(x) for x in a.fwd.split(",") if x]
     bv = [int(x) for x in a.bwd.split(",") if x]
     ref_o = ref_g = None
@@ -51,7 +52,7 @@ def main():
     for rnd in range(a.rounds):
         for v in fv:
             os.environ["REPLICANN_ATTN_FWD"] = str(v)
-            f = lambda: ops.attention_packed(qkv, causal=True)
+            f = lambda: ops.attention_packed(qkv, causal=not a.noncausal)
             t = timeit(f)
             o = f().detach()
             if ref_o is None:
@@ -59,9 +60,9 @@ def main():
             err = (o.float() - ref_o.float()).abs().max().item()
             res.setdefault(("fwd", v), []).append((t, err))
         os.environ["REPLICANN_ATTN_FWD"] = "1"
-        out = ops.attention_packed(qkv, causal=True)
+        out = ops.attention_packed(qkv, causal=not a.noncausal)
         for v in bv:
-            os.environ["REPLICANN_ATTN_BWD"] = str(v)
+            os.environ["REPLICANN_ATTN_DQ"] = str(v)
             f = lambda: torch.autograd.grad(out, qkv, go, retain_graph=True)[0]
             t = timeit(f)
             gq = f()
