@@ -31,7 +31,18 @@ def load_committed(model: str) -> int:
 
     from .. import _ext
 
-    text = p.read_text()
-    json.loads(text)  # malformed file: fail loudly here, not as a silent partial parse in C++
+    rows = json.loads(p.read_text())  # malformed file: fail loudly here, not as a silent partial parse
     _ext.ops()
-    return int(torch.ops.replicann.gemm_tuning_load(text))
+    n = int(torch.ops.replicann.gemm_tuning_load(canonical(rows)))
+    if n != len(rows):
+        raise RuntimeError(f"{p}: the native loader took {n} of {len(rows)} entries")
+    return n
+
+
+KEYS = ("M", "N", "K", "ta", "tb", "act", "f32", "as", "epi", "cfg", "split")
+
+
+def canonical(rows) -> str:
+    """The exact compact form gemm_tuning_table() emits and gemm_tuning_load() parses (key order
+    M, N, K, ta, tb, act, f32, as, epi, cfg, split; no spaces)."""
+    return json.dumps([{k: int(r[k]) for k in KEYS} for r in rows], separators=(",", ":"))

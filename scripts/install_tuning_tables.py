@@ -6,6 +6,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from replicann_amd.tuning import KEYS, canonical  # noqa: E402
 MODELS = ["gpt2-small", "gpt2-medium", "gpt2-medium-fp8", "vit-b16", "resnet18"]
 
 
@@ -16,9 +18,10 @@ def main():
         if not src.exists():
             print(f"missing {src}", file=sys.stderr)
             continue
-        rows = sorted(json.loads(src.read_text()), key=lambda r: json.dumps(r, sort_keys=True))
+        rows = json.loads(canonical(json.loads(src.read_text())))
+        rows.sort(key=lambda r: tuple(r[k] for k in KEYS))
         dst = ROOT / "replicann_amd" / "tuning" / f"gemm_{m}.json"
-        dst.write_text("[\n" + ",\n".join(json.dumps(r, sort_keys=True) for r in rows) + "\n]\n")
+        dst.write_text("[\n" + ",\n".join(canonical([r])[1:-1] for r in rows) + "\n]\n")
         print(f"{dst.name}: {len(rows)} shapes")
         n += 1
     return 0 if n else 1

@@ -24,3 +24,20 @@ def test_tuning_table_round_trip():
     e2 = dict(entries[1], cfg=1)
     assert torch.ops.replicann.gemm_tuning_load(json.dumps([e2], separators=(",", ":"))) == 1
     assert e2 in json.loads(torch.ops.replicann.gemm_tuning_table())
+
+
+@pytest.mark.skipif(not SO.exists(), reason="extension not built")
+def test_committed_tables_load_completely():
+    """Every committed per-model table (replicann_amd/tuning/gemm_<model>.json) is loaded entry for
+    entry by the native loader (load_committed raises on a partial parse)."""
+    from replicann_amd import tuning
+
+    torch.ops.load_library(str(SO))
+    models = [p.stem[len("gemm_"):] for p in tuning.DIR.glob("gemm_*.json")]
+    assert {"gpt2-small", "gpt2-medium", "gpt2-medium-fp8", "vit-b16", "resnet18"} <= set(models)
+    for m in models:
+        rows = json.loads(tuning.table_path(m).read_text())
+        assert rows and tuning.load_committed(m) == len(rows)
+        table = json.loads(torch.ops.replicann.gemm_tuning_table())
+        for r in rows:
+            assert {k: r[k] for k in tuning.KEYS} in table
