@@ -1,0 +1,6 @@
+#!/bin/bash
+# round 3: the full GPU test tier (as the driver runs it) + smoke
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -15 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2
