@@ -35,7 +35,7 @@ int rn_bias_act_grad_splits(int, int);
 int rn_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
               hipStream_t, void*, float*);
 void rn_fp8_roll(float*, hipStream_t);
-void rn_fp8_quant_many(const void*, const long*, int, long, void*, hipStream_t);
+void rn_fp8_quant_many(const void*, const long*, int, long, void*, int, hipStream_t);
 int rn_ln_bwd_waves(int);
 long rn_ln_bwd_ws(int, int);
 int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
@@ -981,13 +981,13 @@ std::tuple<Tensor, Tensor> gemm_fp8_q8(const Tensor& a8, const Tensor& b8, const
 }
 
 // e4m3 copies of many weights of one flat bf16 parameter buffer, two launches (see fp8.hip)
-void fp8_quant_many(const Tensor& flat, const Tensor& segs, int64_t max_n, const Tensor& qbuf) {
+void fp8_quant_many(const Tensor& flat, const Tensor& segs, int64_t max_n, const Tensor& qbuf, bool roll) {
     CHECK_BF16(flat); GUARD(flat);
     TORCH_CHECK(segs.scalar_type() == at::kLong && segs.is_cuda() && segs.dim() == 2 && segs.size(1) == 4 &&
                 segs.is_contiguous());
     TORCH_CHECK(qbuf.scalar_type() == at::kByte && qbuf.is_cuda());
     rn_fp8_quant_many(flat.data_ptr(), segs.data_ptr<int64_t>(), (int)segs.size(0), (long)max_n, qbuf.data_ptr(),
-                      cur_stream());
+                      roll ? 1 : 0, cur_stream());
 }
 
 int64_t native_version() { return 1; }
@@ -1051,7 +1051,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("gemm_fp8_q8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, int act, Tensor(a!) preact, Tensor(b!) q8_state) -> (Tensor, Tensor)");
-    m.def("fp8_quant_many(Tensor flat, Tensor segs, int max_n, Tensor(a!) qbuf) -> ()");
+    m.def("fp8_quant_many(Tensor flat, Tensor segs, int max_n, Tensor(a!) qbuf, bool roll=True) -> ()");
     m.def("native_version() -> int");
     m.def("gemm_tuning_table() -> str");
     m.def("gemm_tuning_load(str table) -> int");

@@ -91,24 +91,33 @@ RN_DEV float hash_uniform(uint64_t seed, uint64_t idx) {
 //   0.5·x·(1 + tanh(u)) = x·σ(2u),  u = √(2/π)(x + 0.044715x³)
 // → one v_exp_f32 + one v_rcp_f32 per element (no libm tanhf).
 RN_DEV float fast_sigmoid(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
-RN_DEV float gelu_f(float x) {
-    const float c2 = 2.f * 0.7978845608028654f;
-    return x * fast_sigmoid(c2 * (x + 0.044715f * x * x * x));
+// s = σ(2u) with the constants folded into the exp2 argument: 2u·log2e = x·(B + A·x²), so the
+// argument is one FMA + one multiply and exp2 is the raw v_exp_f32 (its argument range is the
+// whole line, but σ saturates correctly: exp2(+big) = inf → rcp(inf) = 0, exp2(-big) = 0 → 1).
+RN_DEV float gelu_sig(float x, float x2) {
+    constexpr float c = 0.7978845608028654f, L2E = 1.4426950408889634f;
+    constexpr float B = -2.f * c * L2E, A = -2.f * c * 0.044715f * L2E;
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * __builtin_fmaf(x2, A, B)));
+}
+RN_DEV float gelu_f(float x) { return x * gelu_sig(x, x * x); }
+// d/dx x·σ(2u) = s + s(1-s)·k,  k = 2x·u'(x)/… = x·(2c + 2c·3·0.044715·x²)  →  d = s·(1 + (1-s)·k)
+RN_DEV float gelu_dk(float x, float x2) {
+    constexpr float c = 0.7978845608028654f;
+    return x * __builtin_fmaf(x2, 2.f * c * 0.134145f, 2.f * c);
 }
 RN_DEV float gelu_grad_f(float x) {
-    const float c = 0.7978845608028654f;
     const float x2 = x * x;
-    const float s = fast_sigmoid(2.f * c * (x + 0.044715f * x2 * x));
-    // d/dx = s + 2·x·s·(1-s)·c·(1 + 3·0.044715·x²)
-    return s + 2.f * x * s * (1.f - s) * c * (1.f + 0.134145f * x2);
+    const float s = gelu_sig(x, x2);
+    const float k = gelu_dk(x, x2);
+    return __builtin_fmaf(s, __builtin_fmaf(-s, k, k), s);
 }
 
 // gelu(x) and gelu'(x) sharing one exp + rcp
 RN_DEV float gelu_and_grad_f(float x, float& d) {
-    const float c = 0.7978845608028654f;
     const float x2 = x * x;
-    const float s = fast_sigmoid(2.f * c * (x + 0.044715f * x2 * x));
-    d = s + 2.f * x * s * (1.f - s) * c * (1.f + 0.134145f * x2);
+    const float s = gelu_sig(x, x2);
+    const float k = gelu_dk(x, x2);
+    d = __builtin_fmaf(s, __builtin_fmaf(-s, k, k), s);
     return x * s;
 }
 

@@ -185,9 +185,12 @@ void rn_fp8_quantize_delayed(const void* x, long n, void* q, float* state, hipSt
 }
 
 // Re-quantise every cached fp8 weight (segs: device int64 [nseg][4], see fp8_quant_many_k).
-void rn_fp8_quant_many(const void* flat, const long* segs, int nseg, long max_n, void* qbuf, hipStream_t st) {
+// roll = 0: keep the scales already in the slots (rebuilding the cache after a checkpoint load: the
+// bytes and the recorded amax are then exactly those of the saving run's last refresh).
+void rn_fp8_quant_many(const void* flat, const long* segs, int nseg, long max_n, void* qbuf, int roll,
+                       hipStream_t st) {
     if (nseg <= 0) return;
-    fp8_roll_many_k<<<(nseg + 255) / 256, 256, 0, st>>>(segs, nseg);
+    if (roll) fp8_roll_many_k<<<(nseg + 255) / 256, 256, 0, st>>>(segs, nseg);
     long per = (max_n / 8 + 255) / 256;  // blocks that cover the largest weight in one sweep
     const int bx = (int)(per < 1 ? 1 : (per > 64 ? 64 : per));
     fp8_quant_many_k<<<dim3(bx, nseg), 256, 0, st>>>((const bf16*)flat, segs, (uint8_t*)qbuf);

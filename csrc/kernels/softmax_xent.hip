@@ -230,17 +230,30 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
         }
     }
     const float mL = (m == -INFINITY) ? 0.f : m * L2E;
+    const float m_own = m;
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
         const int i = threadIdx.x + k * 1024;
         if (i < n8) {
             bf16x8 e;
+            // raw v_exp_f32 (arguments <= 0: no overflow; results below 2^-126 flush to 0, which the
+            // bf16 e could not hold anyway) -- exp2f's denormal range reduction was 4 extra VALU per
+            // element; the padded-column mask only in the one chunk that straddles nvalid
+            if (i * 8 + 8 <= nvalid) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float x = (i * 8 + j < nvalid) ? exp2f(fmaf((float)v[k][j], L2E, -mL)) : 0.f;
-                s += x;
-                e[j] = (bf16)x;
+                for (int j = 0; j < 8; ++j) {
+                    const float x = __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -mL));
+                    s += x;
+                    e[j] = (bf16)x;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float x = (i * 8 + j < nvalid) ? __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -mL)) : 0.f;
+                    s += x;
+                    e[j] = (bf16)x;
+                }
             }
             v[k] = e;
         }
@@ -250,7 +263,7 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
     for (int o = 32; o > 0; o >>= 1) {
         const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
         const float M = fmaxf(m, m2);
-        s = (M == -INFINITY) ? 0.f : s * exp2f((m - M) * L2E) + s2 * exp2f((m2 - M) * L2E);
+        s = (M == -INFINITY) ? 0.f : s * __builtin_amdgcn_exp2f((m - M) * L2E) + s2 * __builtin_amdgcn_exp2f((m2 - M) * L2E);
         m = M;
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -264,14 +277,15 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
     for (int w = 0; w < 16; ++w) M = fmaxf(M, sm_m[w]);
     float S = 0.f;
 #pragma unroll
-    for (int w = 0; w < 16; ++w) S += sm_s[w] * exp2f((sm_m[w] - M) * L2E);
+    for (int w = 0; w < 16; ++w) S += sm_s[w] * __builtin_amdgcn_exp2f((sm_m[w] - M) * L2E);
     const float lse = M + __logf(S);
     if (threadIdx.x == 0) {
         lse_out[blockIdx.x] = lse;
         loss[blockIdx.x] = ign ? 0.f : lse - xt;
     }
     // this thread's e values were taken relative to ITS local max (mL): rescale to the row's lse
-    const float f = ign ? 0.f : exp2f(mL - lse * L2E);
+    // (a thread without a valid column has e = 0 and m = -inf: f = 0, never 0 · inf)
+    const float f = (ign || m_own == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(mL - lse * L2E);
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
         const int i = threadIdx.x + k * 1024;
@@ -279,9 +293,14 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
             float g[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) g[j] = (float)v[k][j] * f;
-            if (!ign && t >= (long)i * 8 && t < (long)i * 8 + 8) g[t - (long)i * 8] -= 1.f;
             store8(row + i * 8, g);
         }
+    }
+    // the one-hot term: the thread that owns column t rewrites it (a runtime index into g[] was a
+    // compare + select per element); its e is recomputed bit-identically from xt
+    if (!ign && threadIdx.x == (int)((t >> 3) & 1023)) {
+        const float et = (float)(bf16)__builtin_amdgcn_exp2f(fmaf(xt, L2E, -mL));
+        row[t] = (bf16)(et * f - 1.f);
     }
 }
 

@@ -222,6 +222,22 @@ class Fp8WeightCache:
         for w, st, _, _ in self.entries:
             self.version[id(st)] = w._version
 
+    def rebuild(self):
+        """Re-create every cached e4m3 weight from the current bf16 weights WITHOUT rolling the
+        delayed scales: the scales in the slots are the ones the last refresh used, so after a
+        checkpoint load (weights and fp8 state slots restored together) the cache holds exactly the
+        bytes the saving run's last refresh wrote and a resumed run continues bit for bit."""
+        if not self.entries or not _ext.use_native(self.flat.data):
+            return
+        if (self.segs is None or any(st.t is None for _, st, _, _ in self.entries)
+                or [st.t.data_ptr() for _, st, _, _ in self.entries] != self._slot_ptrs):
+            self._ensure_states()
+        if not all(st.ready[1] for _, st, _, _ in self.entries):
+            return  # no scale yet (fresh run): the first forward seeds them, the next step refreshes
+        _ext.ops().fp8_quant_many(self.flat.data, self.segs, self.max_n, self.qbuf, False)
+        for w, st, _, _ in self.entries:
+            self.version[id(st)] = w._version
+
     def lookup(self, st, w):
         """The cached e4m3 weight of ``st`` if it is current for ``w``, else None."""
         v = self.version.get(id(st))

@@ -169,7 +169,10 @@ class FusedAdamW(_FlatOptimizer):
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         self.lr = sd.get("lr", self.lr)
-        self.flat.data.copy_(self.master)
+        # the parameters themselves are NOT re-derived from the fp32 master: the model state_dict
+        # carries the exact (stochastically rounded) bf16 copy the saving run used, and a
+        # round-to-nearest master -> bf16 copy here made a resumed GPU run diverge from the
+        # uninterrupted one at its first forward
 
 
 class FusedSGD(_FlatOptimizer):
@@ -220,8 +223,7 @@ class FusedSGD(_FlatOptimizer):
         self.step_count = sd["step"]
         self.norm_buf[2] = float(self.step_count)
         self.master.copy_(sd["master"])
-        self.buf.copy_(sd["buf"])
-        self.flat.data.copy_(self.master)
+        self.buf.copy_(sd["buf"])  # parameters: from the model state_dict (see FusedAdamW)
 
 
 def cosine_lr(step, base_lr, warmup, total, min_ratio=0.1):

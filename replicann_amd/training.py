@@ -146,6 +146,11 @@ class Trainer:
         self._resume_state = None
         if cfg.resume:
             self.step_idx, _, self._resume_state = load_checkpoint(cfg.resume, self.model, self.opt)
+            tun = ((self._resume_state or {}).get("extra") or {}).get("gemm_tuning")
+            if tun and self.device.type == "cuda":
+                torch.ops.replicann.gemm_tuning_load(tun)
+            if self.fp8_cache is not None:  # the saved run's e4m3 weights, same scales (no roll)
+                self.fp8_cache.rebuild()
             if self.ddp is not None:
                 self.ddp._broadcast_state()
         self.data = self._make_data()
@@ -343,9 +348,12 @@ class Trainer:
         return loss
 
     def save(self, path):
-        """Checkpoint (collective under DDP): model, optimizer, step, config, and every rank's RNG
-        states and data cursor."""
-        save_checkpoint(path, self.model, self.opt, self.step_idx, asdict(self.cfg), data=self.data)
+        """Checkpoint (collective under DDP): model, optimizer, step, config, every rank's RNG
+        states and data cursor, and (GPU) the GEMM autotuner's per-shape kernel picks."""
+        extra = None
+        if self.device.type == "cuda":  # the GEMM kernel picks: a resumed process runs the same kernels
+            extra = {"gemm_tuning": torch.ops.replicann.gemm_tuning_table()}
+        save_checkpoint(path, self.model, self.opt, self.step_idx, asdict(self.cfg), extra=extra, data=self.data)
 
     def lr_at(self, i):
         c = self.cfg

@@ -94,6 +94,8 @@ def load_checkpoint(path, model, optimizer=None, strict=True, map_location="cpu"
         warnings.warn(msg + "; restoring model/optimizer state only, per-rank streams start fresh")
         return sd.get("step", 0), sd.get("config", {}), None
     mine = ranks[r] if r < len(ranks) else None
+    if mine is not None and sd.get("extra"):
+        mine = dict(mine, extra=sd["extra"])
     if restore_rng:
         cpu = mine["rng_cpu"] if mine is not None else sd.get("rng_cpu")
         if cpu is not None:
