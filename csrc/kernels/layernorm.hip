@@ -40,22 +40,45 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const bf16* __restrict__ x, cons
             if constexpr (BIAS) bv[i] = *reinterpret_cast<const bf16x8*>(b + c * 8);
         }
     }
-    for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
-        const bf16* xr = x + (long)row * E;
+    // grid-strided rows with a one-row software prefetch: the next row's x (and r) loads are in
+    // flight while this row is reduced, normalised and stored (one HBM round trip per row was the
+    // limiter of the one-row-per-wave version: ~4.6 TB/s)
+    const int rstride = gridDim.x * 4;
+    bf16x8 xn[NV];
+    [[maybe_unused]] bf16x8 rn[NV];
+    auto fetch = [&](int rr) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int c = lane + i * 64;
+            if (c < nvec) {
+                xn[i] = *reinterpret_cast<const bf16x8*>(x + (long)rr * E + c * 8);
+                if constexpr (RES) rn[i] = *reinterpret_cast<const bf16x8*>(r + (long)rr * E + c * 8);
+            }
+        }
+    };
+    int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row < M) fetch(row);
+    for (; row < M; row += rstride) {
         float v[NV][8];
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             int c = (lane + i * 64);
             if (c < nvec) {
-                load8(xr + c * 8, v[i]);
-                if constexpr (RES) {
-                    float t[8];
-                    load8(r + (long)row * E + c * 8, t);
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[i][j] += t[j];
-                    store8(hout + (long)row * E + c * 8, v[i]);
+                for (int j = 0; j < 8; ++j) v[i][j] = (float)xn[i][j];
+                if constexpr (RES) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[i][j] += (float)rn[i][j];
                 }
+            }
+        }
+        if (row + rstride < M) fetch(row + rstride);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            int c = (lane + i * 64);
+            if (c < nvec) {
+                if constexpr (RES) store8(hout + (long)row * E + c * 8, v[i]);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) s += v[i][j];
             }
@@ -138,35 +161,53 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
         }
         if (c < nvec) load8(w + c * 8, wf[i]);
     }
-    for (int row = wave; row < M; row += nwaves) {
-        const float mu = mean[row], rs = rstd[row];
-        float xh[NV][8], g[NV][8];
-        float s1 = 0.f, s2 = 0.f;
-        // the residual-gradient operand is loaded with h and dy, not after the two row reductions:
-        // one memory round trip per row instead of two
-        [[maybe_unused]] bf16x8 ghv[NV];
-        if constexpr (GH) {
+    // one-row software prefetch (as the forward): the next row's dy / h / gh loads and its mean /
+    // rstd are in flight while this row is reduced and dx stored
+    bf16x8 hn[NV], dn[NV];
+    [[maybe_unused]] bf16x8 gn[NV];
+    float mun = 0.f, rsn = 0.f;
+    auto fetch = [&](int rr) {
+        mun = mean[rr];
+        rsn = rstd[rr];
 #pragma unroll
-            for (int i = 0; i < NV; ++i) {
-                int c = lane + i * 64;
-                if (c < nvec) ghv[i] = *reinterpret_cast<const bf16x8*>(gh + (long)row * E + c * 8);
+        for (int i = 0; i < NV; ++i) {
+            const int c = lane + i * 64;
+            if (c < nvec) {
+                if constexpr (GH) gn[i] = *reinterpret_cast<const bf16x8*>(gh + (long)rr * E + c * 8);
+                hn[i] = *reinterpret_cast<const bf16x8*>(h + (long)rr * E + c * 8);
+                dn[i] = *reinterpret_cast<const bf16x8*>(dy + (long)rr * E + c * 8);
             }
         }
+    };
+    if (wave < M) fetch(wave);
+    for (int row = wave; row < M; row += nwaves) {
+        const float mu = mun, rs = rsn;
+        float xh[NV][8], g[NV][8];
+        float s1 = 0.f, s2 = 0.f;
+        [[maybe_unused]] bf16x8 ghv[NV];
+        float d[NV][8];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            if constexpr (GH) ghv[i] = gn[i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                xh[i][j] = (float)hn[i][j];
+                d[i][j] = (float)dn[i][j];
+            }
+        }
+        if (row + nwaves < M) fetch(row + nwaves);
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             int c = lane + i * 64;
             if (c < nvec) {
-                float d[8];
-                load8(h + (long)row * E + c * 8, xh[i]);
-                load8(dy + (long)row * E + c * 8, d);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     xh[i][j] = (xh[i][j] - mu) * rs;
-                    g[i][j] = d[j] * wf[i][j];
+                    g[i][j] = d[i][j] * wf[i][j];
                     s1 += g[i][j];
                     s2 += g[i][j] * xh[i][j];
-                    acc[0][i][j] += d[j] * xh[i][j];
-                    acc[1][i][j] += d[j];
+                    acc[0][i][j] += d[i][j] * xh[i][j];
+                    acc[1][i][j] += d[i][j];
                 }
             }
         }
@@ -247,7 +288,8 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
 #undef RN_LNF
         return 0;
     }
-    dim3 grid((M + 3) / 4);
+    // 2048 blocks = 8192 waves (32 per CU): each wave walks M / 8192 rows with the prefetch
+    dim3 grid((M + 3) / 4 < 2048 ? (M + 3) / 4 : 2048);
 #define RN_LNF(NV, R, B) ln_fwd_k<NV, R, B><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)r, (const bf16*)w, (const bf16*)b, (bf16*)y, (bf16*)h, mean, rstd, M, E, eps)
 #define RN_LNF2(NV) { if (r) { if (b) RN_LNF(NV, true, true); else RN_LNF(NV, true, false); } \
                       else { if (b) RN_LNF(NV, false, true); else RN_LNF(NV, false, false); } }
