@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
             for (int t = 0; t < 8; ++t) bias[nh][t] = 0.f;
-        if (!SPLIT && p.bias) {
+        if (!SPLIT && !act_bwd(ACT) && p.bias) {  // (activation-backward epilogues never take a bias)
 #pragma unroll
             for (int nh = 0; nh < 2; ++nh) {
                 const int cb = n0 + nh * 128 + wc * 32;
@@ -476,7 +476,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                                  : (act_bwd(ACT) ? p.pre : (p.res ? p.res : ((p.accumulate && !F32) ? (const bf16*)p.C : nullptr)));
         // (loaded one 128-row half at a time: 32 VGPRs, all 8 loads of a half in flight together;
         // both halves at once spill: the kernel is at the 256-VGPR limit)
-        u32x4 aux[4][2];
+        // activation-backward epilogues (no bias, no pre-activation store) load BOTH halves up front:
+        // one exposed load round trip per tile instead of two
+        constexpr bool AUX2 = act_bwd(ACT) && !SPLIT && !F32;
+        u32x4 aux[AUX2 ? 2 : 1][4][2];
         const __amdgpu_buffer_rsrc_t ars = pk_rsrc(auxp ? auxp + (long)m0 * p.ldc + n0 : nullptr, 0x7FFFFFF0u);
         const u32x4 prs = pk_rsrc_u(act_fwd(ACT) && p.pre ? (void*)(p.pre + (long)m0 * p.ldc + n0) : nullptr,
                                     act_fwd(ACT) && p.pre ? 0x7FFFFFF0u : 0u);
@@ -487,15 +490,17 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             for (int t = 0; t < 8; ++t) csum[nh][t] = 0.f;
 #pragma unroll
         for (int mh = 0; mh < 2; ++mh) {
-            if (auxp) {
+            if (auxp && (!AUX2 || mh == 0)) {
+#pragma unroll
+                for (int ah = 0; ah < (AUX2 ? 2 : 1); ++ah)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int nh = 0; nh < 2; ++nh) {
 #ifdef RN_PK_NO_AUX  // A/B only: no aux traffic and no wait (wrong outputs)
-                        aux[i][nh] = (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+                        aux[ah][i][nh] = (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
 #else
-                        aux[i][nh] = __builtin_amdgcn_raw_buffer_load_b128(ars, off(mh, i, nh, 2), 0, 0);
+                        aux[ah][i][nh] = __builtin_amdgcn_raw_buffer_load_b128(ars, off(AUX2 ? ah : mh, i, nh, 2), 0, 0);
 #endif
                     }
                 // retire them HERE, in the branch that issued them (vmcnt(0); this epilogue drains the
@@ -553,7 +558,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                     }
                     if (auxp) {
                         float ax[8];
-                        pk_unpack8(aux[i][nh], ax);
+                        pk_unpack8(aux[AUX2 ? mh : 0][i][nh], ax);
                         if constexpr (act_bwd(ACT)) {
 #pragma unroll
                             for (int c = 0; c < 8; ++c) {
