@@ -77,6 +77,59 @@ __global__ void __launch_bounds__(256) im2col_chunk_k(const bf16* __restrict__ x
     }
 }
 
+// im2col for C % 8 != 0 with the KH input rows of one output row staged in LDS (the 7×7×3 stem):
+// block = (image, output row).  The KH rows (W + 2P pixels incl. the zero border, C channels) are
+// read once with coalesced loads; each lane then writes whole 16-B chunks of a cols row from LDS
+// (k = (kh·KW + kw)·C + c reads row kh at pixel ow·S + kw, i.e. a contiguous run of KW·C elements
+// per kh).  The per-chunk gather of im2col_chunk_k issued 8 dependent 2-byte global loads instead.
+__global__ void __launch_bounds__(256) im2col_rows_k(const bf16* __restrict__ x, bf16* __restrict__ cols, int N,
+                                                     int H, int W, int C, int KH, int KW, int S, int P, int OH,
+                                                     int OW, int Kp) {
+    // [KH][RS] rows: padded row element r at lead + r, with lead chosen so the unpadded part starts
+    // 16-B aligned (its fill is 16-B loads / ds_write_b128 when W·C % 8 == 0)
+    extern __shared__ __attribute__((aligned(16))) short srow[];
+    const int oh = blockIdx.x % OH, n = blockIdx.x / OH;
+    const int WPC = (W + 2 * P) * C, PC = P * C, WC = W * C;
+    const int lead = (8 - PC % 8) % 8, RS = (lead + WPC + 7) / 8 * 8;
+    const bool vec = WC % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    const bf16* xn = x + (long)n * H * W * C;
+    for (int kh = 0; kh < KH; ++kh) {
+        const int ih = oh * S - P + kh;
+        short* dst = srow + kh * RS + lead;
+        if (ih < 0 || ih >= H) {
+            for (int r = threadIdx.x; r < WPC; r += 256) dst[r] = 0;
+            continue;
+        }
+        const bf16* xr = xn + (long)ih * W * C;
+        for (int r = threadIdx.x; r < PC; r += 256) {
+            dst[r] = 0;
+            dst[PC + WC + r] = 0;
+        }
+        if (vec) {
+            for (int q = threadIdx.x; q < WC / 8; q += 256)
+                *reinterpret_cast<s16x8*>(dst + PC + 8 * q) = *reinterpret_cast<const s16x8*>(xr + 8 * q);
+        } else {
+            for (int e = threadIdx.x; e < WC; e += 256) dst[PC + e] = __builtin_bit_cast(short, xr[e]);
+        }
+    }
+    __syncthreads();
+    const int chunks = Kp / 8, K = KH * KW * C, KWC = KW * C;
+    bf16* crow = cols + (long)(n * OH + oh) * OW * Kp;
+    for (int i = threadIdx.x; i < OW * chunks; i += 256) {
+        const int ow = i / chunks;
+        const int k0 = (i - ow * chunks) * 8;
+        int kh = k0 / KWC, j = k0 - kh * KWC;
+        const int base = ow * S * C;
+        s16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            v[e] = (k0 + e < K) ? srow[kh * RS + lead + base + j] : (short)0;
+            if (++j == KWC) j = 0, ++kh;
+        }
+        *reinterpret_cast<s16x8*>(crow + (long)ow * Kp + k0) = v;
+    }
+}
+
 // col2im gather for C % 8 == 0: one lane per (pixel, 8-channel chunk), 16-B loads/stores, only
 // the taps whose output position exists (stride-aligned) are visited.
 __global__ void __launch_bounds__(256) col2im_vec_k(const bf16* __restrict__ dcols, bf16* __restrict__ dx, int N,
@@ -413,6 +466,12 @@ extern "C" {
 void rn_im2col(const void* x, void* cols, int N, int H, int W, int C, int KH, int KW, int S, int P, int OH, int OW,
                int Kp, hipStream_t st) {
     const int vec = (C % 8 == 0);
+    const long rs = ((8 - (P * C) % 8) % 8 + (long)(W + 2 * P) * C + 7) / 8 * 8;  // im2col_rows_k's RS
+    if (!vec && KH * rs * 2 <= 32768) {  // the KH input rows of one output row fit in LDS
+        im2col_rows_k<<<N * OH, 256, KH * rs * 2, st>>>((const bf16*)x, (bf16*)cols, N, H, W, C, KH, KW,
+                                                                      S, P, OH, OW, Kp);
+        return;
+    }
     if (!vec) {
         im2col_chunk_k<<<gridn((long)N * OH * OW * (Kp / 8)), 256, 0, st>>>((const bf16*)x, (bf16*)cols, N, H, W, C,
                                                                             KH, KW, S, P, OH, OW, Kp);

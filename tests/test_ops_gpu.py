@@ -591,6 +591,25 @@ def test_conv2d(cuda, cfg):
         assert rel_err(t.grad, tf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,K,S,P", [(2, 224, 224, 3, 7, 2, 3), (3, 37, 29, 3, 7, 2, 3), (2, 20, 18, 5, 3, 1, 1),
+                                           (1, 9, 2200, 3, 5, 3, 2)])
+def test_im2col_small_channels(cuda, N, H, W, C, K, S, P):
+    """The small-C im2col (LDS-staged rows; the last case exceeds the LDS budget and takes the
+    per-chunk gather) is a pure copy: bitwise equal to F.unfold's layout ((kh, kw, c) per row)."""
+    from replicann_amd import _ext
+    torch.manual_seed(3)
+    x = bf(N, H, W, C)
+    OH, OW = (H + 2 * P - K) // S + 1, (W + 2 * P - K) // S + 1
+    Kd = K * K * C
+    Kp = (Kd + 7) // 8 * 8
+    cols = _ext.ops().im2col(x.contiguous(), K, K, S, P, Kp)
+    u = F.unfold(x.permute(0, 3, 1, 2).float(), K, padding=P, stride=S)  # [N, C*K*K (c, kh, kw)], L
+    u = u.view(N, C, K, K, OH * OW).permute(0, 4, 2, 3, 1).reshape(N * OH * OW, Kd)
+    ref = torch.zeros(N * OH * OW, Kp, device=x.device, dtype=torch.bfloat16)
+    ref[:, :Kd] = u.to(torch.bfloat16)
+    assert torch.equal(cols.view(N * OH * OW, Kp), ref)
+
+
 @pytest.mark.parametrize("C,OC,Kk,S,P,HW", [(64, 64, 3, 1, 1, 14), (64, 128, 3, 2, 1, 15), (128, 64, 3, 1, 1, 9),
                                            (64, 128, 1, 2, 0, 16), (128, 128, 3, 1, 1, 7), (64, 64, 3, 1, 0, 10),
                                            (64, 256, 3, 1, 1, 8)])
