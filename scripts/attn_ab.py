@@ -38,8 +38,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--D", type=int, default=64, help="head size (H = 768 // D keeps E = 768)")
     ap.add_argument("--noncausal", action="store_true")
+    ap.add_argument("--T", type=int, default=1024, help="sequence length (ViT-B/16: 197, non-causal)")
     a = ap.parse_args()
-    B, T, D = a.B, 1024, a.D
+    B, T, D = a.B, a.T, a.D
     H = 768 // D
     torch.manual_seed(0)
     qkv = torch.randn(B, T, 3, H, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
@@ -73,7 +74,7 @@ def main():
     for (ps, v), lst in sorted(res.items()):
         ms = min(x[0] for x in lst)
         fl = fl_f if ps == "fwd" else 2.5 * fl_f
-        print(json.dumps(dict(op=f"attn_{ps}", variant=v, B=B, H=H, D=D, ms=round(ms, 4), tflops=round(fl / ms / 1e9, 1),
+        print(json.dumps(dict(op=f"attn_{ps}", variant=v, B=B, H=H, T=T, D=D, ms=round(ms, 4), tflops=round(fl / ms / 1e9, 1),
                               all_ms=[round(x[0], 4) for x in lst], max_abs_diff_vs_first=max(x[1] for x in lst))),
               flush=True)
 
