@@ -51,7 +51,7 @@ def parse_args(argv=None):
                          "global batch on 8 GPUs, sized for 288 GB HBM; 512 images ViT, 256 ResNet)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
+    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16", "rsag"],
                     help="DDP gradient sum precision (fp32: widened, 2x the wire bytes of bf16)")
     ap.add_argument("--ddp", default="auto", choices=["auto", "on"],
                     help="on: run the data-parallel step (buckets, fp32 widening, collectives) even on 1 GPU")

@@ -44,6 +44,7 @@
 #include <vector>
 
 extern "C" void rn_comm_proxy(void* buf, long bytes, double volume_bytes, int wgs, double gbps, hipStream_t st);
+extern "C" void rn_cast_f32_bf16(const float* in, void* out, long n, hipStream_t st);
 
 namespace {
 
@@ -319,7 +320,8 @@ void comm_all_gather(int64_t h, const Tensor& in, Tensor out) {
     if (c.proxy) out.copy_(in.reshape(out.sizes()));
     bool cap = fork_from_current(c);
     if (c.proxy) {
-        proxy_issue(c, out, (double)(c.proxy_world - 1) / c.proxy_world * out.numel() * out.element_size() * c.proxy_world);
+        // a W-rank ring all-gather moves (W-1)/W of the full output per GPU (world 1: out is that output)
+        proxy_issue(c, out, (double)(c.proxy_world - 1) / c.proxy_world * out.numel() * out.element_size());
     } else
         RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), c.comm, c.stream));
     after_issue(c, cap, "all_gather", out.numel() * out.element_size());
@@ -337,11 +339,37 @@ void comm_reduce_scatter(int64_t h, const Tensor& in, Tensor out, int64_t op) {
     if (c.proxy) out.copy_(in.reshape(out.sizes()));
     bool cap = fork_from_current(c);
     if (c.proxy) {
-        proxy_issue(c, out, (double)(c.proxy_world - 1) / c.proxy_world * out.numel() * out.element_size() * c.proxy_world);
+        // a W-rank ring reduce-scatter moves (W-1)/W of the full input per GPU (world 1: out = in)
+        proxy_issue(c, out, (double)(c.proxy_world - 1) / c.proxy_world * out.numel() * out.element_size());
     } else
         RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), nccl_dtype(in), nccl_op(op),
                                      c.comm, c.stream));
     after_issue(c, cap, "reduce_scatter", in.numel() * in.element_size());
+}
+
+// The second half of the reducer's reduce-scatter -> all-gather path, on the comm stream right after
+// the reduce-scatter that filled shard32: narrow this rank's reduced fp32 shard to bf16 (shard16), then
+// all-gather the bf16 shards into `full` (rank order).  bf16 is rounded ONCE, after the exact fp32
+// cross-rank sum, and the gather moves half the bytes of an fp32 all-gather.
+void comm_narrow_all_gather(int64_t h, const Tensor& shard32, Tensor shard16, Tensor full) {
+    Comm& c = get(h);
+    check_alive(c);
+    TORCH_CHECK(shard32.is_cuda() && shard32.is_contiguous() && shard32.scalar_type() == at::kFloat &&
+                    shard16.is_contiguous() && shard16.scalar_type() == at::kBFloat16 &&
+                    shard16.numel() == shard32.numel() && full.is_contiguous() &&
+                    full.scalar_type() == at::kBFloat16 && full.numel() == shard16.numel() * c.world,
+                "comm_narrow_all_gather: fp32 shard, bf16 shard of the same size, bf16 full = world x shard");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(shard32.device());
+    bool cap = fork_from_current(c);
+    rn_cast_f32_bf16(shard32.data_ptr<float>(), shard16.data_ptr(), shard32.numel(), c.stream);
+    if (c.proxy) {
+        // world 1: the gathered result is the narrowed shard itself
+        HIP_OK(hipMemcpyAsync(full.data_ptr(), shard16.data_ptr(), shard16.numel() * 2, hipMemcpyDeviceToDevice, c.stream));
+        proxy_issue(c, full, (double)(c.proxy_world - 1) / c.proxy_world * full.numel() * full.element_size());
+    } else
+        RCCL_CHECK(ncclAllGather(shard16.data_ptr(), full.data_ptr(), (size_t)shard16.numel(), ncclBfloat16, c.comm,
+                                 c.stream));
+    after_issue(c, cap, "all_gather", full.numel() * full.element_size());
 }
 
 // the caller's current stream waits for every collective issued so far (no host sync)
@@ -411,6 +439,8 @@ TORCH_LIBRARY_FRAGMENT(replicann, m) {
     m.def("comm_broadcast(int h, Tensor(a!) t, int root) -> ()", &comm_broadcast);
     m.def("comm_all_gather(int h, Tensor inp, Tensor(a!) out) -> ()", &comm_all_gather);
     m.def("comm_reduce_scatter(int h, Tensor inp, Tensor(a!) out, int op) -> ()", &comm_reduce_scatter);
+    m.def("comm_narrow_all_gather(int h, Tensor shard32, Tensor(a!) shard16, Tensor(b!) full) -> ()",
+          &comm_narrow_all_gather);
     m.def("comm_wait(int h) -> ()", &comm_wait);
     m.def("comm_synchronize(int h) -> ()", &comm_synchronize);
     m.def("comm_info(int h) -> int[]", &comm_info);

@@ -137,7 +137,26 @@ __global__ void __launch_bounds__(TPB) bias_act_grad_k(const bf16* __restrict__ 
 
 }  // namespace
 
+// fp32 -> bf16 (round to nearest even), 8 elements per lane: the narrowing step of the data-parallel
+// reducer's reduce-scatter (fp32) -> all-gather (bf16) path, run on the communicator's stream
+__global__ void __launch_bounds__(256) cast_f32_bf16_k(const float* __restrict__ in, bf16* __restrict__ out, long n) {
+    const long n8 = n / 8;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+        const float4 a = reinterpret_cast<const float4*>(in)[2 * i], b = reinterpret_cast<const float4*>(in)[2 * i + 1];
+        const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        store8(out + i * 8, f);
+    }
+    for (long i = n8 * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = (bf16)in[i];
+}
+
 extern "C" {
+
+void rn_cast_f32_bf16(const float* in, void* out, long n, hipStream_t st) {
+    if (n <= 0) return;
+    long g = (n / 8 + 255) / 256;
+    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    cast_f32_bf16_k<<<(int)g, 256, 0, st>>>(in, (bf16*)out, n);
+}
 
 void rn_act_fwd(const void* x, void* y, long n, int kind, hipStream_t st) {
     int g = ew_grid(n / 8 + 1);

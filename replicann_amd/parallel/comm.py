@@ -1,8 +1,8 @@
 """Collective back-ends for the data-parallel reducer (SURVEY.md §1 L1', N16).
 
 Two implementations of one small interface (``all_reduce`` / ``broadcast`` /
-``all_gather`` / ``reduce_scatter`` issue asynchronously, ``wait`` joins them into the
-caller's stream, ``synchronize`` blocks the host):
+``all_gather`` / ``reduce_scatter`` / ``narrow_all_gather`` issue asynchronously, ``wait`` joins
+them into the caller's stream, ``synchronize`` blocks the host):
 
 * :class:`NativeComm` — the framework's own RCCL communicator
   (``csrc/comm/rccl_comm.cpp``): collectives on a dedicated high-priority HIP comm
@@ -53,6 +53,26 @@ class TorchComm:
 
     def reduce_scatter(self, inp, out, op="sum"):
         self._works.append(dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True))
+
+    _side = None
+
+    def narrow_all_gather(self, shard32, shard16, full):
+        """After ``reduce_scatter(…, shard32)``: narrow this rank's reduced fp32 shard into ``shard16``
+        and all-gather the bf16 shards into ``full`` — on a side stream that waits for the
+        reduce-scatter, so the compute stream is not held (GPU); in order on the CPU."""
+        rs = self._works[-1]
+        if shard32.is_cuda:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=shard32.device)
+            with torch.cuda.stream(self._side):
+                rs.wait()  # the side stream waits for the reduce-scatter's completion
+                shard16.copy_(shard32)
+                # issued from the side stream: the collective is ordered after the narrowing copy
+                self._works.append(dist.all_gather_into_tensor(full, shard16, group=self.group, async_op=True))
+        else:
+            rs.wait()
+            shard16.copy_(shard32)
+            self._works.append(dist.all_gather_into_tensor(full, shard16, group=self.group, async_op=True))
 
     def wait(self):
         for w in self._works:
@@ -127,6 +147,10 @@ class NativeComm:
 
     def reduce_scatter(self, inp, out, op="sum"):
         self.ops.comm_reduce_scatter(self.handle, inp, out, _OPS[op])
+
+    def narrow_all_gather(self, shard32, shard16, full):
+        """Narrow + bf16 all-gather on the comm stream, after the preceding reduce-scatter."""
+        self.ops.comm_narrow_all_gather(self.handle, shard32, shard16, full)
 
     def wait(self):
         """The current stream waits for every collective issued so far (stream-ordered)."""

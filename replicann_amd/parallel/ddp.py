@@ -11,6 +11,13 @@ parallelism at all; this is built MI355X-first:
   bf16 partials in a bf16 ring loses up to 3 bits).  The fused optimizer then reads
   the fp32 sums directly (``grad_source``), so there is no narrowing pass either.
   ``reduce_dtype=torch.bfloat16`` keeps the bf16-in-place variant (half the bytes);
+  ``reduce_mode="rsag"`` (with fp32) splits each bucket's all-reduce into its two ring halves and
+  narrows in between: an fp32 reduce-scatter (the exact cross-rank sum of this rank's shard), a
+  cast of that shard to bf16, and a bf16 all-gather of the reduced shards straight into the
+  gradient slice — 0.75x the wire bytes of the fp32 all-reduce, one bf16 rounding of the final
+  sum (the precision a one-GPU step's bf16 gradient has), and the optimizer reads bf16 gradients.
+  Buckets whose span does not split into ``world`` equal shards, and tied parameters' per-
+  contribution reductions, keep the fp32 all-reduce and are narrowed in ``finish()``;
 * buckets are formed in reverse parameter order (the order backward produces
   gradients) and sized for point-to-point xGMI rings (default 64 MB of reduced
   elements: large enough to amortise RCCL's per-collective latency over the 7
@@ -61,7 +68,8 @@ from .comm import make_comm
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, flat: FlatParams, bucket_mb: float = 64.0,
                  process_group=None, broadcast: bool = True, check_unused: bool = False,
-                 reduce_dtype=torch.float32, split_tied: bool = True, comm="auto", force: bool = False):
+                 reduce_dtype=torch.float32, split_tied: bool = True, comm="auto", force: bool = False,
+                 reduce_mode: str = "allreduce"):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -79,6 +87,15 @@ class DistributedDataParallel(nn.Module):
         # the buffer the all-reduce runs on (and the optimizer reads): fp32 copy, or the grads themselves
         self.reduce_buf = (torch.zeros(flat.numel, dtype=torch.float32, device=flat.grad.device)
                            if self.fp32 else flat.grad)
+        if reduce_mode not in ("allreduce", "rsag"):
+            raise ValueError(f"reduce_mode {reduce_mode!r}: allreduce | rsag")
+        # rsag: fp32 reduce-scatter + bf16 all-gather (needs the fp32 reduction of bf16 gradients)
+        self.rsag = reduce_mode == "rsag" and self.fp32 and flat.grad.dtype == torch.bfloat16
+        if self.rsag:  # shard scratch: bucket [lo, hi) owns [lo / world, hi / world)
+            W = self.world
+            self.rs32 = torch.zeros(flat.numel // W + 1, dtype=torch.float32, device=flat.grad.device)
+            self.rs16 = torch.zeros(flat.numel // W + 1, dtype=torch.bfloat16, device=flat.grad.device)
+        self._narrow = []  # fp32-reduced spans to narrow into the bf16 gradient in finish() (rsag)
         # ---- bucket assignment (reverse layout order); split (tied) parameters alone ----
         segs = flat.segments()
         self.split = {}  # id(p) -> [lo, hi, uses, side buffers]
@@ -157,6 +174,7 @@ class DistributedDataParallel(nn.Module):
         self.comm.wait()
 
     def _reset(self):
+        self._narrow = []
         self._pending = [b[2] for b in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
@@ -165,11 +183,26 @@ class DistributedDataParallel(nn.Module):
         self._split_done = {k: 0 for k in self.split}  # contributions reduced this step
         self.launched_in_backward = 0
 
-    def _reduce_slice(self, lo, hi, dst=None):
-        """Widen (fp32 mode) and all-reduce grad[lo:hi]; ``dst`` overrides the target buffer."""
+    def _reduce_slice(self, lo, hi, dst=None, whole=True):
+        """Widen (fp32 mode) and all-reduce grad[lo:hi]; ``dst`` overrides the target buffer.
+        rsag mode: a whole bucket that splits into ``world`` equal shards is reduce-scattered in fp32
+        and all-gathered back into grad[lo:hi] in bf16 instead (``whole`` False: one contribution of a
+        split parameter, summed with the others in fp32 in finish(): always the fp32 all-reduce)."""
         g = self.flat.grad[lo:hi]
+        W = self.world
+        if self.rsag and whole and dst is None and (hi - lo) % W == 0 and lo % W == 0:
+            red = self.reduce_buf[lo:hi]
+            red.copy_(g)  # widen: the reduce-scatter sums in fp32
+            o, n = lo // W, (hi - lo) // W
+            self.comm.reduce_scatter(red, self.rs32[o:o + n])
+            self.comm.narrow_all_gather(self.rs32[o:o + n], self.rs16[o:o + n], g)
+            if self._sched_ops is not None:
+                self._sched_ops.gemm_set_sched(1)
+            return
         if dst is None:
             dst = self.reduce_buf[lo:hi]
+        if self.rsag:
+            self._narrow.append((lo, hi))
         if dst.data_ptr() != g.data_ptr():
             dst.copy_(g)  # stream-ordered after the kernels that produced the gradient
         self.comm.all_reduce(dst)
@@ -195,7 +228,7 @@ class DistributedDataParallel(nn.Module):
         g = self.flat.grad[lo:hi]
         if self.fp32:
             # contribution 0 → the reduction buffer, later ones → side buffers (added in finish)
-            self._reduce_slice(lo, hi, None if k == 0 else sides[k - 1])
+            self._reduce_slice(lo, hi, None if k == 0 else sides[k - 1], whole=False)
             if not final:
                 g.zero_()  # the next contribution accumulates into a cleared slice
         elif final:
@@ -229,8 +262,9 @@ class DistributedDataParallel(nn.Module):
 
     @property
     def grad_source(self):
-        """The tensor holding the all-reduced (SUM over ranks) flat gradient after ``finish()``."""
-        return self.reduce_buf
+        """The tensor holding the all-reduced (SUM over ranks) flat gradient after ``finish()``:
+        the fp32 reduction buffer, or (rsag) the bf16 gradient buffer itself."""
+        return self.flat.grad if self.rsag else self.reduce_buf
 
     reduced_grad = grad_source
 
@@ -255,10 +289,11 @@ class DistributedDataParallel(nn.Module):
                 # the contributions that never signalled (e.g. autograd accumulated both uses at
                 # once, CPU path) are all in the slice: reduce it as ONE contribution
                 if self.fp32 and k > 0:
-                    self._reduce_slice(lo, hi, sides[k - 1])
+                    self._reduce_slice(lo, hi, sides[k - 1], whole=False)
                     unused_sides = sides[k:]
                 else:
-                    self._reduce_slice(lo, hi)  # fp32: contribution 0; bf16: in place, sides[:k] hold the rest
+                    # fp32: contribution 0; bf16: in place, sides[:k] hold the rest
+                    self._reduce_slice(lo, hi, whole=False)
                     unused_sides = sides[k:]
                 for s_ in unused_sides:
                     s_.zero_()
@@ -269,6 +304,10 @@ class DistributedDataParallel(nn.Module):
         for pid, (lo, hi, uses, sides) in self.split.items():
             for s in sides:
                 self.reduce_buf[lo:hi].add_(s)
+        # rsag: spans that took the fp32 all-reduce (tied contributions, unevenly split buckets) are
+        # narrowed into the bf16 gradient the optimizer reads
+        for lo, hi in dict.fromkeys(self._narrow):
+            self.flat.grad[lo:hi].copy_(self.reduce_buf[lo:hi])
         assert all(self._launched), "a gradient bucket was never reduced"
         self.comm_wait_ms = (time.perf_counter() - t0) * 1e3
 

@@ -81,7 +81,9 @@ class TrainConfig:
     grad_accum: int = 1
     max_grad_norm: float = 1.0
     bucket_mb: float = 64.0
-    reduce_dtype: str = "fp32"    # DDP cross-rank sum: fp32 (exact widening) | bf16 (in place, half the bytes)
+    # DDP cross-rank sum: fp32 (exact widening) | bf16 (in place, half the bytes) | rsag (fp32
+    # reduce-scatter + bf16 all-gather of the reduced shards: 0.75x the bytes, one final rounding)
+    reduce_dtype: str = "fp32"
     ddp: str = "auto"             # auto (world > 1) | on (also at world 1: one-GPU rehearsal of the DDP step)
     comm: str = "auto"            # auto (native RCCL communicator on GPUs, torch.distributed otherwise) | native | torch
     graph: str = "auto"           # auto | on | off — capture the whole step in one hipGraph
@@ -120,7 +122,8 @@ class Trainer:
         use_ddp = self.world > 1 or cfg.ddp == "on"
         self.ddp = (DistributedDataParallel(
             self.model, self.flat, cfg.bucket_mb, comm=cfg.comm, force=True,
-            reduce_dtype=torch.bfloat16 if cfg.reduce_dtype == "bf16" else torch.float32)
+            reduce_dtype=torch.bfloat16 if cfg.reduce_dtype == "bf16" else torch.float32,
+            reduce_mode="rsag" if cfg.reduce_dtype == "rsag" else "allreduce")
                     if use_ddp else None)
         gs = 1.0 / self.world
         if cfg.optimizer == "adamw":

@@ -200,3 +200,40 @@ def test_ddp_step_proxy_matches_native_and_enables_queue(one_rank_pg, monkeypatc
     finally:
         torch.ops.replicann.gemm_set_sched(0)
         torch.ops.replicann.gemm_set_reserve(0)
+
+
+def test_ddp_step_rsag_native_torch_graph(one_rank_pg):
+    """reduce_dtype="rsag" (fp32 reduce-scatter -> bf16 narrow -> bf16 all-gather per bucket): the
+    native communicator (narrow on its comm stream) and ProcessGroupNCCL (narrow on a side stream)
+    give the same bits, the native step captures into one hipGraph with the same result, and the
+    training tracks the fp32 all-reduce step (one bf16 rounding of the summed gradient)."""
+    fp_l, fp_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"))
+    nat_l, nat_w, _, nat_c, hooked = _run(dict(graph="off", ddp="on", comm="native", reduce_dtype="rsag"))
+    tor_l, tor_w, _, tor_c, _ = _run(dict(graph="off", ddp="on", comm="torch", reduce_dtype="rsag"))
+    gr_l, gr_w, gr_g, _, _ = _run(dict(graph="auto", ddp="on", comm="native", reduce_dtype="rsag"))
+    assert (nat_c, tor_c) == ("native", "torch") and hooked > 0 and gr_g
+    assert nat_l == tor_l and torch.equal(nat_w, tor_w)
+    assert nat_l == gr_l and torch.equal(nat_w, gr_w)
+    for a, b in zip(nat_l, fp_l):
+        assert abs(a - b) <= 2e-2 * abs(b), (nat_l, fp_l)
+    assert (nat_w - fp_w).abs().max().item() < 5e-2
+
+
+def test_proxy_reduce_scatter_narrow_all_gather():
+    """Proxy communicator: reduce-scatter (world 1: a copy) then narrow + bf16 all-gather returns the
+    bf16-rounded input, stream-ordered on the comm stream."""
+    from replicann_amd.parallel.comm import NativeComm
+
+    c = NativeComm(device="cuda:0", proxy=True)
+    try:
+        a = torch.randn(1 << 20, device="cuda")
+        s32 = torch.empty_like(a)
+        s16 = torch.empty(a.numel(), device="cuda", dtype=torch.bfloat16)
+        full = torch.empty_like(s16)
+        c.reduce_scatter(a, s32)
+        c.narrow_all_gather(s32, s16, full)
+        c.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(full, a.to(torch.bfloat16)) and torch.equal(s16, full)
+    finally:
+        c.close()

@@ -181,11 +181,14 @@ def _tied_worker(rank, world, port, dtype_name, reduce_name, q):
     try:
         from replicann_amd.parallel import DistributedDataParallel
         from replicann_amd.utils.flat import FlatParams
-        dtype, rdt = getattr(torch, dtype_name), getattr(torch, reduce_name)
+        mode = "rsag" if reduce_name == "rsag" else "allreduce"
+        dtype, rdt = getattr(torch, dtype_name), getattr(torch, "float32" if mode == "rsag" else reduce_name)
         torch.manual_seed(0)
         net = TiedNet().to(dtype)
         flat = FlatParams(net)
-        ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_dtype=rdt)
+        ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_dtype=rdt, reduce_mode=mode)
+        if mode == "rsag":  # every regular bucket splits into world shards: none takes the fp32 all-reduce
+            assert ddp.rsag and all((hi - lo) % world == 0 and lo % world == 0 for lo, hi, _ in ddp.buckets)
         X, Y = _tied_data(world)
         x, y = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
         res = []
@@ -201,11 +204,12 @@ def _tied_worker(rank, world, port, dtype_name, reduce_name, q):
 
 
 @pytest.mark.parametrize("dtype_name,reduce_name", [("float32", "float32"), ("bfloat16", "float32"),
-                                                    ("bfloat16", "bfloat16")])
+                                                    ("bfloat16", "bfloat16"), ("bfloat16", "rsag")])
 def test_ddp_tied_split_gloo(dtype_name, reduce_name):
     """A tied parameter's two contributions are all-reduced separately (the head's during the
     backward) and summed in finish(); result = single-process gradient of the whole batch, for the
-    fp32 reduction buffer (bf16 grads widened) and the bf16 in-place mode."""
+    fp32 reduction buffer (bf16 grads widened), the bf16 in-place mode, and rsag (fp32
+    reduce-scatter + bf16 all-gather per bucket; the tied parameter narrowed in finish())."""
     from replicann_amd.utils.flat import FlatParams
     world = 2
     ctx = mp.get_context("spawn")
@@ -230,7 +234,7 @@ def test_ddp_tied_split_gloo(dtype_name, reduce_name):
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     for rank, grads, launched, nb, is_fp32 in res:
         assert nb >= 2
-        assert is_fp32 == (reduce_name == "float32" or dtype == torch.float32)
+        assert is_fp32 == (reduce_name == "float32" or dtype == torch.float32)  # rsag: bf16 gradients
         # the head contribution + every regular bucket + the embedding contribution, all in backward
         assert launched == nb + 2, (launched, nb)
         for g in grads:
