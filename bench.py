@@ -51,8 +51,12 @@ def parse_args(argv=None):
                          "global batch on 8 GPUs, sized for 288 GB HBM; 512 images ViT, 256 ResNet)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16", "rsag"],
-                    help="DDP gradient sum precision (fp32: widened, 2x the wire bytes of bf16)")
+    ap.add_argument("--reduce-dtype", default="rsag", choices=["rsag", "fp32", "bf16"],
+                    help="DDP gradient sum: rsag = fp32 reduce-scatter + bf16 all-gather of the reduced shards "
+                         "(exact sum, one rounding, 0.75x the bytes of fp32); fp32 all-reduce; bf16 in place")
+    ap.add_argument("--ddp-schedule", default="auto", choices=["auto", "eager", "window", "end"],
+                    help="when a ready gradient bucket's collective is issued: at once, beside the next attention "
+                         "backward (the persistent GEMMs own every CU), or after the backward")
     ap.add_argument("--ddp", default="auto", choices=["auto", "on"],
                     help="on: run the data-parallel step (buckets, fp32 widening, collectives) even on 1 GPU")
     ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
@@ -129,7 +133,7 @@ def main(argv=None):
                       optimizer="adamw" if not args.model.startswith("resnet") else "sgd",
                       weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,
                       warmup_steps=10, lr=3e-4 if args.model.startswith("gpt2-medium") else 6e-4, bucket_mb=args.bucket_mb,
-                      reduce_dtype=args.reduce_dtype, log_every=10**9,
+                      reduce_dtype=args.reduce_dtype, ddp_schedule=args.ddp_schedule, log_every=10**9,
                       graph=args.graph, ddp=args.ddp, comm=args.comm, device=args.device)
     tr = Trainer(cfg)
     world = tr.world
@@ -212,6 +216,7 @@ def main(argv=None):
             "comm": (tr.ddp.comm.name if tr.ddp is not None else None),
             "comm_world": comm_world,
             "grad_reduce_dtype": args.reduce_dtype if tr.ddp is not None else None,
+            "ddp_schedule": args.ddp_schedule if tr.ddp is not None else None,
             "gemm_cu_reserve": (int(torch.ops.replicann.gemm_get_reserve())
                                 if dev.type == "cuda" and hasattr(torch.ops.replicann, "gemm_get_reserve") else None),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],

@@ -95,7 +95,9 @@ class _AttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
+        from ..parallel.windows import open_window
         q, k, v, o, lse, bias = ctx.saved_tensors
+        open_window()
         dq, dk, dv = _ext.ops().attn_bwd(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
                                          ctx.dropout_p, 0, ctx.seed)
         return dq, dk, dv, None, None, None, None, None
@@ -134,8 +136,10 @@ class _AttnPackedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         from .linear import _direct_grad, _notify
+        from ..parallel.windows import open_window
         qkv, o, lse, bias = ctx.saved_tensors
         q, k, v = qkv.unbind(2)
+        open_window()  # queued gradient collectives run beside the attention backward's short workgroups
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.unbind(2)
         pb = ctx.producer_bias

@@ -42,6 +42,15 @@ parallelism at all; this is built MI355X-first:
   launches buckets whose parameters received no gradient (unused parameters:
   their slice is zero on every rank), and checks every bucket was reduced
   exactly once;
+* **when** a ready bucket's collective is issued (``schedule``; ``"auto"``, the default, is
+  ``"window"`` once a step has shown a window and ``"eager"`` otherwise): ``"eager"`` at once (the classic
+  overlap), ``"window"`` queued until the next communication window — the attention backward, whose
+  short workgroups a high-priority collective interleaves with (``parallel/windows.py``) — at most
+  ``window_mb`` of reduction bytes per window (a larger tied-parameter contribution is split into
+  pieces), the rest in ``finish()``; ``"end"`` everything in ``finish()``.  The widening copy always
+  runs when the bucket is ready.  Why not simply eager: the persistent GEMM owns every CU, and a
+  collective beside it delays the GEMM's workgroups on the CUs it holds for its whole duration
+  (profiles/ddp_window_proxy_r3ze.txt);
 * ``no_sync()`` disables reduction for gradient accumulation;
 * construction broadcasts rank 0's parameters and buffers (one flat broadcast);
 * the collectives go through a :mod:`~replicann_amd.parallel.comm` back-end: on GPUs
@@ -69,7 +78,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, flat: FlatParams, bucket_mb: float = 64.0,
                  process_group=None, broadcast: bool = True, check_unused: bool = False,
                  reduce_dtype=torch.float32, split_tied: bool = True, comm="auto", force: bool = False,
-                 reduce_mode: str = "allreduce"):
+                 reduce_mode: str = "allreduce", schedule: str = "auto", window_mb: float | None = None):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -96,6 +105,22 @@ class DistributedDataParallel(nn.Module):
             self.rs32 = torch.zeros(flat.numel // W + 1, dtype=torch.float32, device=flat.grad.device)
             self.rs16 = torch.zeros(flat.numel // W + 1, dtype=torch.bfloat16, device=flat.grad.device)
         self._narrow = []  # fp32-reduced spans to narrow into the bf16 gradient in finish() (rsag)
+        if schedule not in ("auto", "eager", "window", "end"):
+            raise ValueError(f"schedule {schedule!r}: auto | eager | window | end")
+        self.schedule = schedule
+        # auto: eager until a step has shown a window (a model without attention backward keeps
+        # eager), window from the next step on — every rank runs the same model, so the switch is
+        # at the same step everywhere
+        self._windowed = schedule == "window"
+        self._saw_window = False
+        if window_mb is None:  # REPLICANN_DDP_WINDOW_MB: reduction bytes issued per window (default 64)
+            import os
+            window_mb = float(os.environ.get("REPLICANN_DDP_WINDOW_MB", 64.0))
+        self.window_bytes = int(window_mb * 1024 * 1024)
+        self._queue = []  # prepared collectives waiting for a window (schedule window / end)
+        if schedule in ("window", "auto"):
+            from .windows import register
+            register(self._window)
         # ---- bucket assignment (reverse layout order); split (tied) parameters alone ----
         segs = flat.segments()
         self.split = {}  # id(p) -> [lo, hi, uses, side buffers]
@@ -175,6 +200,7 @@ class DistributedDataParallel(nn.Module):
 
     def _reset(self):
         self._narrow = []
+        self._queue = []
         self._pending = [b[2] for b in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
@@ -184,6 +210,42 @@ class DistributedDataParallel(nn.Module):
         self.launched_in_backward = 0
 
     def _reduce_slice(self, lo, hi, dst=None, whole=True):
+        """Prepare (widen, now) and issue or queue (``schedule``) the reduction of grad[lo:hi]."""
+        for job in self._prepare(lo, hi, dst, whole):
+            if self.schedule == "eager" or (self.schedule == "auto" and not self._windowed):
+                self._issue(job)
+            else:
+                self._queue.append(job)
+
+    def _job_bytes(self, job):
+        return (job[2] - job[1]) * 4 if job[0] == "rsag" else job[1].numel() * job[1].element_size()
+
+    def _issue(self, job):
+        if job[0] == "rsag":
+            _, lo, hi = job
+            W = self.world
+            o, n = lo // W, (hi - lo) // W
+            self.comm.reduce_scatter(self.reduce_buf[lo:hi], self.rs32[o:o + n])
+            self.comm.narrow_all_gather(self.rs32[o:o + n], self.rs16[o:o + n], self.flat.grad[lo:hi])
+        else:
+            self.comm.all_reduce(job[1])
+        if self._sched_ops is not None:
+            self._sched_ops.gemm_set_sched(1)  # later GEMMs of this backward share the CUs with RCCL
+
+    def _window(self):
+        """A communication window opened: issue queued collectives, up to ``window_bytes``."""
+        if not (self._sync and self.active):
+            return
+        self._saw_window = True
+        if not self._windowed or not self._queue:
+            return
+        used = 0
+        while self._queue and (used == 0 or used + self._job_bytes(self._queue[0]) <= self.window_bytes):
+            job = self._queue.pop(0)
+            used += self._job_bytes(job)
+            self._issue(job)
+
+    def _prepare(self, lo, hi, dst=None, whole=True):
         """Widen (fp32 mode) and all-reduce grad[lo:hi]; ``dst`` overrides the target buffer.
         rsag mode: a whole bucket that splits into ``world`` equal shards is reduce-scattered in fp32
         and all-gathered back into grad[lo:hi] in bf16 instead (``whole`` False: one contribution of a
@@ -191,23 +253,19 @@ class DistributedDataParallel(nn.Module):
         g = self.flat.grad[lo:hi]
         W = self.world
         if self.rsag and whole and dst is None and (hi - lo) % W == 0 and lo % W == 0:
-            red = self.reduce_buf[lo:hi]
-            red.copy_(g)  # widen: the reduce-scatter sums in fp32
-            o, n = lo // W, (hi - lo) // W
-            self.comm.reduce_scatter(red, self.rs32[o:o + n])
-            self.comm.narrow_all_gather(self.rs32[o:o + n], self.rs16[o:o + n], g)
-            if self._sched_ops is not None:
-                self._sched_ops.gemm_set_sched(1)
-            return
+            self.reduce_buf[lo:hi].copy_(g)  # widen: the reduce-scatter sums in fp32
+            return [("rsag", lo, hi)]
         if dst is None:
             dst = self.reduce_buf[lo:hi]
         if self.rsag:
             self._narrow.append((lo, hi))
         if dst.data_ptr() != g.data_ptr():
             dst.copy_(g)  # stream-ordered after the kernels that produced the gradient
-        self.comm.all_reduce(dst)
-        if self._sched_ops is not None:
-            self._sched_ops.gemm_set_sched(1)  # later GEMMs of this backward share the CUs with RCCL
+        if not self._windowed and self.schedule != "end":
+            return [("ar", dst)]
+        # queued: pieces of at most one window's budget (a tied contribution can exceed it)
+        step = max(1, self.window_bytes // dst.element_size())
+        return [("ar", dst[i:i + step]) for i in range(0, dst.numel(), step)]
 
     def _launch_ready(self, from_hook=False):
         while self._next < len(self.buckets) and self._ready[self._next]:
@@ -298,6 +356,10 @@ class DistributedDataParallel(nn.Module):
                 for s_ in unused_sides:
                     s_.zero_()
             self._split_done[pid] = uses
+        while self._queue:  # collectives no window took (schedule window / end), in queue order
+            self._issue(self._queue.pop(0))
+        if self.schedule == "auto":
+            self._windowed = self._saw_window
         self.comm.wait()  # native: the compute stream joins the comm stream (no host sync)
         if self._sched_ops is not None:
             self._sched_ops.gemm_set_sched(0)

@@ -81,9 +81,14 @@ class TrainConfig:
     grad_accum: int = 1
     max_grad_norm: float = 1.0
     bucket_mb: float = 64.0
-    # DDP cross-rank sum: fp32 (exact widening) | bf16 (in place, half the bytes) | rsag (fp32
-    # reduce-scatter + bf16 all-gather of the reduced shards: 0.75x the bytes, one final rounding)
-    reduce_dtype: str = "fp32"
+    # DDP cross-rank sum: rsag (default: fp32 reduce-scatter = exact sum, then a bf16 all-gather of
+    # the reduced shards: 0.75x the bytes of fp32, one final rounding = the one-GPU step's gradient
+    # precision) | fp32 (all-reduce in fp32, the optimizer reads it unrounded) | bf16 (in place)
+    reduce_dtype: str = "rsag"
+    # when a ready gradient bucket's collective is issued: auto (window once the model has shown one,
+    # else eager) | eager (at once) | window (beside the next attention backward, parallel/windows.py)
+    # | end (after the backward).  Measured under the 8-GPU comm proxy: profiles/ddp_window_proxy_r3ze.txt
+    ddp_schedule: str = "auto"
     ddp: str = "auto"             # auto (world > 1) | on (also at world 1: one-GPU rehearsal of the DDP step)
     comm: str = "auto"            # auto (native RCCL communicator on GPUs, torch.distributed otherwise) | native | torch
     graph: str = "auto"           # auto | on | off — capture the whole step in one hipGraph
@@ -123,7 +128,7 @@ class Trainer:
         self.ddp = (DistributedDataParallel(
             self.model, self.flat, cfg.bucket_mb, comm=cfg.comm, force=True,
             reduce_dtype=torch.bfloat16 if cfg.reduce_dtype == "bf16" else torch.float32,
-            reduce_mode="rsag" if cfg.reduce_dtype == "rsag" else "allreduce")
+            reduce_mode="rsag" if cfg.reduce_dtype == "rsag" else "allreduce", schedule=cfg.ddp_schedule)
                     if use_ddp else None)
         gs = 1.0 / self.world
         if cfg.optimizer == "adamw":

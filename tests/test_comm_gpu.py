@@ -207,7 +207,7 @@ def test_ddp_step_rsag_native_torch_graph(one_rank_pg):
     native communicator (narrow on its comm stream) and ProcessGroupNCCL (narrow on a side stream)
     give the same bits, the native step captures into one hipGraph with the same result, and the
     training tracks the fp32 all-reduce step (one bf16 rounding of the summed gradient)."""
-    fp_l, fp_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native"))
+    fp_l, fp_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native", reduce_dtype="fp32"))
     nat_l, nat_w, _, nat_c, hooked = _run(dict(graph="off", ddp="on", comm="native", reduce_dtype="rsag"))
     tor_l, tor_w, _, tor_c, _ = _run(dict(graph="off", ddp="on", comm="torch", reduce_dtype="rsag"))
     gr_l, gr_w, gr_g, _, _ = _run(dict(graph="auto", ddp="on", comm="native", reduce_dtype="rsag"))
@@ -237,3 +237,17 @@ def test_proxy_reduce_scatter_narrow_all_gather():
         assert torch.equal(full, a.to(torch.bfloat16)) and torch.equal(s16, full)
     finally:
         c.close()
+
+
+def test_ddp_window_schedule_matches_eager(one_rank_pg):
+    """schedule="window" (collectives queued until the next attention backward, at most window_mb per
+    window, the rest in finish()) and "end" change WHEN the reductions run, not their result: losses and
+    weights equal the eager schedule's, for the fp32 all-reduce and rsag, native and torch transports."""
+    for red in ("fp32", "rsag"):
+        ref_l, ref_w, _, _, _ = _run(dict(graph="off", ddp="on", comm="native", reduce_dtype=red))
+        for comm in ("native", "torch"):
+            for sched in ("window", "end"):
+                l, w, _, _, _ = _run(dict(graph="off", ddp="on", comm=comm, reduce_dtype=red, ddp_schedule=sched))
+                assert l == ref_l and torch.equal(w, ref_w), (red, comm, sched)
+        gl, gw, gg, _, _ = _run(dict(graph="auto", ddp="on", comm="native", reduce_dtype=red, ddp_schedule="window"))
+        assert gg and gl == ref_l and torch.equal(gw, ref_w)  # window schedule captures into one hipGraph

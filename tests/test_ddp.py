@@ -175,7 +175,7 @@ def _tied_data(world):
     return torch.randint(0, 40, (world * 4, 6), generator=g), torch.randint(0, 40, (world * 4, 6), generator=g)
 
 
-def _tied_worker(rank, world, port, dtype_name, reduce_name, q):
+def _tied_worker(rank, world, port, dtype_name, reduce_name, q, schedule="eager"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -186,7 +186,11 @@ def _tied_worker(rank, world, port, dtype_name, reduce_name, q):
         torch.manual_seed(0)
         net = TiedNet().to(dtype)
         flat = FlatParams(net)
-        ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_dtype=rdt, reduce_mode=mode)
+        ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_dtype=rdt, reduce_mode=mode,
+                                      schedule=schedule, window_mb=0.0003)
+        from replicann_amd.parallel.windows import open_window
+        if schedule == "window":  # a window mid-backward issues part of the queue (tiny budget: several pieces)
+            net.mid.register_full_backward_hook(lambda *a: open_window())
         if mode == "rsag":  # every regular bucket splits into world shards: none takes the fp32 all-reduce
             assert ddp.rsag and all((hi - lo) % world == 0 and lo % world == 0 for lo, hi, _ in ddp.buckets)
         X, Y = _tied_data(world)
@@ -203,9 +207,11 @@ def _tied_worker(rank, world, port, dtype_name, reduce_name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype_name,reduce_name", [("float32", "float32"), ("bfloat16", "float32"),
-                                                    ("bfloat16", "bfloat16"), ("bfloat16", "rsag")])
-def test_ddp_tied_split_gloo(dtype_name, reduce_name):
+@pytest.mark.parametrize("dtype_name,reduce_name,schedule", [
+    ("float32", "float32", "eager"), ("bfloat16", "float32", "eager"), ("bfloat16", "bfloat16", "eager"),
+    ("bfloat16", "rsag", "eager"), ("bfloat16", "float32", "window"), ("bfloat16", "rsag", "window"),
+    ("float32", "float32", "end")])
+def test_ddp_tied_split_gloo(dtype_name, reduce_name, schedule):
     """A tied parameter's two contributions are all-reduced separately (the head's during the
     backward) and summed in finish(); result = single-process gradient of the whole batch, for the
     fp32 reduction buffer (bf16 grads widened), the bf16 in-place mode, and rsag (fp32
@@ -215,7 +221,8 @@ def test_ddp_tied_split_gloo(dtype_name, reduce_name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_tied_worker, args=(r, world, port, dtype_name, reduce_name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_tied_worker, args=(r, world, port, dtype_name, reduce_name, q, schedule))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])

@@ -41,7 +41,7 @@ def _batch(world):
     return ids[:, :-1].cuda(), ids[:, 1:].cuda()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="allreduce", schedule="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), REPLICANN_DIST_BACKEND="gloo", REPLICANN_SHARE_DEVICE="1")
     from replicann_amd.parallel import DistributedDataParallel, init_distributed
@@ -50,13 +50,15 @@ def _worker(rank, world, port, q):
     try:
         m = _model()
         flat = FlatParams(m)
-        ddp = DistributedDataParallel(m, flat, bucket_mb=0.25)  # several buckets
+        ddp = DistributedDataParallel(m, flat, bucket_mb=0.25, reduce_mode=mode, schedule=schedule,
+                                      window_mb=0.2)  # several buckets; windows take a few pieces each
         x, y = _batch(world)
         x, y = x[2 * rank:2 * rank + 2], y[2 * rank:2 * rank + 2]
-        flat.zero_grad()
-        ddp(x, y).backward()
-        hooked = ddp.launched_in_backward
-        ddp.finish()
+        for _ in range(2 if schedule == "auto" else 1):  # auto: step 1 eager, step 2 windowed
+            flat.zero_grad()
+            ddp(x, y).backward()
+            hooked = ddp.launched_in_backward
+            ddp.finish()
         torch.cuda.synchronize()
         # numpy is pickled by value (a CPU tensor would travel as a shared-memory fd
         # that can vanish when this worker exits before the parent unpickles it)
@@ -65,7 +67,10 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_ddp_native_path_two_ranks_one_gpu():
+@pytest.mark.parametrize("mode,schedule", [("allreduce", "eager"), ("rsag", "auto"), ("rsag", "end")])
+def test_ddp_native_path_two_ranks_one_gpu(mode, schedule):
+    """Two ranks on one card over gloo (torch.distributed transport with GPU tensors: the rsag
+    narrowing runs on the side stream, windows are opened by the attention backward)."""
     from replicann_amd import _ext
     from replicann_amd.utils.flat import FlatParams
     assert _ext.available()
@@ -73,7 +78,7 @@ def test_ddp_native_path_two_ranks_one_gpu():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, schedule)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
