@@ -56,21 +56,27 @@ class TorchComm:
 
     _side = None
 
-    def narrow_all_gather(self, shard32, shard16, full):
+    def narrow_all_gather(self, shard32, shard16, full, after_rs=True):
         """After ``reduce_scatter(…, shard32)``: narrow this rank's reduced fp32 shard into ``shard16``
         and all-gather the bf16 shards into ``full`` — on a side stream that waits for the
-        reduce-scatter, so the compute stream is not held (GPU); in order on the CPU."""
-        rs = self._works[-1]
+        reduce-scatter, so the compute stream is not held (GPU); in order on the CPU.
+        ``after_rs=False``: shard32 was produced on the current stream instead (e.g. a sum of shards)."""
+        rs = self._works[-1] if after_rs else None
         if shard32.is_cuda:
             if self._side is None:
                 self._side = torch.cuda.Stream(device=shard32.device)
+            cur = torch.cuda.current_stream(shard32.device)
             with torch.cuda.stream(self._side):
-                rs.wait()  # the side stream waits for the reduce-scatter's completion
+                if rs is not None:
+                    rs.wait()  # the side stream waits for the reduce-scatter's completion
+                else:
+                    self._side.wait_stream(cur)
                 shard16.copy_(shard32)
                 # issued from the side stream: the collective is ordered after the narrowing copy
                 self._works.append(dist.all_gather_into_tensor(full, shard16, group=self.group, async_op=True))
         else:
-            rs.wait()
+            if rs is not None:
+                rs.wait()
             shard16.copy_(shard32)
             self._works.append(dist.all_gather_into_tensor(full, shard16, group=self.group, async_op=True))
 
@@ -148,8 +154,9 @@ class NativeComm:
     def reduce_scatter(self, inp, out, op="sum"):
         self.ops.comm_reduce_scatter(self.handle, inp, out, _OPS[op])
 
-    def narrow_all_gather(self, shard32, shard16, full):
-        """Narrow + bf16 all-gather on the comm stream, after the preceding reduce-scatter."""
+    def narrow_all_gather(self, shard32, shard16, full, after_rs=True):
+        """Narrow + bf16 all-gather on the comm stream, after the preceding reduce-scatter (and, being
+        forked from the current stream, after whatever produced shard32 there)."""
         self.ops.comm_narrow_all_gather(self.handle, shard32, shard16, full)
 
     def wait(self):

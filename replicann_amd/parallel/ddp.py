@@ -104,6 +104,7 @@ class DistributedDataParallel(nn.Module):
             W = self.world
             self.rs32 = torch.zeros(flat.numel // W + 1, dtype=torch.float32, device=flat.grad.device)
             self.rs16 = torch.zeros(flat.numel // W + 1, dtype=torch.bfloat16, device=flat.grad.device)
+        self.tie_rs = {}  # rsag: tied parameter -> one fp32 shard per contribution (summed in finish)
         self._narrow = []  # fp32-reduced spans to narrow into the bf16 gradient in finish() (rsag)
         if schedule not in ("auto", "eager", "window", "end"):
             raise ValueError(f"schedule {schedule!r}: auto | eager | window | end")
@@ -154,6 +155,11 @@ class DistributedDataParallel(nn.Module):
         if cur_hi is not None:
             self.buckets.append([cur_lo, cur_hi, cur_n])
         self._split_params = {id(p): p for p, _, _ in segs if id(p) in self.split}
+        if self.rsag:
+            for pid, (lo, hi, uses, _) in self.split.items():
+                if (hi - lo) % self.world == 0 and lo % self.world == 0:
+                    self.tie_rs[pid] = [torch.zeros((hi - lo) // self.world, dtype=torch.float32,
+                                                    device=flat.grad.device) for _ in range(uses)]
         self._reset()
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p, _, _ in segs]
         flat.ready_hooks.append(self._hook)  # parameters whose grads are accumulated directly by kernels
@@ -201,6 +207,7 @@ class DistributedDataParallel(nn.Module):
     def _reset(self):
         self._narrow = []
         self._queue = []
+        self._tie_plan = {}  # tied parameter -> the reduce-scatter pieces this step (rsag)
         self._pending = [b[2] for b in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
@@ -212,13 +219,40 @@ class DistributedDataParallel(nn.Module):
     def _reduce_slice(self, lo, hi, dst=None, whole=True):
         """Prepare (widen, now) and issue or queue (``schedule``) the reduction of grad[lo:hi]."""
         for job in self._prepare(lo, hi, dst, whole):
-            if self.schedule == "eager" or (self.schedule == "auto" and not self._windowed):
-                self._issue(job)
-            else:
-                self._queue.append(job)
+            self._submit(job)
+
+    def _submit(self, job):
+        if self.schedule == "eager" or (self.schedule == "auto" and not self._windowed):
+            self._issue(job)
+        else:
+            self._queue.append(job)
 
     def _job_bytes(self, job):
-        return (job[2] - job[1]) * 4 if job[0] == "rsag" else job[1].numel() * job[1].element_size()
+        if job[0] == "rsag":
+            return (job[2] - job[1]) * 4
+        return job[1].numel() * job[1].element_size()  # "ar" (buffer) / "rs" (input)
+
+    def _tie_chunks(self, n):
+        """[start, end) pieces of a tied span of n elements: each a multiple of world (the reduce-
+        scatter and the final all-gather use the same pieces, so the shard layout matches)."""
+        W = self.world
+        if not self._windowed and self.schedule != "end":
+            return [(0, n)]
+        m = max(W, (self.window_bytes // 4) // W * W)
+        return [(i, min(i + m, n)) for i in range(0, n, m)]
+
+    def _tie_contribution(self, pid, k):
+        """rsag, tied parameter: widen contribution k (the slice's current content) and reduce-scatter
+        it, piece by piece, into its fp32 shard (the shards are summed and all-gathered in finish())."""
+        lo, hi, uses, sides = self.split[pid]
+        src = self.reduce_buf[lo:hi] if k == 0 else sides[k - 1]
+        src.copy_(self.flat.grad[lo:hi])
+        W, sh = self.world, self.tie_rs[pid][k]
+        # the pieces are fixed by the step's first contribution: every contribution's shard and the
+        # final all-gather must share one layout even if the schedule changes at finish() (auto)
+        plan = self._tie_plan.setdefault(pid, self._tie_chunks(hi - lo))
+        for a, b in plan:
+            self._submit(("rs", src[a:b], sh[a // W:b // W]))
 
     def _issue(self, job):
         if job[0] == "rsag":
@@ -227,6 +261,8 @@ class DistributedDataParallel(nn.Module):
             o, n = lo // W, (hi - lo) // W
             self.comm.reduce_scatter(self.reduce_buf[lo:hi], self.rs32[o:o + n])
             self.comm.narrow_all_gather(self.rs32[o:o + n], self.rs16[o:o + n], self.flat.grad[lo:hi])
+        elif job[0] == "rs":
+            self.comm.reduce_scatter(job[1], job[2])
         else:
             self.comm.all_reduce(job[1])
         if self._sched_ops is not None:
@@ -284,7 +320,11 @@ class DistributedDataParallel(nn.Module):
         if k >= uses:
             return
         g = self.flat.grad[lo:hi]
-        if self.fp32:
+        if id(p) in self.tie_rs:  # rsag: reduce-scatter now, one bf16 all-gather of the summed shards later
+            self._tie_contribution(id(p), k)
+            if not final:
+                g.zero_()
+        elif self.fp32:
             # contribution 0 → the reduction buffer, later ones → side buffers (added in finish)
             self._reduce_slice(lo, hi, None if k == 0 else sides[k - 1], whole=False)
             if not final:
@@ -343,7 +383,11 @@ class DistributedDataParallel(nn.Module):
         # where both uses land in .grad at once) are reduced now, as one
         for pid, (lo, hi, uses, sides) in self.split.items():
             k = self._split_done[pid]
-            if k < uses:
+            if k < uses and pid in self.tie_rs:
+                self._tie_contribution(pid, k)  # the slice holds every missing contribution: as one
+                for sh in self.tie_rs[pid][k + 1:]:
+                    sh.zero_()
+            elif k < uses:
                 # the contributions that never signalled (e.g. autograd accumulated both uses at
                 # once, CPU path) are all in the slice: reduce it as ONE contribution
                 if self.fp32 and k > 0:
@@ -364,8 +408,19 @@ class DistributedDataParallel(nn.Module):
         if self._sched_ops is not None:
             self._sched_ops.gemm_set_sched(0)
         for pid, (lo, hi, uses, sides) in self.split.items():
+            if pid in self.tie_rs:  # rsag: sum the contributions' fp32 shards, narrow, bf16 all-gather
+                sh = self.tie_rs[pid]
+                for extra in sh[1:]:
+                    sh[0].add_(extra)
+                W = self.world
+                for a, b in self._tie_plan[pid]:
+                    self.comm.narrow_all_gather(sh[0][a // W:b // W], self.rs16[(lo + a) // W:(lo + b) // W],
+                                                self.flat.grad[lo + a:lo + b], after_rs=False)
+                continue
             for s in sides:
                 self.reduce_buf[lo:hi].add_(s)
+        if self.tie_rs:
+            self.comm.wait()
         # rsag: spans that took the fp32 all-reduce (tied contributions, unevenly split buckets) are
         # narrowed into the bf16 gradient the optimizer reads
         for lo, hi in dict.fromkeys(self._narrow):

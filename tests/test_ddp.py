@@ -189,7 +189,7 @@ def _tied_worker(rank, world, port, dtype_name, reduce_name, q, schedule="eager"
         ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_dtype=rdt, reduce_mode=mode,
                                       schedule=schedule, window_mb=0.0003)
         from replicann_amd.parallel.windows import open_window
-        if schedule == "window":  # a window mid-backward issues part of the queue (tiny budget: several pieces)
+        if schedule in ("window", "auto"):  # a window mid-backward issues part of the queue (tiny budget)
             net.mid.register_full_backward_hook(lambda *a: open_window())
         if mode == "rsag":  # every regular bucket splits into world shards: none takes the fp32 all-reduce
             assert ddp.rsag and all((hi - lo) % world == 0 and lo % world == 0 for lo, hi, _ in ddp.buckets)
@@ -210,7 +210,7 @@ def _tied_worker(rank, world, port, dtype_name, reduce_name, q, schedule="eager"
 @pytest.mark.parametrize("dtype_name,reduce_name,schedule", [
     ("float32", "float32", "eager"), ("bfloat16", "float32", "eager"), ("bfloat16", "bfloat16", "eager"),
     ("bfloat16", "rsag", "eager"), ("bfloat16", "float32", "window"), ("bfloat16", "rsag", "window"),
-    ("float32", "float32", "end")])
+    ("float32", "float32", "end"), ("bfloat16", "rsag", "auto")])
 def test_ddp_tied_split_gloo(dtype_name, reduce_name, schedule):
     """A tied parameter's two contributions are all-reduced separately (the head's during the
     backward) and summed in finish(); result = single-process gradient of the whole batch, for the
