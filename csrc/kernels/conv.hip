@@ -334,23 +334,40 @@ __global__ void __launch_bounds__(BN_T) bn_part_k(const bf16* __restrict__ a, co
         for (int j = 0; j < 8; ++j) { mu[j] = mean[cg * 8 + j]; rs[j] = rstd[cg * 8 + j]; }
     }
     if (active) {
-        for (int r = r0 + ro; r < r1; r += rpi) {
-            const long e = (long)r * C + cg * 8;
-            float v[8];
-            load8(a + e, v);
-            if (MODE == 0) {
+        // rows in batches of U: all U rows' loads are issued before any is accumulated (one memory
+        // round trip per batch instead of per row: the loop was latency-bound at ~3 TB/s); the adds
+        // stay in row order, so the sums do not depend on the batching
+        constexpr int U = 4;
+        for (int rb = r0 + ro; rb < r1; rb += U * rpi) {
+            bf16x8 av[U], xvv[U];
+            unsigned mm[U];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] += v[j] * v[j]; }
-            } else {
-                float xv[8];
-                load8(xin + e, xv);
-                if (relu) {
-                    const unsigned m = mk[e >> 3];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = ((m >> j) & 1u) ? v[j] : 0.f;
+            for (int u = 0; u < U; ++u) {
+                const int r = min(rb + u * rpi, r1 - 1);  // clamped: no per-load branch
+                const long e = (long)r * C + cg * 8;
+                av[u] = *reinterpret_cast<const bf16x8*>(a + e);
+                if (MODE == 1) {
+                    xvv[u] = *reinterpret_cast<const bf16x8*>(xin + e);
+                    mm[u] = relu ? (unsigned)mk[e >> 3] : 0xFFu;
                 }
+            }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] += v[j] * (xv[j] - mu[j]) * rs[j]; }
+            for (int u = 0; u < U; ++u) {
+                if (rb + u * rpi >= r1) break;
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (float)av[u][j];
+                if (MODE == 0) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] += v[j] * v[j]; }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float g = ((mm[u] >> j) & 1u) ? v[j] : 0.f;
+                        s0[j] += g;
+                        s1[j] += g * ((float)xvv[u][j] - mu[j]) * rs[j];
+                    }
+                }
             }
         }
     }
@@ -385,7 +402,10 @@ __global__ void bn_finalize_k(const float* __restrict__ sums, int C, int M, floa
     }
 }
 
-// y = [relu](BN(x) [+ res]); per-channel affine from (mean, rstd, w, b) or, in eval mode, running stats
+// y = [relu](BN(x) [+ res]); per-channel affine from (mean, rstd, w, b) or, in eval mode, running stats.
+// The grid stride is a multiple of C/8 for every launch of ResNet-18 (powers of two), so a thread's
+// channel group never changes: its 8 scale / shift pairs are computed once (recomputed only if the
+// group does change) and each element costs one FMA; two grid-stride iterations are loaded together.
 template <bool EVAL>
 __global__ void __launch_bounds__(256) bn_apply_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const bf16* __restrict__ b, const float* __restrict__ mean,
@@ -393,19 +413,28 @@ __global__ void __launch_bounds__(256) bn_apply_k(const bf16* __restrict__ x, co
                                                   bf16* __restrict__ y, uint8_t* __restrict__ mk, long total8, int C,
                                                   float eps, int relu) {
     const int CG = C / 8;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
-        const int c0 = (int)(i % CG) * 8;
-        float v[8], wf[8], bf[8];
-        load8(x + i * 8, v);
+    const long stride = (long)gridDim.x * 256;
+    int cprev = -1;
+    float sc[8], sh[8];
+    auto affine = [&](int c0) {
+        if (c0 == cprev) return;
+        cprev = c0;
+        float wf[8], bf[8];
         load8(w + c0, wf);
         load8(b + c0, bf);
-        float rr[8];
-        if (res) load8(res + i * 8, rr);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float sc = EVAL ? rsqrtf(rstd[c0 + j] + eps) : rstd[c0 + j];  // eval: rstd holds running var
-            float o = (v[j] - mean[c0 + j]) * sc * wf[j] + bf[j];
-            if (res) o += rr[j];
+            const float r = EVAL ? rsqrtf(rstd[c0 + j] + eps) : rstd[c0 + j];  // eval: rstd holds running var
+            sc[j] = r * wf[j];
+            sh[j] = bf[j] - mean[c0 + j] * sc[j];
+        }
+    };
+    auto out = [&](long i, const bf16x8& xv, const bf16x8& rv) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float o = __builtin_fmaf((float)xv[j], sc[j], sh[j]);
+            if (res) o += (float)rv[j];
             v[j] = relu ? fmaxf(o, 0.f) : o;
         }
         store8(y + i * 8, v);
@@ -415,10 +444,32 @@ __global__ void __launch_bounds__(256) bn_apply_k(const bf16* __restrict__ x, co
             for (int j = 0; j < 8; ++j) m |= ((float)(bf16)v[j] > 0.f ? 1u : 0u) << j;
             mk[i] = (uint8_t)m;
         }
+    };
+    long i = blockIdx.x * 256L + threadIdx.x;
+    for (; i + stride < total8; i += 2 * stride) {
+        const long i2 = i + stride;
+        const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(x + i * 8), x2 = *reinterpret_cast<const bf16x8*>(x + i2 * 8);
+        bf16x8 r1 = x1, r2 = x2;
+        if (res) {
+            r1 = *reinterpret_cast<const bf16x8*>(res + i * 8);
+            r2 = *reinterpret_cast<const bf16x8*>(res + i2 * 8);
+        }
+        affine((int)(i % CG) * 8);
+        out(i, x1, r1);
+        affine((int)(i2 % CG) * 8);
+        out(i2, x2, r2);
+    }
+    if (i < total8) {
+        const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(x + i * 8);
+        const bf16x8 r1 = res ? *reinterpret_cast<const bf16x8*>(res + i * 8) : x1;
+        affine((int)(i % CG) * 8);
+        out(i, x1, r1);
     }
 }
 
-// dx = w·rstd·(g' − Σg'/M − x̂·Σ(g'x̂)/M), g' = dy ⊙ relu'(y); optionally g' itself (residual branch)
+// dx = w·rstd·(g' − Σg'/M − x̂·Σ(g'x̂)/M), g' = dy ⊙ relu'(y); optionally g' itself (residual branch).
+// Per channel that is dx = a·g' + k1·x + k0 (a = w·rstd, k1 = −a·rstd·Σ(g'x̂)/M,
+// k0 = −a·Σg'/M − k1·mean): hoisted like the forward apply, two FMAs per element.
 __global__ void __launch_bounds__(256) bn_bwd_apply_k(const bf16* __restrict__ gy, const bf16* __restrict__ x,
                                                       const uint8_t* __restrict__ mk, const bf16* __restrict__ w,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -426,26 +477,49 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const bf16* __restrict__ g
                                                       bf16* __restrict__ gres, long total8, int C, int M, int relu) {
     const int CG = C / 8;
     const float invM = 1.f / M;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
-        const int c0 = (int)(i % CG) * 8;
-        float g[8], xv[8], wf[8];
-        load8(gy + i * 8, g);
-        load8(x + i * 8, xv);
+    const long stride = (long)gridDim.x * 256;
+    int cprev = -1;
+    float ka[8], k1[8], k0[8];
+    auto coef = [&](int c0) {
+        if (c0 == cprev) return;
+        cprev = c0;
+        float wf[8];
         load8(w + c0, wf);
-        if (relu) {
-            const unsigned m = mk[i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) g[j] = ((m >> j) & 1u) ? g[j] : 0.f;
-        }
-        if (gres) store8(gres + i * 8, g);
-        float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int c = c0 + j;
-            const float xh = (xv[j] - mean[c]) * rstd[c];
-            o[j] = wf[j] * rstd[c] * (g[j] - sums[c] * invM - xh * sums[C + c] * invM);
+            ka[j] = wf[j] * rstd[c];
+            k1[j] = -ka[j] * rstd[c] * (sums[C + c] * invM);
+            k0[j] = -ka[j] * (sums[c] * invM) - k1[j] * mean[c];
         }
+    };
+    auto out = [&](long i, const bf16x8& gv, const bf16x8& xv, unsigned m) {
+        float g[8], o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            g[j] = (float)gv[j];
+            if (relu) g[j] = ((m >> j) & 1u) ? g[j] : 0.f;
+            o[j] = __builtin_fmaf(ka[j], g[j], __builtin_fmaf(k1[j], (float)xv[j], k0[j]));
+        }
+        if (gres) store8(gres + i * 8, g);
         store8(dx + i * 8, o);
+    };
+    long i = blockIdx.x * 256L + threadIdx.x;
+    for (; i + stride < total8; i += 2 * stride) {
+        const long i2 = i + stride;
+        const bf16x8 g1 = *reinterpret_cast<const bf16x8*>(gy + i * 8), g2 = *reinterpret_cast<const bf16x8*>(gy + i2 * 8);
+        const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(x + i * 8), x2 = *reinterpret_cast<const bf16x8*>(x + i2 * 8);
+        const unsigned m1 = relu ? mk[i] : 0u, m2 = relu ? mk[i2] : 0u;
+        coef((int)(i % CG) * 8);
+        out(i, g1, x1, m1);
+        coef((int)(i2 % CG) * 8);
+        out(i2, g2, x2, m2);
+    }
+    if (i < total8) {
+        const bf16x8 g1 = *reinterpret_cast<const bf16x8*>(gy + i * 8);
+        const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(x + i * 8);
+        coef((int)(i % CG) * 8);
+        out(i, g1, x1, relu ? mk[i] : 0u);
     }
 }
 
