@@ -68,6 +68,9 @@ struct GemmArgs {
     // for outputs larger than the 256 MiB Infinity Cache, e.g. the LM-head logits: such a stream
     // cannot stay resident and would only evict the operand panels the main loop re-reads)
     int st_nt;
+    // split-K reduction only: slab s lives at ws + s·slab_step·M·N (<= 1: contiguous slabs); set when
+    // a group pre-reduction (splitk_group_k) left its partial sums in every slab_step-th slab
+    int slab_step;
 };
 
 template <int BN, int NT>
@@ -841,6 +844,25 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_k(GemmArgs p) {
     }
 }
 
+// Group pre-reduction for a tall slab stack over a small output (e.g. an implicit-conv weight gradient:
+// 64 x 576 outputs over up to 256 pixel slabs): the one-pass reduction below would run a few dozen blocks,
+// each thread walking every slab in sequence.  Here block (x, g) sums slabs [g·per, min((g+1)·per, S)) of
+// its 256 four-column groups in order and writes the sum over slab g·per (read by nobody else); the final
+// pass then adds the G group sums in order.  Fixed order throughout: deterministic.
+template <int V = 4>  // (a template: this header is compiled into many translation units)
+__global__ void __launch_bounds__(256) splitk_group_k(float* __restrict__ ws, long MN, int S, int per) {
+    const long q = blockIdx.x * 256L + threadIdx.x;
+    const long total4 = MN / 4;
+    if (q >= total4) return;
+    const int s0 = blockIdx.y * per, s1 = min(S, s0 + per);
+    float4 acc = reinterpret_cast<const float4*>(ws + (long)s0 * MN)[q];
+    for (int s = s0 + 1; s < s1; ++s) {
+        const float4 t = reinterpret_cast<const float4*>(ws + (long)s * MN)[q];
+        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+    reinterpret_cast<float4*>(ws + (long)s0 * MN)[q] = acc;
+}
+
 // Sum split-K slabs (fixed order) + epilogue.  4 consecutive columns per thread.
 template <int ACT>
 __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
@@ -850,8 +872,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
         float v[4] = {0.f, 0.f, 0.f, 0.f};
         const long MN = (long)p.M * p.N;
         const bool vec = (p.N % 4 == 0);
+        const long step = p.slab_step > 1 ? (long)p.slab_step * MN : MN;
         for (int s = 0; s < p.split; ++s) {
-            const float* w = p.ws + s * MN + e0;
+            const float* w = p.ws + s * step + e0;
             if (vec) { float4 t = *reinterpret_cast<const float4*>(w); v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w; }
             else for (int t = 0; t < 4 && e0 + t < MN; ++t) v[t] += w[t];
         }
@@ -908,7 +931,17 @@ void launch_t(GemmArgs& a, hipStream_t st) {
         ksplit<<<tiles * a.split, NT, lds, st>>>(a);
         long total4 = ((long)a.M * a.N + 3) / 4;
         int g = (int)std::min<long>((total4 + 255) / 256, 4096);
-        splitk_reduce_k<ACT><<<g, 256, 0, st>>>(a);
+        const long MN = (long)a.M * a.N;
+        if (a.split >= 16 && g < 256 && MN % 4 == 0) {  // tall stack, small output: pre-reduce in groups
+            const int G = 16, per = (a.split + G - 1) / G;
+            splitk_group_k<><<<dim3(g, (a.split + per - 1) / per), 256, 0, st>>>(a.ws, MN, a.split, per);
+            GemmArgs r = a;
+            r.split = (a.split + per - 1) / per;
+            r.slab_step = per;
+            splitk_reduce_k<ACT><<<g, 256, 0, st>>>(r);
+        } else {
+            splitk_reduce_k<ACT><<<g, 256, 0, st>>>(a);
+        }
     } else {
         kmain<<<tiles, NT, lds, st>>>(a);
     }
