@@ -280,6 +280,36 @@ __global__ void __launch_bounds__(256) maxpool_bwd_k(const bf16* __restrict__ gy
     }
 }
 
+// Max-pool backward, 8 channels per lane, one input row per grid row: blockIdx.y = (n, h), so the
+// output-row window of the row (oh range) is uniform across the block and the per-lane index math is
+// one division by the channel-chunk count (was four runtime divisions per chunk in maxpool_bwd_k).
+__global__ void __launch_bounds__(256) maxpool_bwd_rows_k(const bf16* __restrict__ gy, const uint8_t* __restrict__ idx,
+                                                          bf16* __restrict__ dx, int H, int W, int C, int K, int S,
+                                                          int P, int OH, int OW) {
+    const int CV = C / 8;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= W * CV) return;
+    const int w = j / CV, cv = j - w * CV;
+    const int n = blockIdx.y / H, h = blockIdx.y - n * H;
+    const int oh0 = max(0, (h + P - K + S) / S), oh1 = min(OH - 1, (h + P) / S);
+    const int ow0 = max(0, (w + P - K + S) / S), ow1 = min(OW - 1, (w + P) / S);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int oh = oh0; oh <= oh1; ++oh)
+        for (int ow = ow0; ow <= ow1; ++ow) {
+            const int pos = (h + P - oh * S) * K + (w + P - ow * S);  // this input's place in the window
+            const long oi = (((long)n * OH + oh) * OW + ow) * C + cv * 8;
+            const uint2 a = *reinterpret_cast<const uint2*>(idx + oi);
+            float g[8];
+            load8(gy + oi, g);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const uint32_t b = ((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xFF;
+                if ((int)b == pos) acc[e] += g[e];
+            }
+        }
+    store8(dx + (((long)n * H + h) * W + w) * C + cv * 8, acc);
+}
+
 __global__ void __launch_bounds__(256) avgpool_fwd_k(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int HW,
                                                      int C) {
     const long total = (long)N * C;
@@ -578,6 +608,11 @@ void rn_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int 
 
 void rn_maxpool_bwd(const void* gy, const void* idx, void* dx, int N, int H, int W, int C, int K, int S, int P,
                     int OH, int OW, hipStream_t st) {
+    if (C % 8 == 0 && (long)N * H < 65536) {
+        maxpool_bwd_rows_k<<<dim3((W * (C / 8) + 255) / 256, N * H), 256, 0, st>>>(
+            (const bf16*)gy, (const uint8_t*)idx, (bf16*)dx, H, W, C, K, S, P, OH, OW);
+        return;
+    }
     if (C % 8 == 0)
         maxpool_bwd_k<8><<<gridn((long)N * H * W * C / 8), 256, 0, st>>>((const bf16*)gy, (const uint8_t*)idx,
                                                                            (bf16*)dx, N, H, W, C, K, S, P, OH, OW);
