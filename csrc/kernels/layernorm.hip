@@ -289,7 +289,9 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
         return 0;
     }
     // 2048 blocks = 8192 waves (32 per CU): each wave walks M / 8192 rows with the prefetch
-    dim3 grid((M + 3) / 4 < 2048 ? (M + 3) / 4 : 2048);
+    // (REPLICANN_LN_FWD_BLOCKS overrides: A/B)
+    static const int fwd_cap = [] { const char* e = std::getenv("REPLICANN_LN_FWD_BLOCKS"); return e ? std::atoi(e) : 2048; }();
+    dim3 grid((M + 3) / 4 < fwd_cap ? (M + 3) / 4 : fwd_cap);
 #define RN_LNF(NV, R, B) ln_fwd_k<NV, R, B><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)r, (const bf16*)w, (const bf16*)b, (bf16*)y, (bf16*)h, mean, rstd, M, E, eps)
 #define RN_LNF2(NV) { if (r) { if (b) RN_LNF(NV, true, true); else RN_LNF(NV, true, false); } \
                       else { if (b) RN_LNF(NV, false, true); else RN_LNF(NV, false, false); } }
