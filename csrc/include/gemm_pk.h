@@ -546,11 +546,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                             float d[8];
 #pragma unroll
                             for (int c = 0; c < 8; ++c) v[c] = gelu_and_grad_f(v[c], d[c]);
-                            pk_st16((u32x4){pk_pack2(d[0], d[1]), pk_pack2(d[2], d[3]), pk_pack2(d[4], d[5]),
-                                            pk_pack2(d[6], d[7])},
-                                    prs, off(mh, i, nh, 2));
+                            const u32x4 du = {pk_pack2(d[0], d[1]), pk_pack2(d[2], d[3]), pk_pack2(d[4], d[5]),
+                                              pk_pack2(d[6], d[7])};
+                            // the saved derivative is read only in the backward: non-temporal when asked
+                            if (p.st_nt & 2) pk_st16_nt(du, prs, off(mh, i, nh, 2));
+                            else pk_st16(du, prs, off(mh, i, nh, 2));
                         } else {
-                            pk_st16(pu, prs, off(mh, i, nh, 2));
+                            if (p.st_nt & 2) pk_st16_nt(pu, prs, off(mh, i, nh, 2));
+                            else pk_st16(pu, prs, off(mh, i, nh, 2));
                             if (p.pre) pk_unpack8(pu, v);
 #pragma unroll
                             for (int c = 0; c < 8; ++c) v[c] = act_f<ACT>(v[c]);
@@ -598,7 +601,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                         const u32x4 ou = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
                                           pk_pack2(v[6], v[7])};
                         if constexpr (DBG & 64) asm volatile("" ::"v"(ou));         // ablation: no stores
-                        else if (p.st_nt) pk_st16_nt(ou, crs_u, o);                // wave-uniform choice
+                        else if (p.st_nt & 1) pk_st16_nt(ou, crs_u, o);            // wave-uniform choice
                         else pk_st16(ou, crs_u, (DBG & 32) ? 0xFFFFFFF0u : o);   // ablation: no traffic
                     }
                 }
@@ -854,9 +857,12 @@ extern "C" int* rn_gemm_sched_slot(int dev, hipStream_t st);
 extern "C" int rn_gemm_get_reserve();
 namespace rn_gemm_detail {
 // non-temporal output stores: plain bf16 outputs over 256 MiB (REPLICANN_GEMM_ST_NT=0 disables)
+// bit 1: the forward activation's second output (pre-activation / saved derivative, read only by the
+// backward) non-temporal too (REPLICANN_GEMM_PRE_NT=1, A/B)
 inline int rn_gemm_st_nt(const GemmArgs& a) {
     static const bool on = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT"); return !(e && e[0] == '0'); }();
-    return (on && a.split <= 1 && (long)a.M * a.N * 2 > (256L << 20)) ? 1 : 0;
+    static const bool pre = [] { const char* e = std::getenv("REPLICANN_GEMM_PRE_NT"); return e && e[0] == '1'; }();
+    return ((on && a.split <= 1 && (long)a.M * a.N * 2 > (256L << 20)) ? 1 : 0) | (pre && a.pre ? 2 : 0);
 }
 }  // namespace rn_gemm_detail
 namespace rn_gemm_detail {
