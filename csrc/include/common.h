@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 typedef __bf16 bf16;
 typedef short  s16x8 __attribute__((ext_vector_type(8)));
 typedef short  s16x4 __attribute__((ext_vector_type(4)));
@@ -269,10 +271,53 @@ __global__ void __launch_bounds__(256) rn_colsum_k(const float* __restrict__ in,
     if (lane == 0) __hip_atomic_store(&rn_colsum_cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Short inputs (R <= RN_COLSUM1_R rows, e.g. the GEMM epilogue's 256 per-tile-row bias partials or
+// the attention backward's 1024 per-block qkv-bias partials):
+// ONE block of 16 waves per 64 columns sums all rows — each wave a strided row subset in 16-deep
+// load batches (adds in row order), the 16 wave sums combined in fixed order through LDS.  No
+// second stage, no arrival ticket: one load round trip per 16 rows per wave instead of the
+// two-stage kernel's slab write + ticket + slab read.  Bitwise reproducible (fixed order).
+// (gpt2-small step: 49 column sums 0.448 -> 0.344 ms at R <= 512, profiles/r3s_resume_xent_gelu.txt)
+constexpr int RN_COLSUM1_R = 1024;
+
+__global__ void __launch_bounds__(1024) rn_colsum1_k(const float* __restrict__ in, int R, int C, RnColOut out) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (c < C) {
+        for (int rb = w; rb < R; rb += 256) {
+            float t[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t[u] = in[(long)min(rb + 16 * u, R - 1) * C + c];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += (rb + 16 * u < R) ? t[u] : 0.f;
+        }
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc += red[i][lane];
+    const int k = c / out.seg, o = c - k * out.seg;
+    if (out.o32[k]) out.o32[k][o] = acc + (out.accum[k] == 1 ? out.o32[k][o] : 0.f);
+    if (out.o16[k]) out.o16[k][o] = (__bf16)(acc + (out.accum[k] ? (float)out.o16[k][o] : 0.f));
+}
+
+static inline bool rn_colsum1_on() {
+    static const bool on = [] { const char* e = std::getenv("REPLICANN_COLSUM_1PASS"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 // Segmented column reduction: out.seg columns per output segment (≤ 3 segments).
 // tmp must hold RN_COLRED_S * C floats.
 static inline void rn_colreduce_seg(const float* in, int R, int C, float* tmp, const RnColOut& out,
                                     hipStream_t st) {
+    if (R <= RN_COLSUM1_R && rn_colsum1_on()) {
+        rn_colsum1_k<<<(C + 63) / 64, 1024, 0, st>>>(in, R, C, out);
+        return;
+    }
     // >= 32 rows per block (8-deep load batches for each of its 4 waves), at most RN_COLRED_S blocks
     int S = (R + 31) / 32;
     S = S < 1 ? 1 : (S > RN_COLRED_S ? RN_COLRED_S : S);
