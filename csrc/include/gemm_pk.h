@@ -856,13 +856,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 extern "C" int* rn_gemm_sched_slot(int dev, hipStream_t st);
 extern "C" int rn_gemm_get_reserve();
 namespace rn_gemm_detail {
-// non-temporal output stores: plain bf16 outputs over 256 MiB (REPLICANN_GEMM_ST_NT=0 disables;
-// REPLICANN_GEMM_ST_NT_MB moves the size threshold, A/B)
+// non-temporal output stores: plain bf16 outputs over 1 GiB (REPLICANN_GEMM_ST_NT=0 disables;
+// REPLICANN_GEMM_ST_NT_MB moves the size threshold; 256 MiB also caught outputs the next kernel reads
+// at once, +0.14-0.4 ms per GPT-2-small step, profiles/r3s_resume_xent_gelu.txt item 17)
 // bit 1: the forward activation's second output (pre-activation / saved derivative, read only by the
 // backward) non-temporal too (REPLICANN_GEMM_PRE_NT=1, A/B)
 inline int rn_gemm_st_nt(const GemmArgs& a) {
     static const bool on = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT"); return !(e && e[0] == '0'); }();
-    static const long thr = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT_MB"); return (e ? std::atol(e) : 256L) << 20; }();
+    static const long thr = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT_MB"); return (e ? std::atol(e) : 1024L) << 20; }();
     static const bool pre = [] { const char* e = std::getenv("REPLICANN_GEMM_PRE_NT"); return e && e[0] == '1'; }();
     return ((on && a.split <= 1 && (long)a.M * a.N * 2 > thr) ? 1 : 0) | (pre && a.pre ? 2 : 0);
 }
