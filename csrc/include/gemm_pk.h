@@ -548,12 +548,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                             for (int c = 0; c < 8; ++c) v[c] = gelu_and_grad_f(v[c], d[c]);
                             const u32x4 du = {pk_pack2(d[0], d[1]), pk_pack2(d[2], d[3]), pk_pack2(d[4], d[5]),
                                               pk_pack2(d[6], d[7])};
-                            // the saved derivative is read only in the backward: non-temporal when asked
-                            if (p.st_nt & 2) pk_st16_nt(du, prs, off(mh, i, nh, 2));
-                            else pk_st16(du, prs, off(mh, i, nh, 2));
+                            pk_st16(du, prs, off(mh, i, nh, 2));
                         } else {
-                            if (p.st_nt & 2) pk_st16_nt(pu, prs, off(mh, i, nh, 2));
-                            else pk_st16(pu, prs, off(mh, i, nh, 2));
+                            pk_st16(pu, prs, off(mh, i, nh, 2));
                             if (p.pre) pk_unpack8(pu, v);
 #pragma unroll
                             for (int c = 0; c < 8; ++c) v[c] = act_f<ACT>(v[c]);
@@ -859,13 +856,12 @@ namespace rn_gemm_detail {
 // non-temporal output stores: plain bf16 outputs over 1 GiB (REPLICANN_GEMM_ST_NT=0 disables;
 // REPLICANN_GEMM_ST_NT_MB moves the size threshold; 256 MiB also caught outputs the next kernel reads
 // at once, +0.14-0.4 ms per GPT-2-small step, profiles/r3s_resume_xent_gelu.txt item 17)
-// bit 1: the forward activation's second output (pre-activation / saved derivative, read only by the
-// backward) non-temporal too (REPLICANN_GEMM_PRE_NT=1, A/B)
+// (a non-temporal store of the activation epilogue's second output, read only by the backward, was
+// measured as no change and removed in round 4)
 inline int rn_gemm_st_nt(const GemmArgs& a) {
     static const bool on = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT"); return !(e && e[0] == '0'); }();
     static const long thr = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT_MB"); return (e ? std::atol(e) : 1024L) << 20; }();
-    static const bool pre = [] { const char* e = std::getenv("REPLICANN_GEMM_PRE_NT"); return e && e[0] == '1'; }();
-    return ((on && a.split <= 1 && (long)a.M * a.N * 2 > thr) ? 1 : 0) | (pre && a.pre ? 2 : 0);
+    return (on && a.split <= 1 && (long)a.M * a.N * 2 > thr) ? 1 : 0;
 }
 }  // namespace rn_gemm_detail
 namespace rn_gemm_detail {

@@ -59,24 +59,15 @@ struct AttnArgs {
     // lse units: the D = 64 forward kernels store log2(Σ exp) in base-2 units (the backward then
     // needs one FMA per score, exp2(s·scale·log2e − lse2)); the generic forward stores natural log.
     int lse_log2;
-    // block order (1-D grid of B·H·nblk blocks): 0 = head-interleaved (block L: head L % (B·H), the
-    // heaviest causal blocks of all heads first); 1 = XCD-grouped — each XCD (blocks b, b+8, …, dealt
-    // round-robin) works through a contiguous range of heads, all blocks of a head back to back
-    int xcd_map;
 };
 
 // (bh, block) of this workgroup; `reverse`: the head's heaviest (last) causal block first
 RN_DEV void blk_map(const AttnArgs& p, int nblk, bool reverse, int& bh, int& blk) {
-    const int BH = p.B * p.H, L = blockIdx.x, n = BH * nblk;
-    int i;
-    if (p.xcd_map && (n & 7) == 0) {
-        const int w = (L & 7) * (n >> 3) + (L >> 3);
-        bh = w / nblk;
-        i = w - bh * nblk;
-    } else {
-        bh = L % BH;
-        i = L / BH;
-    }
+    // head-interleaved 1-D grid of B·H·nblk blocks: block L works on head L % (B·H), so the
+    // heaviest causal blocks of every head are dispatched first
+    const int BH = p.B * p.H, L = blockIdx.x;
+    const int i = L / BH;
+    bh = L % BH;
     blk = reverse ? nblk - 1 - i : i;
 }
 
@@ -1330,14 +1321,9 @@ void attn_bwd_mfma(AttnArgs& a, hipStream_t st) {
     RN_DISPATCH3V(attn_bwd_dkdv64_k, g1, 2 * (2 * kTB<D> + 2048), st, a, (D == 128 ? 1 : 3), 1, D);
 }
 
-// REPLICANN_ATTN_XCD=1 selects the XCD-grouped block order.  Measured slower (GPT-2-small causal
-// B64: fwd 0.177 -> 0.199 ms, bwd 0.571 -> 0.597 ms): a head's 8 query blocks then read the same K/V
-// tiles at the same moment, and the head-interleaved default (heaviest blocks of every head first)
-// balances the causal load better.  Kept for A/B on other shapes.
-int xcd_order() {
-    const char* e = std::getenv("REPLICANN_ATTN_XCD");
-    return e ? std::atoi(e) : 0;
-}
+// Block order: head-interleaved (blk_map).  An XCD-grouped order was measured slower (GPT-2-small
+// causal B64: fwd 0.177 -> 0.199 ms, bwd 0.571 -> 0.597 ms: a head's 8 query blocks then read the
+// same K/V tiles at the same moment) and was removed in round 4.
 
 // the MFMA kernels' requirements: D ∈ {32, 64, 128} and 16-B aligned rows (strides in elements)
 bool mfma_head(int D) { return D == 32 || D == 64 || D == 128; }
@@ -1359,24 +1345,17 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
     a.o_sb = strides[9]; a.o_st = strides[10]; a.o_sh = strides[11];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
     a.scale = scale; a.p_drop = p_drop; a.seed = seed;
-    a.xcd_map = xcd_order();
     const bool fast = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast && D != 64) {
         if (D == 32) attn_fwd_mfma<32>(a, st);
         else attn_fwd_mfma<128>(a, st);
     } else if (fast) {
         dim3 grid(B * H * ((Tq + 127) / 128));
-        // REPLICANN_ATTN_FWD=1 selects the original single-loop kernel, 2 the split-loop v2, 3 (default)
-        // v2 with the LEAN softmax bookkeeping (read per call so one process can A/B them); no bias /
-        // dropout in v2/v3, 3 blocks per CU
-        const char* ev = std::getenv("REPLICANN_ATTN_FWD");
-        const int var = ev ? std::atoi(ev) : 3;  // 3 = v2 + LEAN softmax bookkeeping
-        if (!bias && p_drop == 0.f && var >= 3) {
+        // plain causal / non-causal: the split-loop v2 kernel with the LEAN softmax bookkeeping
+        // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
+        if (!bias && p_drop == 0.f) {
             if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
             else attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
-        } else if (!bias && p_drop == 0.f && var == 2) {
-            if (causal) attn_fwd64v2_k<true, 3><<<grid, 256, 32768, st>>>(a);
-            else attn_fwd64v2_k<false, 3><<<grid, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
         }
@@ -1404,7 +1383,6 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     a.dk_sb = s[18]; a.dk_st = s[19]; a.dk_sh = s[20]; a.dv_sb = s[21]; a.dv_st = s[22]; a.dv_sh = s[23];
     a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.D = D; a.causal = causal; a.bias_b = bias_b;
     a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.dk32 = dk32; a.dv32 = dv32; a.bsum = bsum;
-    a.xcd_map = xcd_order();
     const bool fast = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) &&
                       (a.do_st % 8 == 0) && (a.o_st % 8 == 0) && (a.dq_st % 4 == 0) && (a.dk_st % 4 == 0) &&
                       (a.dv_st % 4 == 0) && (a.o_sh % 8 == 0) && (a.do_sh % 8 == 0);
@@ -1419,22 +1397,17 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         // dQ first: it also produces delta = rowsum(dO∘O), which the dK/dV kernel reads
         dim3 g2(B * H * ((Tq + 63) / 64));
         dim3 g1(B * H * ((Tk + 63) / 64));
-        // REPLICANN_ATTN_DQ: 2 (default) = two 64-query groups per wave (plain causal / non-causal;
-        // bwd -11 % at GPT-2-small shapes), 1 = one
-        const char* eq = std::getenv("REPLICANN_ATTN_DQ");
-        const int dqv = eq ? std::atoi(eq) : 2;
-        if (dqv >= 2 && !bias && p_drop == 0.f) {
+        // plain causal / non-causal: two 64-query groups per wave in dQ (bwd -11 % at GPT-2-small
+        // shapes) and two 64-key groups per wave in dK/dV (-2.4 %, occupancy 2 at 240 VGPRs);
+        // bias / dropout: one group per wave
+        if (!bias && p_drop == 0.f) {
             dim3 g2b(B * H * ((Tq + 127) / 128));
             if (causal) attn_bwd_dq64_k<true, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
             else attn_bwd_dq64_k<false, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         }
-        // REPLICANN_ATTN_DKDV: 2 (default) = two 64-key groups per wave (plain causal / non-causal;
-        // -2.4 % bwd at GPT-2-small shapes, occupancy 2 at 240 VGPRs), 1 = one
-        const char* ek = std::getenv("REPLICANN_ATTN_DKDV");
-        const int kvv = ek ? std::atoi(ek) : 2;
-        if (kvv >= 2 && !bias && p_drop == 0.f) {
+        if (!bias && p_drop == 0.f) {
             dim3 g1b(B * H * ((Tk + 127) / 128));
             if (causal) attn_bwd_dkdv64_k<true, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
             else attn_bwd_dkdv64_k<false, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);

@@ -131,12 +131,26 @@ void rn_gemm_set_reserve(int r) { g_reserve = r < 0 ? 0 : (r > 128 ? 128 : r & ~
 int rn_gemm_get_reserve() { return g_reserve.load(); }
 
 // Counter slots of the dynamic schedule: a per-device pool of self-resetting counter blocks
-// (PK_SCHED_INTS ints each), handed out round robin.  Launches that share a slot are ordered on
-// one stream (the compute stream runs every GEMM), and a launch leaves its slot zeroed.
+// (PK_SCHED_INTS ints each).  A slot must never be used by two launches that can run at the same
+// time, so slots are keyed by stream:
+//   * eager launches: each stream gets its own block of kSlotsPerStream slots, used round robin
+//     (launches on one stream are ordered, and a launch leaves its slot zeroed); at most
+//     kEagerStreams streams per device, further streams take the static walk;
+//   * launches recorded into a graph (stream capture): a slot of their own, never handed out again
+//     (a replay can run beside eager work or another graph); once that part of the pool is used
+//     up, captured launches take the static walk.
 constexpr int kSchedSlots = 256;
+constexpr int kSlotsPerStream = 16;
+constexpr int kEagerStreams = 8;  // slots [0, 128): eager; [128, 256): captured launches
 static std::mutex g_pool_mu;
 static int* g_pool[64] = {};
-static std::atomic<unsigned> g_next_slot{0};
+struct SlotState {
+    hipStream_t streams[kEagerStreams] = {};
+    unsigned next[kEagerStreams] = {};
+    int n_streams = 0;
+    int next_captured = kSlotsPerStream * kEagerStreams;
+};
+static SlotState g_slots[64];
 int rn_gemm_sched_init(int dev) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     if (dev < 0 || dev >= 64) return -1;
@@ -156,13 +170,22 @@ int rn_gemm_sched_init(int dev) {
 }
 int* rn_gemm_sched_slot(int dev, hipStream_t st) {
     if (rn_gemm_get_sched() == 0 || dev < 0 || dev >= 64) return nullptr;
-    if (!g_pool[dev]) {
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        (void)hipStreamIsCapturing(st, &cap);
-        if (cap != hipStreamCaptureStatusNone || rn_gemm_sched_init(dev) != 0) return nullptr;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cap);
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    if (!g_pool[dev] && (capturing || rn_gemm_sched_init(dev) != 0)) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    SlotState& ss = g_slots[dev];
+    int s = -1;
+    if (capturing) {
+        if (ss.next_captured < kSchedSlots) s = ss.next_captured++;
+    } else {
+        int k = 0;
+        while (k < ss.n_streams && ss.streams[k] != st) ++k;
+        if (k == ss.n_streams && ss.n_streams < kEagerStreams) ss.streams[ss.n_streams++] = st;
+        if (k < ss.n_streams) s = k * kSlotsPerStream + (int)(ss.next[k]++ % kSlotsPerStream);
     }
-    const unsigned s = g_next_slot.fetch_add(1) % kSchedSlots;
-    return g_pool[dev] + (size_t)s * rn_gemm_detail::PK_SCHED_INTS;
+    return s < 0 ? nullptr : g_pool[dev] + (size_t)s * rn_gemm_detail::PK_SCHED_INTS;
 }
 
 // Workspace floats needed for a split-K launch.

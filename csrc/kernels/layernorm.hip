@@ -143,8 +143,7 @@ template <int NV, bool GH, bool DXS>
 __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ gh,
                                                 const bf16* __restrict__ h, const bf16* __restrict__ w,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                bf16* __restrict__ dx, float* __restrict__ part, int M, int E,
-                                                int hnt) {
+                                                bf16* __restrict__ dx, float* __restrict__ part, int M, int E) {
     constexpr int Q = DXS ? 3 : 2;
     __shared__ float red[3][NV * 512];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -175,10 +174,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
             const int c = lane + i * 64;
             if (c < nvec) {
                 if constexpr (GH) gn[i] = *reinterpret_cast<const bf16x8*>(gh + (long)rr * E + c * 8);
-                // hnt (REPLICANN_LN_BWD_NT, A/B): the saved forward input, written long before, read
-                // non-temporally so it does not evict the fresh dy / dx from the Infinity Cache
-                if (hnt) hn[i] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(h + (long)rr * E + c * 8));
-                else hn[i] = *reinterpret_cast<const bf16x8*>(h + (long)rr * E + c * 8);
+                hn[i] = *reinterpret_cast<const bf16x8*>(h + (long)rr * E + c * 8);
                 dn[i] = *reinterpret_cast<const bf16x8*>(dy + (long)rr * E + c * 8);
             }
         }
@@ -293,8 +289,7 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
         return 0;
     }
     // 2048 blocks = 8192 waves (32 per CU): each wave walks M / 8192 rows with the prefetch
-    // (REPLICANN_LN_FWD_BLOCKS overrides: A/B)
-    static const int fwd_cap = [] { const char* e = std::getenv("REPLICANN_LN_FWD_BLOCKS"); return e ? std::atoi(e) : 2048; }();
+    constexpr int fwd_cap = 2048;
     dim3 grid((M + 3) / 4 < fwd_cap ? (M + 3) / 4 : fwd_cap);
 #define RN_LNF(NV, R, B) ln_fwd_k<NV, R, B><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)r, (const bf16*)w, (const bf16*)b, (bf16*)y, (bf16*)h, mean, rstd, M, E, eps)
 #define RN_LNF2(NV) { if (r) { if (b) RN_LNF(NV, true, true); else RN_LNF(NV, true, false); } \
@@ -336,8 +331,7 @@ int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, cons
     const int Q = dxs16 ? 3 : 2;
     float* part = ws;
     float* tmp = ws + (long)B * Q * E;
-    static const int hnt = [] { const char* e = std::getenv("REPLICANN_LN_BWD_NT"); return e && e[0] == '1' ? 1 : 0; }();
-#define RN_LNB(NV, G, D) ln_bwd_k<NV, G, D><<<B, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, E, hnt)
+#define RN_LNB(NV, G, D) ln_bwd_k<NV, G, D><<<B, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, E)
 #define RN_LNB2(NV) { if (gh) { if (dxs16) RN_LNB(NV, true, true); else RN_LNB(NV, true, false); } \
                       else { if (dxs16) RN_LNB(NV, false, true); else RN_LNB(NV, false, false); } }
     if (nv <= 1) RN_LNB2(1) else if (nv <= 2) RN_LNB2(2) else if (nv <= 4) RN_LNB2(4) else if (nv <= 8) RN_LNB2(8)

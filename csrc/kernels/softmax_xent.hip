@@ -130,11 +130,11 @@ __global__ void __launch_bounds__(TPB) xent_fwd_k(bf16* __restrict__ logits, con
     }
 }
 
-// Single-pass variant for V % 8 == 0, V <= 8 * 1024 * CH: the 1024-thread block
-// keeps its whole row in registers (CH 16-byte chunks per thread), so the row is
-// read from HBM once and (GRAD) written once — the two-pass kernel above re-reads
-// it.  Same outputs and the same fixed reduction order for every launch.
-template <int CH, bool GRAD>
+// Loss-only single-pass row kernel (evaluation) for V % 8 == 0, V <= 8 * 1024 * CH: the 1024-thread
+// block keeps its whole row in registers (CH 16-byte chunks per thread), so the row is read from HBM
+// once.  Same outputs and the same fixed reduction order for every launch.  (Its round-1 gradient
+// form was replaced by xent_row2_k and removed in round 4.)
+template <int CH>
 __global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                    float* __restrict__ loss, float* __restrict__ lse_out, int V,
                                                    int nvalid, long ignore) {
@@ -174,22 +174,6 @@ __global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, co
         lse_out[blockIdx.x] = lse;
         loss[blockIdx.x] = ign ? 0.f : lse - xt;
     }
-    if constexpr (GRAD) {
-        const float z = ign ? 0.f : 1.f;
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            const int i = threadIdx.x + k * 1024;
-            if (i < n8) {
-                float f[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int c = i * 8 + j;
-                    f[j] = (c < nvalid ? __expf((float)v[k][j] - lse) - (c == t ? 1.f : 0.f) : 0.f) * z;
-                }
-                store8(row + i * 8, f);
-            }
-        }
-    }
 }
 
 // Fused-gradient row kernel, v2 (the default for V % 8 == 0, V <= 8·1024·CH, write_grad):
@@ -200,10 +184,10 @@ __global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, co
 //   * base-2 throughout (x·log2e folded into one FMA with the max), padded-column and target
 //     masks only where a chunk straddles them.
 // Output differs from xent_row_k by the extra bf16 rounding of e (≤ 1 bf16 ulp of the gradient).
-// NT (REPLICANN_XENT_NT, A/B): bit 0 = non-temporal logits loads, bit 1 = non-temporal gradient stores
-// (the 6.6 GB GPT-2 logits stream cannot stay in any cache between the LM-head GEMM, this pass and the
-// backward GEMMs).
-template <int CH, int NT>
+// The logits are loaded non-temporally (the 6.6 GB GPT-2 logits stream cannot stay in any cache
+// between the LM-head GEMM, this pass and the backward GEMMs: 2.42 -> 2.38 ms); the gradient stores
+// stay plain (non-temporal stores measured 1.5x slower, 3.54-3.68 ms, gpu_r3zt).
+template <int CH>
 __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                     float* __restrict__ loss, float* __restrict__ lse_out, int V,
                                                     int nvalid, long ignore) {
@@ -221,8 +205,7 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
     for (int k = 0; k < CH; ++k) {
         const int i = threadIdx.x + k * 1024;
         if (i < n8) {
-            if constexpr (NT & 1) v[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(row + i * 8));
-            else v[k] = *reinterpret_cast<const bf16x8*>(row + i * 8);
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(row + i * 8));
             if (i * 8 + 8 <= nvalid) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) m = fmaxf(m, (float)v[k][j]);
@@ -294,17 +277,10 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
     for (int k = 0; k < CH; ++k) {
         const int i = threadIdx.x + k * 1024;
         if (i < n8) {
-            if constexpr (NT & 2) {
-                bf16x8 g;
+            float g[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) g[j] = (bf16)((float)v[k][j] * f);
-                __builtin_nontemporal_store(g, reinterpret_cast<bf16x8*>(row + i * 8));
-            } else {
-                float g[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) g[j] = (float)v[k][j] * f;
-                store8(row + i * 8, g);
-            }
+            for (int j = 0; j < 8; ++j) g[j] = (float)v[k][j] * f;
+            store8(row + i * 8, g);
         }
     }
     // the one-hot term: the thread that owns column t rewrites it (a runtime index into g[] was a
@@ -358,22 +334,11 @@ void rn_xent_fwd(void* logits, const int64_t* tgt, float* loss, float* lse, int 
                  int write_grad, hipStream_t st) {
     if (V % 8 == 0 && V <= 8 * 1024 * 8) {
         const int ch = (V / 8 + 1023) / 1024;
-        // REPLICANN_XENT=1: the round-1 row kernel (two block reductions, two exps per element)
-        const char* ev = std::getenv("REPLICANN_XENT");
-        const bool v2 = !(ev && ev[0] == '1');
-        // default 1: NT loads 2.42 -> 2.38 ms; NT stores measured 1.5x SLOWER (3.54-3.68 ms, gpu_r3zt)
-        static const int nt = [] { const char* e = std::getenv("REPLICANN_XENT_NT"); return e ? (std::atoi(e) & 3) : 1; }();
-#define RN_XR2(C) { if (nt == 0) xent_row2_k<C, 0><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
-                    else if (nt == 1) xent_row2_k<C, 1><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
-                    else if (nt == 2) xent_row2_k<C, 2><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
-                    else xent_row2_k<C, 3><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); }
-#define RN_XR(C) { if (write_grad && v2) RN_XR2(C) \
-                   else if (write_grad) xent_row_k<C, true><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
-                   else xent_row_k<C, false><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); }
+#define RN_XR(C) { if (write_grad) xent_row2_k<C><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); \
+                   else xent_row_k<C><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore); }
         if (ch <= 1) RN_XR(1) else if (ch <= 2) RN_XR(2) else if (ch <= 4) RN_XR(4) else if (ch <= 7) RN_XR(7)
         else RN_XR(8)
 #undef RN_XR
-#undef RN_XR2
         return;
     }
     if (write_grad) xent_fwd_k<true><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);

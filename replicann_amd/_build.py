@@ -118,16 +118,26 @@ def _sources():
 
 def source_digest() -> str:
     """Location-independent digest of what ``_C.so`` is built from: the relative path and bytes
-    of every compiled source and shared header, plus the build-mode flags.  Written next to the
-    library at link time; ``_ext.load()`` recomputes it and refuses a library built from other
-    sources (a stale ``_C.so`` pushed with a newer tree)."""
+    of every compiled source and shared header.  Written next to the library at link time (first
+    line of ``_C.srcstamp``); ``_ext.load()`` recomputes it and refuses a library built from other
+    sources (a stale ``_C.so`` pushed with a newer tree).  The build-mode ``-D`` flags are recorded
+    on the stamp's second line (``build_defs()``) instead of being folded in here: they describe
+    the build, and a process whose environment differs from the build's must still load it."""
     h = hashlib.sha1()
     for p in sorted(_sources() + sorted((CSRC / "include").glob("*.h"))):
         h.update(str(p.relative_to(ROOT)).encode())
         h.update(b"\0")
         h.update(p.read_bytes())
-    h.update(" ".join(f for f in HIP_FLAGS if f.startswith("-D")).encode())
     return h.hexdigest()
+
+
+def build_defs() -> str:
+    """The preprocessor definitions of this build mode (debug checks, dev ablations, A/B defs)."""
+    return " ".join(f for f in HIP_FLAGS if f.startswith("-D"))
+
+
+def stamp_text() -> str:
+    return f"{source_digest()}\ndefs: {build_defs()}\n"
 
 
 @contextlib.contextmanager
@@ -188,7 +198,7 @@ def _build_locked(verbose, jobs):
         objs = list(ex.map(lambda s: _compile(s, hdr, torch_inc), srcs))
     link_key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
     stamp = OUT.with_suffix(".stamp")
-    digest = source_digest()
+    digest = stamp_text()
     if OUT.exists() and stamp.exists() and stamp.read_text() == link_key:
         if not SRC_STAMP.exists() or SRC_STAMP.read_text() != digest:
             SRC_STAMP.write_text(digest)

@@ -22,17 +22,36 @@ _EXPLICIT = bool(os.environ.get("REPLICANN_SO"))
 
 
 def check_fresh(so: Path = _SO) -> None:
-    """Raise unless ``so`` was built from the sources in this tree (``_build.source_digest``)."""
+    """Raise unless ``so`` was built from the sources in this tree (``_build.source_digest``).
+
+    Only the source digest (the stamp's first line) is compared: the build's ``-D`` flags are
+    recorded on its second line and describe the library, whatever the loading process's
+    environment says.  Without a ``csrc/`` tree (an installed package ships ``_C.so`` and its stamp
+    but no sources) there is nothing to compare against and the library is trusted."""
     from . import _build
 
     stamp = so.with_suffix(".srcstamp")
     if not stamp.exists():
         raise RuntimeError(f"{so} has no source stamp ({stamp.name}); rebuild with `python -m replicann_amd._build`")
+    if not (_build.CSRC / "kernels").is_dir():
+        return
+    have = stamp.read_text().splitlines()[0].strip() if stamp.read_text().strip() else ""
     want = _build.source_digest()
-    if stamp.read_text().strip() != want:
+    if have != want:
         raise RuntimeError(f"{so} is stale: it was built from other csrc/ sources than this tree's "
-                           f"(stamp {stamp.read_text().strip()[:12]} != {want[:12]}); rebuild with "
+                           f"(stamp {have[:12]} != {want[:12]}); rebuild with "
                            "`python -m replicann_amd._build`")
+
+
+def build_defs(so: Path = _SO) -> str:
+    """The ``-D`` flags the loaded library was built with (from its stamp)."""
+    stamp = so.with_suffix(".srcstamp")
+    for line in (stamp.read_text().splitlines() if stamp.exists() else []):
+        if line.startswith("defs:"):
+            return line[5:].strip()
+    return ""
+
+
 _state = {"loaded": False, "error": None}
 _ref = {"on": False}  # process-wide: autograd runs backward on its own device threads
 

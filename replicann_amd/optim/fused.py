@@ -105,6 +105,27 @@ class _FlatOptimizer:
     def _extra_state(self):
         return []
 
+    def _load_flat(self, sd, key, dst):
+        """Restore one flat fp32 state tensor, remapping it when the checkpoint's parameter layout
+        (``sd["layout"]``) differs from this buffer's (e.g. a fusion-group repacking since)."""
+        src = sd[key]
+        lay = sd.get("layout")
+        if lay is None:
+            if src.numel() != dst.numel():
+                raise ValueError(f"optimizer state {key!r} has {src.numel()} elements, the model {dst.numel()}")
+            import warnings
+            warnings.warn("optimizer state has no parameter layout record (older checkpoint): "
+                          "assuming it matches this model's flat layout")
+            dst.copy_(src)
+            return
+        lay = [tuple(e) for e in lay]
+        if lay == self.flat.layout():
+            dst.copy_(src)
+        else:
+            tmp = torch.zeros_like(dst)
+            self.flat.remap_from(lay, src.to(dst.device), tmp)
+            dst.copy_(tmp)
+
     def skipped_last_step(self):
         return bool(self.norm_buf[1].item())
 
@@ -160,14 +181,15 @@ class FusedAdamW(_FlatOptimizer):
         return [self.m, self.v]
 
     def state_dict(self):
-        return {"step": self.step_count, "master": self.master, "m": self.m, "v": self.v, "lr": self.lr}
+        return {"step": self.step_count, "master": self.master, "m": self.m, "v": self.v, "lr": self.lr,
+                "layout": self.flat.layout()}
 
     def load_state_dict(self, sd):
         self.step_count = sd["step"]
         self.norm_buf[2] = float(self.step_count)
-        self.master.copy_(sd["master"])
-        self.m.copy_(sd["m"])
-        self.v.copy_(sd["v"])
+        self._load_flat(sd, "master", self.master)
+        self._load_flat(sd, "m", self.m)
+        self._load_flat(sd, "v", self.v)
         self.lr = sd.get("lr", self.lr)
         # the parameters themselves are NOT re-derived from the fp32 master: the model state_dict
         # carries the exact (stochastically rounded) bf16 copy the saving run used, and a
@@ -217,13 +239,14 @@ class FusedSGD(_FlatOptimizer):
         return [self.buf]
 
     def state_dict(self):
-        return {"step": self.step_count, "master": self.master, "buf": self.buf, "lr": self.lr}
+        return {"step": self.step_count, "master": self.master, "buf": self.buf, "lr": self.lr,
+                "layout": self.flat.layout()}
 
     def load_state_dict(self, sd):
         self.step_count = sd["step"]
         self.norm_buf[2] = float(self.step_count)
-        self.master.copy_(sd["master"])
-        self.buf.copy_(sd["buf"])  # parameters: from the model state_dict (see FusedAdamW)
+        self._load_flat(sd, "master", self.master)
+        self._load_flat(sd, "buf", self.buf)  # parameters: from the model state_dict (see FusedAdamW)
 
 
 def cosine_lr(step, base_lr, warmup, total, min_ratio=0.1):

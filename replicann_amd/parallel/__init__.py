@@ -26,6 +26,19 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def nccl_options():
+    """ProcessGroupNCCL (RCCL) options of the world > 1 step: collectives on a HIGH-priority stream.
+
+    The DDP schedule (parallel/ddp.py, windows.py) issues bucket collectives beside the attention
+    backward so that RCCL's workgroups interleave with that kernel's short workgroups; that only
+    works if the command processor dispatches them ahead of the compute stream's queued work, which
+    is what the native communicator's stream (csrc/comm) and the 1-GPU proxy measurements
+    (profiles/ddp_window_proxy_r3ze.txt) assume.  torch's default is a normal-priority stream."""
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
+
+
 def init_distributed(backend=None, timeout_s=600, force=False):
     """Initialise torch.distributed from env:// if WORLD_SIZE>1 (or ``force``: also a
     one-process group, for the one-GPU rehearsal of the data-parallel step).
@@ -58,8 +71,10 @@ def init_distributed(backend=None, timeout_s=600, force=False):
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device
+            kw["pg_options"] = nccl_options()
         dist.init_process_group(**kw)
     return rank, local_rank, world, device
 
 
-__all__ = ["DistributedDataParallel", "NativeComm", "TorchComm", "dist_env", "init_distributed", "make_comm"]
+__all__ = ["DistributedDataParallel", "NativeComm", "TorchComm", "dist_env", "init_distributed", "make_comm",
+           "nccl_options"]

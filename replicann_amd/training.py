@@ -96,6 +96,9 @@ class TrainConfig:
     metrics_path: str | None = None
     checkpoint: str | None = None
     resume: str | None = None
+    # resume a checkpoint saved by another world size: model / optimizer state only, fresh per-rank
+    # RNG streams and data cursors (always on for evaluation, which never uses them)
+    allow_world_change: bool = False
     seed: int = 0
     device: str | None = None
     data: str | None = None       # LM token shards (comma-separated paths / globs); None = synthetic
@@ -153,7 +156,9 @@ class Trainer:
         self._tuned = False
         self._resume_state = None
         if cfg.resume:
-            self.step_idx, _, self._resume_state = load_checkpoint(cfg.resume, self.model, self.opt)
+            self.step_idx, _, self._resume_state = load_checkpoint(
+                cfg.resume, self.model, self.opt,
+                allow_world_change=cfg.allow_world_change or cfg.data_mode != "train")
             tun = ((self._resume_state or {}).get("extra") or {}).get("gemm_tuning")
             if tun and self.device.type == "cuda":
                 torch.ops.replicann.gemm_tuning_load(tun)

@@ -123,6 +123,23 @@ class FlatParams:
         """[(param, offset, numel)] in layout order."""
         return [(p, o, p.numel()) for p, o in zip(self.params, self.offsets)]
 
+    def layout(self):
+        """[(name, offset, numel)] of every parameter in layout order: what a raw flat-buffer
+        snapshot (optimizer master / moments) means.  Saved with optimizer state so a checkpoint
+        written under another packing (fusion groups, alignment) is remapped, never misread."""
+        return [(self.names.get(id(p), f"#{i}"), int(o), int(p.numel()))
+                for i, (p, o) in enumerate(zip(self.params, self.offsets))]
+
+    def remap_from(self, saved_layout, flat_tensor, out):
+        """Copy a flat tensor laid out by ``saved_layout`` into ``out`` (this buffer's layout),
+        parameter by parameter, matched by name and size.  Raises if a parameter is missing."""
+        old = {n: (o, k) for n, o, k in saved_layout}
+        for n, o, k in self.layout():
+            if n not in old or old[n][1] != k:
+                raise ValueError(f"optimizer state has no entry of {k} elements for parameter {n!r}")
+            so = old[n][0]
+            out[o:o + k].copy_(flat_tensor[so:so + k])
+
     def span(self, p):
         """(offset, allocation end) of parameter ``p`` in the flat buffers."""
         i = self._index[id(p)]

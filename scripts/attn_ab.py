@@ -1,11 +1,11 @@
-"""A/B the attention kernel variants in ONE process (interleaved rounds, random data):
-GPT-2-small shapes (H=12, T=1024, D=64, causal), batch from argv (default 64).
+"""Time the production attention kernels (forward, backward) on GPT-2-small shapes (H=12, T=1024,
+D=64, causal by default), batch from argv (default 64), random data, several rounds.
 
-    python scripts/attn_ab.py [B] [--fwd 1,2,3] [--bwd 1,2]
+    python scripts/attn_ab.py [B] [--rounds 3] [--D 64] [--T 1024] [--noncausal]
 
-Variants are selected per call through REPLICANN_ATTN_FWD / REPLICANN_ATTN_BWD.  Each
-variant's outputs are compared with variant 1's (bitwise-identical math is not required:
-max |Δ| is printed).  One JSON line per (pass, variant)."""
+Kernel revisions are compared by building each into its own library (REPLICANN_BUILD_OUT) and
+running this script once per library (REPLICANN_SO=...): the outputs' checksums are printed so two
+revisions can be checked for bitwise equality.  One JSON line per pass (min over rounds)."""
 
 import argparse
 import json
@@ -33,8 +33,6 @@ def timeit(fn, iters=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("B", type=int, nargs="?", default=64)
-    ap.add_argument("--fwd", default="1,2")
-    ap.add_argument("--bwd", default="2", help="REPLICANN_ATTN_DQ values (1 or 2 query groups per wave in the dQ kernel)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--D", type=int, default=64, help="head size (H = 768 // D keeps E = 768)")
     ap.add_argument("--noncausal", action="store_true")
@@ -46,37 +44,21 @@ def main():
     qkv = torch.randn(B, T, 3, H, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
     go = torch.randn(B, T, H, D, device="cuda", dtype=torch.bfloat16)
     fl_f = 4 * B * H * T * T * D / (1 if a.noncausal else 2)
-    fv = [int(x) for x in a.fwd.split(",") if x]
-    bv = [int(x) for x in a.bwd.split(",") if x]
-    ref_o = ref_g = None
-    res = {}
-    for rnd in range(a.rounds):
-        for v in fv:
-            os.environ["REPLICANN_ATTN_FWD"] = str(v)
-            f = lambda: ops.attention_packed(qkv, causal=not a.noncausal)
-            t = timeit(f)
-            o = f().detach()
-            if ref_o is None:
-                ref_o = o
-            err = (o.float() - ref_o.float()).abs().max().item()
-            res.setdefault(("fwd", v), []).append((t, err))
-        os.environ["REPLICANN_ATTN_FWD"] = "1"
-        out = ops.attention_packed(qkv, causal=not a.noncausal)
-        for v in bv:
-            os.environ["REPLICANN_ATTN_DQ"] = str(v)
-            f = lambda: torch.autograd.grad(out, qkv, go, retain_graph=True)[0]
-            t = timeit(f)
-            gq = f()
-            if ref_g is None:
-                ref_g = gq
-            err = (gq.float() - ref_g.float()).abs().max().item()
-            res.setdefault(("bwd", v), []).append((t, err))
-    for (ps, v), lst in sorted(res.items()):
-        ms = min(x[0] for x in lst)
+    fwd = lambda: ops.attention_packed(qkv, causal=not a.noncausal)
+    out = fwd()
+    bwd = lambda: torch.autograd.grad(out, qkv, go, retain_graph=True)[0]
+    res = {"fwd": [], "bwd": []}
+    for _ in range(a.rounds):
+        res["fwd"].append(timeit(fwd))
+        res["bwd"].append(timeit(bwd))
+    o, g = fwd().detach(), bwd()
+    sums = {"fwd": float(o.float().abs().sum()), "bwd": float(g.float().abs().sum())}
+    for ps, lst in res.items():
+        ms = min(lst)
         fl = fl_f if ps == "fwd" else 2.5 * fl_f
-        print(json.dumps(dict(op=f"attn_{ps}", variant=v, B=B, H=H, T=T, D=D, ms=round(ms, 4), tflops=round(fl / ms / 1e9, 1),
-                              all_ms=[round(x[0], 4) for x in lst], max_abs_diff_vs_first=max(x[1] for x in lst))),
-              flush=True)
+        print(json.dumps(dict(op=f"attn_{ps}", B=B, H=H, T=T, D=D, causal=not a.noncausal, ms=round(ms, 4),
+                              tflops=round(fl / ms / 1e9, 1), all_ms=[round(x, 4) for x in lst],
+                              abs_sum=sums[ps])), flush=True)
 
 
 if __name__ == "__main__":

@@ -31,6 +31,26 @@ def test_stale_library_is_refused(tmp_path):
     _ext.check_fresh(fake)  # matching stamp: accepted
 
 
+def test_stamp_flags_do_not_depend_on_the_loading_environment(tmp_path, monkeypatch):
+    """A library built with debug checks still loads in a process without REPLICANN_CHECK: the
+    stamp's first line is the source digest, the build defs are recorded, not re-derived."""
+    fake = tmp_path / "_C.so"
+    fake.write_bytes(b"\0")
+    fake.with_suffix(".srcstamp").write_text(f"{_build.source_digest()}\ndefs: -DREPLICANN_CHECK=1\n")
+    _ext.check_fresh(fake)
+    assert _ext.build_defs(fake) == "-DREPLICANN_CHECK=1"
+    assert _build.stamp_text().splitlines()[0] == _build.source_digest()
+
+
+def test_installed_package_without_sources_is_trusted(tmp_path, monkeypatch):
+    """A non-editable install ships _C.so + its stamp but no csrc/: nothing to compare, load it."""
+    fake = tmp_path / "_C.so"
+    fake.write_bytes(b"\0")
+    fake.with_suffix(".srcstamp").write_text("0" * 40 + "\ndefs: \n")
+    monkeypatch.setattr(_build, "CSRC", tmp_path / "no_csrc")
+    _ext.check_fresh(fake)
+
+
 @pytest.mark.skipif(not SO.exists(), reason="extension not built")
 def test_built_library_matches_tree():
     _ext.check_fresh(SO)

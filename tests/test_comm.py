@@ -111,3 +111,11 @@ def test_native_comm_rendezvous_multi_rank(world):
         assert len(calls) == 1
         _, uid, crank, cworld, dev, _ = calls[0]
         assert uid == uid0 and crank == rank and cworld == world and dev == rank
+
+
+def test_nccl_process_group_uses_high_priority_streams():
+    """Round-3 verdict: the world > 1 default (ProcessGroupNCCL) runs its collectives on a
+    high-priority stream, as the native communicator and the proxy measurements do."""
+    from replicann_amd.parallel import nccl_options
+
+    assert nccl_options().is_high_priority_stream

@@ -249,3 +249,75 @@ def test_ddp_tied_split_gloo(dtype_name, reduce_name, schedule):
             err = ((g - ref).norm() / ref.norm()).item()
             assert err < tol, (rank, err)
     torch.testing.assert_close(torch.from_numpy(res[0][1][1]), torch.from_numpy(res[1][1][1]), atol=0, rtol=0)
+
+
+def _sequence_worker(rank, world, port, q):
+    """Record every collective this rank issues (op, dtype, numel, and the backward phase it was
+    issued in) over three steps of the default world>1 DDP form: TorchComm, schedule="auto"."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from replicann_amd.parallel import DistributedDataParallel, TorchComm
+        from replicann_amd.parallel.windows import open_window
+        from replicann_amd.utils.flat import FlatParams
+
+        torch.manual_seed(0)
+        net = TiedNet().to(torch.bfloat16)
+        flat = FlatParams(net)
+        ddp = DistributedDataParallel(net, flat, bucket_mb=0.0005, reduce_mode="rsag", schedule="auto",
+                                      window_mb=0.0003)
+        assert isinstance(ddp.comm, TorchComm)
+        log, phase = [], ["fwd"]
+        for name in ("all_reduce", "broadcast", "all_gather", "reduce_scatter", "narrow_all_gather"):
+            orig = getattr(ddp.comm, name)
+
+            def rec(*a, _o=orig, _n=name, **k):
+                t = a[0]
+                log.append((phase[0], ddp._windowed, _n, str(t.dtype), int(t.numel())))
+                return _o(*a, **k)
+            setattr(ddp.comm, name, rec)
+
+        def window_hook(*_):
+            phase[0] = "window"
+            open_window()
+        net.mid.register_full_backward_hook(window_hook)
+        X, Y = _tied_data(world)
+        x, y = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
+        steps = []
+        for _ in range(3):
+            log.clear()
+            phase[0] = "bwd"
+            flat.zero_grad()
+            ddp(x, y).backward()
+            phase[0] = "finish"
+            ddp.finish()
+            steps.append((list(log), ddp._windowed))
+        q.put((rank, steps))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_identical_collective_sequence_gloo(world):
+    """Round-3 verdict: the world>1 default (TorchComm = ProcessGroupNCCL on GPUs, schedule "auto")
+    must issue the SAME collective sequence on every rank — including the eager→window switch,
+    which must happen at the same step everywhere (a rank-dependent switch would pair mismatched
+    collectives and hang RCCL)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sequence_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seqs = [steps for _, steps in res]
+    for r in range(1, world):
+        assert seqs[r] == seqs[0], f"rank {r} issued another collective sequence than rank 0"
+    (s1, w1), (s2, w2), (s3, w3) = seqs[0]
+    assert not any(win for ph, win, *_ in s1 if ph != "finish")  # step 1's backward: eager (no window seen yet)
+    assert w1 and w2 and w3                           # the switch happened after step 1, on every rank
+    assert any(ph == "window" and win for ph, win, *_ in s2) and s2 == s3
+    assert all(n for *_, n in s1)

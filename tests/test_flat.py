@@ -55,3 +55,36 @@ def test_wd_mask_matrices_only():
     wd = flat.wd_mask.cpu()
     for p, off, n in flat.segments():
         assert int(wd[off // 64]) == (1 if p.dim() >= 2 else 0)
+
+
+def test_optimizer_state_remapped_across_flat_layouts():
+    """optimizer master / moments are raw flat tensors; a checkpoint taken under another
+    packing (here: the reference MHSA's fused Q/K/V group disabled) must land on the same NAMED
+    parameters, not be read permuted."""
+    import replicann_amd as R
+    from replicann_amd.optim import FusedAdamW
+
+    torch.manual_seed(0)
+    a = R.TransformerEncoder(n_heads=2, embedding_size=16)
+    fa = FlatParams(a)
+    oa = FusedAdamW(fa, lr=1e-2)
+    for p in fa.params:
+        p.grad.copy_(torch.randn_like(p))
+    oa.step()
+    sd = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in oa.state_dict().items()}
+
+    torch.manual_seed(0)
+    b = R.TransformerEncoder(n_heads=2, embedding_size=16)
+    for mod in b.modules():  # another packing: no fusion groups
+        if hasattr(mod, "_rn_fuse_groups"):
+            mod._rn_fuse_groups = lambda: []
+    fb = FlatParams(b)
+    assert fb.layout() != fa.layout()
+    ob = FusedAdamW(fb, lr=1e-2)
+    ob.load_state_dict(sd)
+    names_a = {fa.names[id(p)]: p for p in fa.params}
+    for p, o, n in fb.segments():
+        q = names_a[fb.names[id(p)]]
+        qo = fa.span(q)[0]
+        assert torch.equal(ob.m[o:o + n], oa.m[qo:qo + n])
+        assert torch.equal(ob.master[o:o + n], oa.master[qo:qo + n])

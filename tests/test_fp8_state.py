@@ -44,3 +44,16 @@ def test_fp8_resume_bitwise_gpu(cuda, tmp_path):
     b = Trainer(TrainConfig(**kw, resume=ck))
     lb = [float(b.step()) for _ in range(3)]
     assert la == lb
+
+
+def test_fp8_checkpoint_without_scales_loads_strict():
+    """A state_dict written before the fp8_scales buffer existed loads with strict=True: the
+    missing slots start empty (current scaling on the first call) instead of raising."""
+    m = _model()
+    old = {k: v for k, v in m.state_dict().items() if not k.endswith("fp8_scales")}
+    m2 = _model()
+    for st in fp8_states(m2):
+        st.t.fill_(3.0)
+    m2.load_state_dict(old, strict=True)
+    assert all(not any(st.ready) for st in fp8_states(m2))
+    assert all(float(st.t.abs().sum()) == 0.0 for st in fp8_states(m2))
