@@ -127,6 +127,19 @@ int rn_gemm_get_sched() {
     }
     return v;
 }
+// staged epilogue of the persistent GEMM (gemm_pk_launch.h pk_staged): on unless
+// REPLICANN_GEMM_STAGED=0; the setter exists for same-process A/B tests
+static std::atomic<int> g_staged{-1};
+void rn_gemm_set_staged(int m) { g_staged = m ? 1 : 0; }
+int rn_gemm_get_staged() {
+    int v = g_staged.load();
+    if (v < 0) {
+        const char* e = std::getenv("REPLICANN_GEMM_STAGED");
+        v = (e && e[0] == '0') ? 0 : 1;
+        g_staged = v;
+    }
+    return v;
+}
 void rn_gemm_set_reserve(int r) { g_reserve = r < 0 ? 0 : (r > 128 ? 128 : r & ~7); }
 int rn_gemm_get_reserve() { return g_reserve.load(); }
 
