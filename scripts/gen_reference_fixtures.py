@@ -65,6 +65,46 @@ def main():
     out = os.path.join(ROOT, "tests", "fixtures", "ref_gpu_parity.pt")
     torch.save(fx, out)
     print(f"wrote {out} ({os.path.getsize(out) / 2**20:.1f} MiB), cases: {sorted(fx)}")
+    gx = grad_fixtures(tr)
+    out = os.path.join(ROOT, "tests", "fixtures", "ref_gpu_grads.pt")
+    torch.save(gx, out)
+    print(f"wrote {out} ({os.path.getsize(out) / 2**20:.1f} MiB), cases: {sorted(gx)}")
+
+
+def param_grads(mod, prefix=""):
+    """{state_dict key: .grad} for every parameter (fp16: the fixture travels to the GPU box)."""
+    # (a parameter the path does not use — the encoder's _attn._proj under return_kv, quirk Q5 — has
+    # no .grad: recorded as an empty tensor, and the native path must not produce one either)
+    return {prefix + n: (p.grad.detach().half() if p.grad is not None else torch.empty(0))
+            for n, p in mod.named_parameters()}
+
+
+def grad_fixtures(tr):
+    """Train mode, all dropout at p = 0: outputs, input gradients and EVERY parameter gradient of the
+    reference blocks (the native optimizer consumes the parameter gradients, through the fused-QKV
+    flat-buffer views)."""
+    fx = {}
+    for i, (name, cls, H, E, T, kw) in enumerate(refgen.GRAD_CASES):
+        torch.manual_seed(0)
+        m = refgen.zero_dropout(getattr(tr, cls)(H, E, **kw)).train()
+        m.load_state_dict(refgen.det_state_dict(m, 600 + i), strict=True)
+        x = refgen.det_input((2, T, E), 700 + i)
+        y, (g,) = fwd_bwd(m, x, gseed=800 + i)
+        fx[name] = {"y": y.half(), "gx": g.half(), "params": param_grads(m)}
+    name, H, E, Ts, Tt = refgen.GRAD_CROSS
+    torch.manual_seed(0)
+    enc = refgen.zero_dropout(tr.TransformerEncoder(H, E)).train()
+    dec = refgen.zero_dropout(tr.TransformerCrossDecoder(H, E, context_size=64)).train()
+    enc.load_state_dict(refgen.det_state_dict(enc, 900), strict=True)
+    dec.load_state_dict(refgen.det_state_dict(dec, 901), strict=True)
+    src = refgen.det_input((2, Ts, E), 902).requires_grad_()
+    tgt = refgen.det_input((2, Tt, E), 903).requires_grad_()
+    _, k, v = enc(src, return_kv=True)
+    y = dec(tgt, k, v)
+    y.backward(refgen.det_grad(y.shape, 904))
+    fx[name] = {"y": y.detach().half(), "g_src": src.grad.half(), "g_tgt": tgt.grad.half(),
+                "params": {**param_grads(enc, "enc."), **param_grads(dec, "dec.")}}
+    return fx
 
 
 if __name__ == "__main__":

@@ -39,3 +39,23 @@ def det_input(shape, seed):
 def det_grad(shape, seed):
     g = torch.Generator().manual_seed(seed + 7)
     return torch.randn(shape, generator=g)
+
+
+# Parameter-gradient parity: train mode, every dropout p = 0 (the reference's
+# head dropout is fixed at 0.1 by its constructor — quirk Q4 — so it is zeroed on the module), the
+# reference's per-parameter .grad recorded for every state_dict key; small widths keep the fixture
+# small (head sizes 64 and 32 both covered).
+GRAD_CASES = [  # name, block, n_heads, E, T, extra ctor kwargs
+    ("genc_h4_e256", "TransformerEncoder", 4, 256, 64, {}),
+    ("genc_h8_e256", "TransformerEncoder", 8, 256, 72, {}),
+    ("gdec_h4_e256", "TransformerDecoder", 4, 256, 80, {"context_size": 128}),
+]
+GRAD_CROSS = ("gxdec_h4_e256", 4, 256, 64, 48)  # encoder (return_kv) -> cross decoder, both trained
+
+
+def zero_dropout(module):
+    """Train-mode parity without randomness: every nn.Dropout (block, MHA, FFN AND per-head) at 0."""
+    for m in module.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    return module

@@ -85,3 +85,96 @@ def test_fixture_matches_live_reference(ref, fx):
     m.load_state_dict(refgen.det_state_dict(m, 100 + i), strict=True)
     y = m(refgen.det_input((2, T_, E), 200 + i))
     assert rel(y, fx[name]["y"]) < 1e-3
+
+
+# ---- parameter gradients: train mode, every dropout at p = 0 ----------------
+GFIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "ref_gpu_grads.pt")
+
+
+@pytest.fixture(scope="module")
+def gfx():
+    return torch.load(GFIX, weights_only=True)
+
+
+def _train_block(cls, H, E, seed, dev, dtype, flat, **kw):
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m = refgen.zero_dropout(getattr(T, cls)(H, E, **kw)).train()
+    m.load_state_dict(refgen.det_state_dict(m, seed), strict=True)
+    m = m.to(dev)
+    for p in m.parameters():
+        p.data = p.data.to(dtype)
+    fp = FlatParams(m) if flat else None  # the trainer's layout: grads land in the flat buffer views
+    return m, fp
+
+
+def _check_param_grads(named, ref, tol, where):
+    """Every state_dict parameter's gradient vs the reference's (relative L2); a parameter the
+    reference path leaves without a gradient must have none (or an all-zero one) here too."""
+    for n, p in named:
+        r = ref[n]
+        if r.numel() == 0:
+            assert p.grad is None or float(p.grad.float().abs().max()) == 0.0, (where, n)
+            continue
+        assert p.grad is not None, (where, n)
+        e = rel(p.grad, r)
+        assert e < tol, (where, n, e)
+
+
+def _param_case(gfx, i, dev, dtype, flat, tol):
+    name, cls, H, E, T_, kw = refgen.GRAD_CASES[i]
+    ref = gfx[name]
+    m, fp = _train_block(cls, H, E, 600 + i, dev, dtype, flat, **kw)
+    x = refgen.det_input((2, T_, E), 700 + i).to(dev, dtype).requires_grad_()
+    y = m(x)
+    y.backward(refgen.det_grad(y.shape, 800 + i).to(dev, dtype))
+    assert rel(y, ref["y"]) < tol, name
+    assert rel(x.grad, ref["gx"]) < tol, name
+    if fp is not None:  # the gradients ARE the flat buffer (what the fused optimizer reads)
+        for p, o, n in fp.segments():
+            assert p.grad.data_ptr() == fp.grad[o:o + n].data_ptr()
+    _check_param_grads(m.named_parameters(), ref["params"], tol, name)
+
+
+def _param_cross(gfx, dev, dtype, flat, tol):
+    name, H, E, Ts, Tt = refgen.GRAD_CROSS
+    ref = gfx[name]
+    enc, _ = _train_block("TransformerEncoder", H, E, 900, dev, dtype, flat)
+    dec, _ = _train_block("TransformerCrossDecoder", H, E, 901, dev, dtype, flat, context_size=64)
+    src = refgen.det_input((2, Ts, E), 902).to(dev, dtype).requires_grad_()
+    tgt = refgen.det_input((2, Tt, E), 903).to(dev, dtype).requires_grad_()
+    _, k, v = enc(src, return_kv=True)
+    y = dec(tgt, k, v)
+    y.backward(refgen.det_grad(y.shape, 904).to(dev, dtype))
+    assert rel(y, ref["y"]) < tol
+    assert rel(src.grad, ref["g_src"]) < tol and rel(tgt.grad, ref["g_tgt"]) < tol
+    named = [("enc." + n, p) for n, p in enc.named_parameters()] + [("dec." + n, p) for n, p in dec.named_parameters()]
+    _check_param_grads(named, ref["params"], tol, name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flat", [False, True], ids=["autograd", "flat"])
+@pytest.mark.parametrize("i", range(len(refgen.GRAD_CASES)), ids=[c[0] for c in refgen.GRAD_CASES])
+def test_param_grads_gpu_vs_reference(cuda, gfx, i, flat):
+    """Native bf16 training path (fused QKV through the flat-buffer views, fused attention backward,
+    LayerNorm backward with the residual gradient, GEMM epilogues, direct accumulation) vs the
+    reference's fp32 parameter gradients."""
+    _param_case(gfx, i, cuda, torch.bfloat16, flat, 3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flat", [False, True], ids=["autograd", "flat"])
+def test_param_grads_cross_gpu_vs_reference(cuda, gfx, flat):
+    _param_cross(gfx, cuda, torch.bfloat16, flat, 3e-2)
+
+
+@pytest.mark.parametrize("flat", [False, True], ids=["autograd", "flat"])
+@pytest.mark.parametrize("i", range(len(refgen.GRAD_CASES)), ids=[c[0] for c in refgen.GRAD_CASES])
+def test_param_grads_cpu_vs_reference_fixture(gfx, i, flat):
+    """The same comparison on the CPU (fp32 ATen path; the fixture is fp16): pins the test's own
+    bookkeeping — names, the flat layout, the unused-parameter rule — without a GPU."""
+    _param_case(gfx, i, torch.device("cpu"), torch.float32, flat, 2e-3)
+
+
+def test_param_grads_cross_cpu_vs_reference_fixture(gfx):
+    _param_cross(gfx, torch.device("cpu"), torch.float32, True, 2e-3)
