@@ -9,6 +9,7 @@ step() {  # step <name> <timeout> cmd...
   echo "=== $n rc=$rc"; grep -v "amdgpu.ids" gpurun_out/$n.log | grep -o '"ms_per_step": [0-9.]*' | tail -1; grep -E "passed|failed|smoke ok|max_rel" gpurun_out/$n.log | tail -1
   return $rc
 }
+step tr8_probe 30 ./scripts/dev/tr8_probe || exit 1
 step t_staged 300 python -u -m pytest tests/test_gemm_staged_gpu.py tests/test_reference_parity_gpu.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider || exit 1
 step gpu_all 1000 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider || exit 1
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
