@@ -97,6 +97,78 @@ __global__ void __launch_bounds__(256) quant_delayed_k(const bf16* __restrict__ 
     if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
 }
 
+// Gradient operands of the fp8 weight-gradient GEMM: OCP e5m2 ("bf8": 2 more exponent bits, the
+// range gradients need) with the same one-pass delayed scaling (scale from the previous pass's amax,
+// x2 headroom, this pass records the new amax).  state as quant_delayed_k; the roll is folded in
+// (block 0 rolls nothing: the host launches fp8_roll_fmt_k first).
+constexpr float E5M2_MAX = 57344.f;
+__global__ void fp8_roll_bf8_k(float* __restrict__ state) {
+    const float a = state[1];
+    state[2] = a;
+    state[0] = a > 0.f ? 2.f * a / E5M2_MAX : 1.f;
+    state[1] = 0.f;
+}
+__global__ void __launch_bounds__(256) quant_delayed_bf8_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
+                                                           float* __restrict__ state) {
+    __shared__ float sm[16];
+    const float inv = 1.f / state[0];
+    float m = 0.f;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            m = fmaxf(m, fabsf(f[j]));
+            f[j] = fminf(fmaxf(f[j] * inv, -E5M2_MAX), E5M2_MAX);
+        }
+        int w0 = 0, w1 = 0;
+        w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], w1, true);
+        *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    }
+    for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float v = bf2f(x[i]);
+        m = fmaxf(m, fabsf(v));
+        const float f = fminf(fmaxf(v * inv, -E5M2_MAX), E5M2_MAX);
+        q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_bf8_f32(f, 0.f, 0, false) & 0xFF);
+    }
+    m = block_max(m, sm);
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
+}
+// first (current-scaling) pass of a gradient slot: amax, then scale = amax / E5M2_MAX
+__global__ void __launch_bounds__(256) quant_bf8_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
+                                                   float* __restrict__ state) {
+    const float amax = state[1];
+    const float scale = amax > 0.f ? amax / E5M2_MAX : 1.f;
+    const float inv = 1.f / scale;
+    if (blockIdx.x == 0 && threadIdx.x == 0) state[0] = scale;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(x + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(f[j] * inv, -E5M2_MAX), E5M2_MAX);
+        int w0 = 0, w1 = 0;
+        w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], w1, true);
+        *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    }
+    for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float f = fminf(fmaxf(bf2f(x[i]) * inv, -E5M2_MAX), E5M2_MAX);
+        q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_bf8_f32(f, 0.f, 0, false) & 0xFF);
+    }
+}
+
+__global__ void dequant_bf8_k(const uint8_t* __restrict__ q, long n, const float* __restrict__ state,
+                              bf16* __restrict__ y) {
+    const float scale = state[0];
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        y[i] = (bf16)(__builtin_amdgcn_cvt_f32_bf8((int)q[i], 0) * scale);
+}
+
 __global__ void dequant_k(const uint8_t* __restrict__ q, long n, const float* __restrict__ state,
                           bf16* __restrict__ y) {
     const float scale = state[0];
@@ -201,6 +273,22 @@ void rn_fp8_roll(float* state, hipStream_t st) { fp8_roll_k<<<1, 1, 0, st>>>(sta
 
 void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
     dequant_k<<<gridn(n), 256, 0, st>>>((const uint8_t*)q, n, state, (bf16*)y);
+}
+
+// e5m2 gradient quantisation: delayed (roll + one pass) or, for a slot without a scale yet,
+// current scaling (memset + amax + quantise); state as rn_fp8_quantize_delayed
+void rn_bf8_quantize(const void* x, long n, void* q, float* state, int delayed, hipStream_t st) {
+    if (delayed) {
+        fp8_roll_bf8_k<<<1, 1, 0, st>>>(state);
+        quant_delayed_bf8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
+        return;
+    }
+    (void)hipMemsetAsync(state, 0, 2 * sizeof(float), st);
+    amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
+    quant_bf8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
+}
+void rn_bf8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
+    dequant_bf8_k<<<gridn(n), 256, 0, st>>>((const uint8_t*)q, n, state, (bf16*)y);
 }
 
 // C[M,N] (bf16) = act(sa·sb · A8[M,K] · B8[N,K]ᵀ + bias) + res ; K % 16 == 0, lda/ldb in bytes % 16 == 0
