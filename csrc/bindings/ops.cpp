@@ -87,6 +87,11 @@ void rn_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
 void rn_fp8_quantize(const void*, long, void*, float*, hipStream_t);
 void rn_fp8_dequantize(const void*, long, const float*, void*, hipStream_t);
 void rn_fp8_quantize_delayed(const void*, long, void*, float*, hipStream_t);
+void rn_bf8_quantize(const void*, long, void*, float*, int, hipStream_t);
+void rn_bf8_dequantize(const void*, long, const float*, void*, hipStream_t);
+long rn_gemm_fp8_wgrad_ws(int, int, int);
+int rn_gemm_fp8_wgrad(const void*, const void*, void*, const float*, const float*, float*, float*, int, int, int, long,
+                      long, long, int, int, int, hipStream_t);
 int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
                 int, int, int, long, long, long, int, hipStream_t, void*, float*);
 long rn_bn_ws_floats(int, int);
@@ -939,6 +944,40 @@ Tensor fp8_quantize_delayed(const Tensor& x, const Tensor& state) {
     rn_fp8_quantize_delayed(x.data_ptr(), x.numel(), q.data_ptr(), state.data_ptr<float>(), cur_stream());
     return q;
 }
+// e5m2 ("bf8") quantisation of a gradient operand: delayed scaling (roll + one pass) or, for a slot
+// without a scale yet, current scaling; state: [scale, amax, amax the scale came from, -]
+Tensor bf8_quantize(const Tensor& x, const Tensor& state, bool delayed) {
+    CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
+    TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda());
+    Tensor q = at::empty(x.sizes(), x.options().dtype(at::kByte));
+    rn_bf8_quantize(x.data_ptr(), x.numel(), q.data_ptr(), state.data_ptr<float>(), delayed ? 1 : 0, cur_stream());
+    return q;
+}
+Tensor bf8_dequantize(const Tensor& q, const Tensor& state) {
+    GUARD(q);
+    Tensor y = at::empty(q.sizes(), q.options().dtype(at::kBFloat16));
+    rn_bf8_dequantize(q.data_ptr(), q.numel(), state.data_ptr<float>(), y.data_ptr(), cur_stream());
+    return y;
+}
+// fp8 weight gradient: out[M,N] (+)= sa·sb · a8ᵀ · b8 with a8 [K][M] (e5m2 if a_bf8, else e4m3) and
+// b8 [K][N] e4m3, K = tokens (csrc/include/gemm_pk.h, fp8 MN-contiguous operands)
+void gemm_fp8_wgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb, const Tensor& out,
+                    bool accumulate, bool a_bf8) {
+    GUARD(a8);
+    TORCH_CHECK(a8.scalar_type() == at::kByte && b8.scalar_type() == at::kByte, "fp8 operands are uint8 storage");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.size(0) == b8.size(0) && a8.stride(1) == 1 && b8.stride(1) == 1);
+    const int K = a8.size(0), M = a8.size(1), N = b8.size(1);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1);
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat);
+    Tensor ws = at::empty({rn_gemm_fp8_wgrad_ws(M, N, K)}, a8.options().dtype(at::kFloat));
+    Tensor alpha = at::empty({1}, a8.options().dtype(at::kFloat));
+    int rc = rn_gemm_fp8_wgrad(a8.data_ptr(), b8.data_ptr(), out.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(),
+                               alpha.data_ptr<float>(), ws.data_ptr<float>(), M, N, K, a8.stride(0), b8.stride(0),
+                               out.stride(0), accumulate ? 1 : 0, out.scalar_type() == at::kFloat ? 1 : 0, a_bf8 ? 1 : 0,
+                               cur_stream());
+    TORCH_CHECK(rc == 0, "gemm_fp8_wgrad: M, N and row strides must be multiples of 16 and K of 128, got M=", M,
+                " N=", N, " K=", K);
+}
 Tensor fp8_dequantize(const Tensor& q, const Tensor& state) {
     GUARD(q);
     Tensor y = at::empty(q.sizes(), q.options().dtype(at::kBFloat16));
@@ -1051,6 +1090,9 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_quantize(Tensor x) -> (Tensor, Tensor)");
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");
+    m.def("bf8_quantize(Tensor x, Tensor(a!) state, bool delayed) -> Tensor");
+    m.def("bf8_dequantize(Tensor q, Tensor state) -> Tensor");
+    m.def("gemm_fp8_wgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) out, bool accumulate, bool a_bf8) -> ()");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("gemm_fp8_q8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, int act, Tensor(a!) preact, Tensor(b!) q8_state) -> (Tensor, Tensor)");
     m.def("fp8_quant_many(Tensor flat, Tensor segs, int max_n, Tensor(a!) qbuf, bool roll=True) -> ()");
@@ -1107,6 +1149,9 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("fp8_quantize", &fp8_quantize);
     m.impl("fp8_dequantize", &fp8_dequantize);
     m.impl("fp8_quantize_delayed", &fp8_quantize_delayed);
+    m.impl("bf8_quantize", &bf8_quantize);
+    m.impl("bf8_dequantize", &bf8_dequantize);
+    m.impl("gemm_fp8_wgrad", &gemm_fp8_wgrad);
     m.impl("gemm_fp8", &gemm_fp8);
     m.impl("gemm_fp8_q8", &gemm_fp8_q8);
     m.impl("fp8_quant_many", &fp8_quant_many);

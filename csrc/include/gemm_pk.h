@@ -121,6 +121,33 @@ RN_DEV void pk_stage(const u32x4& rs, long ld, int mn_lim, int k_lim, char* lds,
     }
 }
 
+// fp8 MN-contiguous half-tile image (FP8 with !AK / !BKC: the weight gradient dW = dYᵀ·X reads both
+// operands as stored, [k = token][mn]): [128 k rows][128 mn bytes], 16-B chunk c of row r at
+// c ^ swz_f8(r).  Read with ds_read_b64_tr_b8 (gfx950 transposing LDS read: per 16-lane group, lane
+// 2q+p supplies 8 bytes of row q, columns 8p..8p+7, and lane i receives column i of the 8 rows), so a
+// lane gets 8 consecutive k of one mn column.  swz_f8 puts the same-parity rows a 32-lane half reads
+// (rows 16g + 8t + q of groups g, g+1) on 8 distinct chunks: conflict-free.
+RN_DEV int swz_f8(int r) { return ((r >> 1) & 3) | (((r >> 4) & 1) << 2); }
+
+// fp8 MN fragment (k-step s ∈ {0, 1}: k = 64·s + 16·(lane>>4) + 0..15) of the 16 mn columns
+// col0 .. col0 + 15 (col0 % 16 == 0), column col0 + (lane & 15) per lane: the same byte → k map as the
+// K-contiguous fp8 fragment (chunks g and g + 4 of a 128-byte k row), so either layout pairs with
+// either in one scaled MFMA.
+RN_DEV s16x8 pk_frag8_mn(const char* lds, int col0, int s, int lane) {
+    typedef int i32x2v __attribute__((ext_vector_type(2)));
+    const int g = lane >> 4, ii = lane & 15, q = ii >> 1, pp = ii & 1;
+    const int cb = col0 + 8 * pp;
+    i32x2v v[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int row = s * 64 + 16 * g + 8 * t + q;
+        const char* a = lds + row * 128 + (((cb >> 4) ^ swz_f8(row)) << 4) + (cb & 15);
+        v[t] = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2v*)a);
+    }
+    const i32x4 w = {v[0][0], v[0][1], v[1][0], v[1][1]};
+    return __builtin_bit_cast(s16x8, w);
+}
+
 // A fragment (k-step s) of rows mnbase + (lane & 15) of a half-tile image.
 template <bool KC>
 RN_DEV s16x8 pk_frag_a(const char* lds, int mnbase, int s, int lane) {
@@ -252,10 +279,14 @@ RN_DEV int pk_deq_take(uint32_t v) {
 }
 #pragma clang diagnostic pop
 
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false, bool DYN = false,
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false,
           bool STG = false>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
-    static_assert(!FP8 || (AK && BKC && !(DBG & 8)), "fp8: K-contiguous operands only");
+    // FP8: 0 bf16; 1 e4m3 x e4m3; 2 A e5m2 (a gradient) x B e4m3.  Operands both K-contiguous (the
+    // forward) or both MN-contiguous (the weight gradient: fp32 split-K slabs only)
+    static_assert(!FP8 || (AK == BKC && !(DBG & 8)), "fp8: both operands K- or both MN-contiguous");
+    static_assert(!FP8 || AK || SPLIT, "fp8 MN-contiguous: split-K slab output only");
+    constexpr bool F8MN = FP8 && !AK;
     static_assert(!DYN || (!FP8 && DBG == 0), "dynamic schedule: bf16 production kernels only");
     static_assert(!STG || (!SPLIT && !F32 && !DYN && !FP8 && DBG == 0), "staged epilogue: bf16 static walk only");
     constexpr int BM = 256, BN = 256;
@@ -326,6 +357,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         if (kc) {
             mn = ins * 8 + (lane >> 3);
             k = ((lane & 7) ^ (isA ? swz_kc(mn) : swz_kcp(mn))) * 8;
+        } else if (F8MN) {  // k: byte row 0..127 of the fp8 MN image; mn: byte column
+            k = ins * 8 + (lane >> 3);
+            mn = ((lane & 7) ^ swz_f8(k)) * 16;
         } else {
             k = (ins & 7) * 8 + (lane >> 3);
             mn = (ins >> 3) * 64 + ((lane & 7) ^ (isA ? swz_mn(k) : swz_mnp(k))) * 8;
@@ -336,12 +370,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     for (int i = 0; i < 2; ++i) {
         int mn, k;
         lane_mnk(true, i, mn, k);
-        a_off[i] = (uint32_t)((AK ? (long)mn * p.lda + k : (long)k * p.lda + mn) * 2);
+        // (fp8 MN: lda / ldb in BYTES, offsets in bytes)
+        a_off[i] = (uint32_t)(F8MN ? (long)k * p.lda + mn : (AK ? (long)mn * p.lda + k : (long)k * p.lda + mn) * 2);
         lane_mnk(false, i, mn, k);
-        b_off[i] = (uint32_t)((BKC ? (long)mn * p.ldb + k : (long)k * p.ldb + mn) * 2);
+        b_off[i] = (uint32_t)(F8MN ? (long)k * p.ldb + mn : (BKC ? (long)mn * p.ldb + k : (long)k * p.ldb + mn) * 2);
     }
     const long a_step = AK ? (long)BK : (long)BK * p.lda, b_step = BKC ? (long)BK : (long)BK * p.ldb;
-    const long a_half = AK ? 128L * p.lda : 128L, b_half = BKC ? 128L * p.ldb : 128L;
+    // (fp8 MN: one K-tile = 128 k rows of lda bytes = 64·lda bf16 elements, the a_step formula; the
+    // second half-tile starts 128 mn BYTES = 64 bf16 elements in)
+    const long a_half = AK ? 128L * p.lda : (F8MN ? 64L : 128L), b_half = BKC ? 128L * p.ldb : (F8MN ? 64L : 128L);
     // cursor: the K-tile being issued (limits 0 once the block's items are exhausted: every
     // lane then reads out of range and the DMA only zero-fills its slot)
     const bf16* ca = p.A;
@@ -367,8 +404,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     auto cur_set = [&]() {
         int m0, n0, kb, ke, tm;
         item_coords(cu, m0, n0, kb, ke, tm);
-        ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + m0;
-        cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + n0;
+        ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + (F8MN ? m0 / 2 : m0);
+        cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + (F8MN ? n0 / 2 : n0);
         cml = p.M - m0;
         cnl = p.N - n0;
         ckl = ke - kb;
@@ -459,7 +496,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                 int mn, kk;
                 lane_mnk(isA, i, mn, kk);
                 const uint32_t o = isA ? a_off[i] : b_off[i];
-                dma16_at(rs, (mn < mnl && kk < ckl) ? o : 0xFFFFFFF0u, dst + i * 1024);
+                const bool kin = F8MN ? kk < 2 * ckl : kk < ckl;  // (fp8 MN: kk is a k byte, ckl in 2-byte units)
+                dma16_at(rs, (mn < mnl && kin) ? o : 0xFFFFFFF0u, dst + i * 1024);
             }
         }
     };
@@ -478,6 +516,17 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     s16x8 Af[4][2], Bl[2][2], Br[2][2];
+    // fragment reads: bf16 / fp8 K-contiguous images as before; fp8 MN images by transposing reads,
+    // the B side then in plain column order (fragment j = the wave's columns 16j .. 16j + 15, see the
+    // epilogue's column map)
+    auto frag_a = [&](const char* half, int mnbase, int s) -> s16x8 {
+        if constexpr (F8MN) return pk_frag8_mn(half, mnbase, s, lane);
+        else return pk_frag_a<AK>(half, mnbase, s, lane);
+    };
+    auto frag_b = [&](const char* half, int j, int s) -> s16x8 {
+        if constexpr (F8MN) return pk_frag8_mn(half, wc * 32 + 16 * j, s, lane);
+        else return pk_frag_b<BKC>(half, wc * 32, j, s, lane);
+    };
 
     // ---- epilogue of one output tile, straight from the accumulators ----
     auto epilogue = [&](int m0, int n0, int tm, int sid) {
@@ -488,9 +537,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         char* cbase = SPLIT ? (char*)(p.ws + ((long)sid * p.M + m0) * p.N + n0) : (char*)p.C + ((long)m0 * ldc + n0) * ES;
         const __amdgpu_buffer_rsrc_t crs = pk_rsrc(cbase, 0x7FFFFFF0u);
         const u32x4 crs_u = pk_rsrc_u(cbase, 0x7FFFFFF0u);
-        auto off = [&](int mh, int i, int nh, int es) -> uint32_t {
+        // output column of a lane's first value: 8 contiguous columns per lane group G (the permuted B
+        // fragments), or for fp8 MN two runs of 4: columns 4G.. (fragment 0) and 16 + 4G.. (fragment 1)
+        auto off = [&](int mh, int i, int nh, int es, int dc = 0) -> uint32_t {
             const int r = mh * 128 + wr * 64 + i * 16 + (lane & 15);
-            const int c = nh * 128 + wc * 32 + 8 * G;
+            const int c = nh * 128 + wc * 32 + (F8MN ? 4 : 8) * G + dc;
             return (r < mlim && c < nlim) ? (uint32_t)(((long)r * ldc + c) * es) : 0xFFFFFFF0u;
         };
         // bias: the wave's 2 × 32 columns through the scalar cache, then each lane picks its 8
@@ -564,7 +615,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                 for (int nh = 0; nh < 2; ++nh) {
                     float v[8];
-                    const bool swp = !BKC && (G & 1);  // MN image: odd lane groups hold fragment 1 first
+                    const bool swp = !BKC && !F8MN && (G & 1);  // bf16 MN image: odd lane groups hold fragment 1 first
 #pragma unroll
                     for (int c = 0; c < 8; ++c) {
                         // compile-time register indices on both sides of the select (a runtime
@@ -574,12 +625,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                     }
                     if constexpr (SPLIT) {
                         const uint32_t o = off(mh, i, nh, 4);
+                        const uint32_t o2 = F8MN ? off(mh, i, nh, 4, 16) : (o == 0xFFFFFFF0u ? o : o + 16);
                         pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1]),
                                     __builtin_bit_cast(uint32_t, v[2]), __builtin_bit_cast(uint32_t, v[3])},
                             crs_u, o);
                         pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[4]), __builtin_bit_cast(uint32_t, v[5]),
                                     __builtin_bit_cast(uint32_t, v[6]), __builtin_bit_cast(uint32_t, v[7])},
-                            crs_u, o == 0xFFFFFFF0u ? o : o + 16);
+                            crs_u, o2);
                         continue;
                     }
 #pragma unroll
@@ -799,8 +851,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                             \
         _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                             \
             acc[MH][NH][i_][j_] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(                   \
-                pk_cat8(BF[j_][0], BF[j_][1]), pk_cat8(Af[i_][0], Af[i_][1]), acc[MH][NH][i_][j_], 0, 0, 0, \
-                127, 0, 127);                                                                          \
+                pk_cat8(BF[j_][0], BF[j_][1]), pk_cat8(Af[i_][0], Af[i_][1]), acc[MH][NH][i_][j_], 0,     \
+                FP8 == 2 ? 1 : 0, 0, 127, 0, 127);                                                     \
     } else {                                                                                           \
     _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                 \
@@ -994,19 +1046,19 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         RN_PK_PHASE(false,
             deq_step();
             _Pragma("unroll") for (int s = 0; s < 2; ++s) {
-                _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl, wr * 64 + i * 16, s, lane);
-                _Pragma("unroll") for (int j = 0; j < 2; ++j) Bl[j][s] = pk_frag_b<BKC>(sl + PK_HALF, wc * 32, j, s, lane);
+                _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = frag_a(sl, wr * 64 + i * 16, s);
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) Bl[j][s] = frag_b(sl + PK_HALF, j, s);
             },
             issue_h(H2{});, 0, 0, Bl)
         // q1: At + Br
         RN_PK_PHASE(true,
             _Pragma("unroll") for (int s = 0; s < 2; ++s)
-                _Pragma("unroll") for (int j = 0; j < 2; ++j) Br[j][s] = pk_frag_b<BKC>(sl + 2 * PK_HALF, wc * 32, j, s, lane);,
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) Br[j][s] = frag_b(sl + 2 * PK_HALF, j, s);,
             issue_h(H3{});, 0, 1, Br)
         // q2: Ab + Br (the cursor moves on to K-tile u + 2)
         RN_PK_PHASE(true,
             _Pragma("unroll") for (int s = 0; s < 2; ++s)
-                _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = pk_frag_a<AK>(sl + 3 * PK_HALF, wr * 64 + i * 16, s, lane);,
+                _Pragma("unroll") for (int i = 0; i < 4; ++i) Af[i][s] = frag_a(sl + 3 * PK_HALF, wr * 64 + i * 16, s);,
             cur_adv(); issue_h(H0{});, 1, 1, Br)
         // q3: Ab + Bl (all fragments already in registers)
         RN_PK_PHASE(true, , issue_h(H1{});, 1, 0, Bl)
@@ -1092,7 +1144,7 @@ inline int* pk_sched_slot(const GemmArgs& a, hipStream_t st) {
     return rn_gemm_sched_slot(dev, st);
 }
 
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, bool FP8 = false, bool DYN = false,
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false,
           bool STG = false>
 void launch_pk_t(GemmArgs& a, hipStream_t st) {
     auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8, DYN, STG>;

@@ -240,6 +240,7 @@ int fp8_gemm_kernel() {
 }  // namespace
 
 void rn_gemm_launch_pk_fp8(rn_gemm_detail::GemmArgs& a, int act, hipStream_t st);
+void rn_gemm_launch_pk_fp8_wgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 
 extern "C" {
 
@@ -324,6 +325,41 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     else if (act == ACT_GELU_D) launch_fp8_t<256, 192, 2, 4, ACT_GELU_D>(a, st);
     else if (act == ACT_RELU) launch_fp8_t<256, 192, 2, 4, ACT_RELU>(a, st);
     else launch_fp8_t<256, 192, 2, 4, ACT_NONE>(a, st);
+    return 0;
+}
+
+// dW[M,N] (+)= sa·sb · Σ_k A8[k][m] · B8[k][n]  — the fp8 weight gradient with both operands as the
+// forward / backward produced them (token-major: A8 = dY [K][lda] e5m2 or e4m3, B8 = X [K][ldb]
+// e4m3; lda / ldb in bytes), K = tokens.  C: bf16 (out_f32 = 0) or fp32, accumulated into when
+// `accumulate`.  ws: split · M · N floats (rn_gemm_fp8_wgrad_ws).  Requirements: M, N, lda, ldb
+// multiples of 16, K a multiple of 128.
+long rn_gemm_fp8_wgrad_split(int M, int N, int K) {
+    // ~2 items per CU over 256 CUs (long K: the per-item epilogue is negligible), K slices of whole
+    // 128-deep K-tiles
+    const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+    long s = (512 + tiles - 1) / tiles;
+    const long kt = K / 128;
+    if (s > kt) s = kt;
+    if (s < 1) s = 1;
+    const long per = (kt + s - 1) / s;
+    return (kt + per - 1) / per;
+}
+long rn_gemm_fp8_wgrad_ws(int M, int N, int K) { return rn_gemm_fp8_wgrad_split(M, N, K) * (long)M * N; }
+int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, const float* sb, float* alpha_ws,
+                      float* ws, int M, int N, int K, long lda, long ldb, long ldc, int accumulate, int out_f32,
+                      int a_bf8, hipStream_t st) {
+    if (M % 16 || N % 16 || lda % 16 || ldb % 16 || K % 128 || M <= 0 || N <= 0) return -1;
+    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
+    const int split = (int)rn_gemm_fp8_wgrad_split(M, N, K);
+    const int kt = K / 128, per = (kt + split - 1) / split;
+    rn_gemm_detail::GemmArgs a = {};
+    a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.ws = ws; a.alpha = alpha_ws;
+    a.M = M; a.N = N; a.K = K / 2; a.lda = lda; a.ldb = ldb; a.ldc = ldc;  // MN-contiguous fp8: ld in bytes
+    a.tiles_m = (M + 255) / 256;
+    a.tiles_n = (N + 255) / 256;
+    a.split = split; a.k_per_split = per * 64; a.out_f32 = out_f32; a.accumulate = accumulate;
+    a.slab_step = 1;
+    rn_gemm_launch_pk_fp8_wgrad(a, a_bf8, st);
     return 0;
 }
 

@@ -43,18 +43,21 @@ class Linear(nn.Module):
         self.fp8_state = None
         if fp8:  # delayed-scaling state [activation, weight] x [scale, amax, -, -]: a checkpointed buffer
             self.register_buffer("fp8_scales", torch.zeros(2, 4))
+            # and the weight gradient's dY slot (e5m2, ops.fp8.fp8_wgrad)
+            self.register_buffer("fp8_gscales", torch.zeros(1, 4))
             self.fp8_state = ops.Fp8State(owner=self)
         nn.init.normal_(self.weight, std=std)
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, *args, **kwargs):
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, *args, **kwargs)
-        key = prefix + "fp8_scales"
-        if self.fp8 and key not in state_dict:
-            # a checkpoint written before the delayed-scaling buffer existed (or by a bf16 model):
-            # start from empty slots (the first call uses current scaling), not a strict-load error
-            self.fp8_scales.zero_()
-            if key in missing_keys:
-                missing_keys.remove(key)
+        for name in ("fp8_scales", "fp8_gscales"):
+            key = prefix + name
+            if self.fp8 and key not in state_dict:
+                # a checkpoint written before the delayed-scaling buffer existed (or by a bf16 model):
+                # start from empty slots (the first call uses current scaling), not a strict-load error
+                getattr(self, name).zero_()
+                if key in missing_keys:
+                    missing_keys.remove(key)
         if self.fp8_state is not None:  # a loaded slot holds a scale: continue with delayed scaling
             self.fp8_state.sync_ready()
 

@@ -13,12 +13,18 @@ CPU tensors emulate the numerics (quantise → dequantise → fp32 matmul).
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _ext
 from .linear import _act_ref, _pre_ref
 
 E4M3_MAX = 448.0
+E5M2_MAX = 57344.0
+# fp8 weight gradients (dW = dYᵀ·X with dY in e5m2, X the forward's e4m3 copy) of the fp8 layers:
+# REPLICANN_FP8_WGRAD=1 (or Fp8State.wgrad); off by default until measured on the GPU
+FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "0") == "1"
 
 
 def quantize_fp8(x):
@@ -29,6 +35,56 @@ def quantize_fp8(x):
     scale = amax / E4M3_MAX if amax > 0 else torch.tensor(1.0)
     q = (x.float() / scale).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
     return q.view(torch.uint8), torch.stack([scale, amax, scale * 0, scale * 0]).float()
+
+
+def quantize_bf8(x, state, delayed):
+    """e5m2 copy of a gradient with its delayed-scaling slot ``state`` (4 floats: scale, amax,
+    previous amax, -): current scaling if not ``delayed``.  Returns q (uint8 storage)."""
+    if _ext.use_native(x):
+        return _ext.ops().bf8_quantize(x.contiguous(), state, bool(delayed))
+    amax = x.detach().abs().max().float()
+    if delayed:
+        prev = state[1].clone()
+        state[2] = prev
+        scale = 2 * prev / E5M2_MAX if float(prev) > 0 else torch.tensor(1.0)
+    else:
+        scale = amax / E5M2_MAX if amax > 0 else torch.tensor(1.0)
+    state[0] = scale
+    state[1] = amax
+    q = (x.float() / scale).clamp(-E5M2_MAX, E5M2_MAX).to(torch.float8_e5m2)
+    return q.view(torch.uint8)
+
+
+def dequantize_bf8(q, state):
+    if _ext.use_native(q):
+        return _ext.ops().bf8_dequantize(q, state)
+    return (q.view(torch.float8_e5m2).float() * state[0]).to(torch.bfloat16)
+
+
+def fp8_wgrad_ok(dy2, x8) -> bool:
+    """Shapes the fp8 weight-gradient GEMM takes: tokens % 128, both widths % 16."""
+    return dy2.shape[0] % 128 == 0 and dy2.shape[1] % 16 == 0 and x8.shape[1] % 16 == 0 and dy2.shape[0] > 0
+
+
+def fp8_wgrad(dy2, x8, xs, state, out=None, accumulate=False):
+    """dW = dYᵀ·X in fp8: dY quantised to e5m2 with ``state``'s gradient slot, X = the forward's e4m3
+    copy ``x8`` with scale slot ``xs``.  Accumulates into ``out`` (the flat gradient view) or returns
+    a new bf16 tensor.  CPU: the same quantise → dequantise numerics in fp32."""
+    dy8, gs = state.gquant(dy2)
+    if _ext.use_native(dy2):
+        if out is None:
+            out = torch.zeros(dy2.shape[1], x8.shape[1], device=dy2.device, dtype=torch.bfloat16)
+            accumulate = False
+        _ext.ops().gemm_fp8_wgrad(dy8, x8, gs, xs, out, accumulate, True)
+        return out
+    g = dequantize_bf8(dy8, gs).float().t() @ dequantize_fp8(x8, xs).float()
+    if out is None:
+        return g.to(dy2.dtype)
+    if accumulate:
+        out.add_(g.to(out.dtype))
+    else:
+        out.copy_(g)
+    return out
 
 
 def dequantize_fp8(q, state):
@@ -55,11 +111,15 @@ class Fp8State:
     state_dict is loaded (:func:`sync_ready_from_tensors`) and snapshotted with it
     (:func:`ready_snapshot` / :func:`ready_restore`)."""
 
-    def __init__(self, owner=None, name="fp8_scales"):
+    def __init__(self, owner=None, name="fp8_scales", gname="fp8_gscales"):
         self._owner = owner
         self._name = name
+        self._gname = gname
         self._t = None
+        self._gt = None
         self.ready = [False, False]
+        self.g_ready = False  # gradient slot (fp8 weight gradient's dY) holds a scale
+        self.wgrad = FP8_WGRAD
         self._offer = None  # (activation tensor, its e4m3 copy) written by the producer kernel
         self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
         self.wcache = None  # Fp8WeightCache holding this GEMM's e4m3 weight (refreshed by the optimizer)
@@ -75,10 +135,36 @@ class Fp8State:
         else:
             self._t = value
 
+    @property
+    def gt(self):
+        """(1, 4) gradient slot [scale, amax, previous amax, -] of the fp8 weight gradient's dY."""
+        if self._owner is not None and self._gname in self._owner._buffers:
+            return self._owner._buffers[self._gname]
+        return self._gt
+
+    @gt.setter
+    def gt(self, value):
+        if self._owner is not None and self._gname in self._owner._buffers:
+            self._owner._buffers[self._gname] = value
+        else:
+            self._gt = value
+
     def sync_ready(self):
         """ready[i] = slot i holds a scale (host sync: call at load time, never inside a step)."""
         t = self.t
         self.ready = [bool(t is not None and float(t[i, 0]) > 0) for i in range(2)]
+        g = self.gt
+        self.g_ready = bool(g is not None and float(g[0, 0]) > 0)
+
+    def gquant(self, dy):
+        """dY in e5m2 with the gradient slot: current scaling on the first call, delayed after."""
+        if self.gt is None or self.gt.device != dy.device:
+            self.gt = torch.zeros(1, 4, device=dy.device, dtype=torch.float32)
+            self.g_ready = False
+        st = self.gt[0]
+        q = quantize_bf8(dy, st, self.g_ready)
+        self.g_ready = True
+        return q, st
 
     def producer_ready(self, device) -> bool:
         """True once the activation slot has a delayed scale, so a producer kernel (LayerNorm)
@@ -119,12 +205,13 @@ def fp8_states(model):
 
 
 def ready_snapshot(model):
-    return [list(st.ready) for st in fp8_states(model)]
+    return [(list(st.ready), st.g_ready) for st in fp8_states(model)]
 
 
 def ready_restore(model, snap):
-    for st, r in zip(fp8_states(model), snap):
+    for st, (r, g) in zip(fp8_states(model), snap):
         st.ready = list(r)
+        st.g_ready = g
 
 
 def sync_ready_from_tensors(model):
@@ -132,13 +219,23 @@ def sync_ready_from_tensors(model):
         st.sync_ready()
 
 
-def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State, out8: Fp8State | None = None):
+def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State, out8: Fp8State | None = None,
+                keep=False):
     """act(x2·weightᵀ + bias) + res2 with both operands in e4m3 (GPU: block-scaled MFMA;
     CPU: the same quantise → dequantise numerics in fp32).
 
     ``out8``: the state of the fp8 GEMM that consumes this output — the epilogue then also writes
-    the output in e4m3 with that state's delayed scale and hands it over (no quantisation pass)."""
+    the output in e4m3 with that state's delayed scale and hands it over (no quantisation pass).
+    ``keep``: return (y, x8, scale) — the e4m3 input and a copy of its scale slot, kept for the fp8
+    weight gradient of the backward."""
     xq, xs = state.quant(x2, 0)
+    y = _fp8_forward_q(x2, xq, xs, weight, bias, res2, act, preact, state, out8)
+    if keep:
+        return y, xq, xs.clone()
+    return y
+
+
+def _fp8_forward_q(x2, xq, xs, weight, bias, res2, act, preact, state, out8):
     wq, ws = state.quant(weight.contiguous(), 1)
     if _ext.use_native(x2):
         if (out8 is not None and res2 is None and preact is not None and x2.shape[0] > 0

@@ -166,11 +166,17 @@ class _LinearFn(torch.autograd.Function):
         preact = None
         if act != ACT_NONE:
             preact = torch.empty(x2.shape[0], weight.shape[0], device=x.device, dtype=x.dtype)
+        ctx.x8 = None
         if fp8 is not None:
             from .fp8 import fp8_forward
             if res2 is not None and not res2.is_contiguous():
                 res2 = res2.contiguous()
-            y = fp8_forward(x2, weight, bias, res2, act, preact, fp8)
+            if fp8.wgrad and ctx.needs_input_grad[1]:
+                # keep the e4m3 input (and its scale) for the fp8 weight gradient
+                y, x8, xs = fp8_forward(x2, weight, bias, res2, act, preact, fp8, keep=True)
+                ctx.x8 = (x8, xs, fp8)
+            else:
+                y = fp8_forward(x2, weight, bias, res2, act, preact, fp8)
         elif native:
             y = _ext.ops().gemm(x2, weight, False, True, bias, res2, act, preact, None, False, 0, False, None, -1)
         else:
@@ -207,11 +213,21 @@ class _LinearFn(torch.autograd.Function):
             gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
             w_acc = _direct_grad(weight) if native else None
-            if w_acc is not None:  # accumulate straight into the flat gradient buffer
+            if ctx.x8 is not None and _fp8_wgrad_ok(dh, ctx.x8[0]):
+                # fp8 weight gradient: e5m2 dY · the forward's e4m3 input
+                from .fp8 import fp8_wgrad
+                x8, xs, st = ctx.x8
+                if w_acc is not None:
+                    fp8_wgrad(dh, x8, xs, st, out=w_acc, accumulate=True)
+                    _notify(weight)
+                else:
+                    gw = fp8_wgrad(dh, x8, xs, st).to(weight.dtype)
+            elif w_acc is not None:  # accumulate straight into the flat gradient buffer
                 gemm(dh, x2, ta=True, split_k=-1, out=w_acc, accumulate=True)
                 _notify(weight)
             else:
                 gw = gemm(dh, x2, ta=True, split_k=-1, out_dtype=weight.dtype)  # split-K chosen natively
+        ctx.x8 = None
         if want_b:
             if db_acc is not None:
                 _notify(bias)
@@ -261,7 +277,22 @@ def _bias_grad(g2, bias, native):
     return db.to(bias.dtype)
 
 
-def _wgrad(g2, x2, weight, native):
+def _fp8_wgrad_ok(dy2, x8):
+    from .fp8 import fp8_wgrad_ok
+    return fp8_wgrad_ok(dy2, x8)
+
+
+def _wgrad(g2, x2, weight, native, x8=None):
+    """Weight gradient g2ᵀ·x2 into the flat gradient view (or returned).  ``x8``: (e4m3 x2, its scale,
+    Fp8State) kept by an fp8 forward → the fp8 weight-gradient GEMM (e5m2 g2)."""
+    if x8 is not None and _fp8_wgrad_ok(g2, x8[0]):
+        from .fp8 import fp8_wgrad
+        acc = _direct_grad(weight) if native else None
+        if acc is not None:
+            fp8_wgrad(g2, x8[0], x8[1], x8[2], out=acc, accumulate=True)
+            _notify(weight)
+            return None
+        return fp8_wgrad(g2, x8[0], x8[1], x8[2]).to(weight.dtype)
     acc = _direct_grad(weight) if native else None
     if acc is not None:
         gemm(g2, x2, ta=True, split_k=-1, out=acc, accumulate=True)
@@ -282,11 +313,19 @@ class _MLPFn(torch.autograd.Function):
         res2 = residual.reshape(-1, w2.shape[0]).contiguous() if residual is not None else None
         ops = _ext.ops()
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
+        ctx.x8 = (None, None)
         if fp8 is not None:  # (state of layer 1, state of layer 2 or None): e4m3 forward GEMMs
             from .fp8 import fp8_forward
             # layer 2's e4m3 input comes out of layer 1's epilogue (its delayed scale permitting)
-            u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1])
-            if fp8[1] is not None:
+            if ctx.needs_input_grad[1] and fp8[0].wgrad:  # the e4m3 inputs are kept for the fp8 weight gradients
+                u, x8, xs = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1], keep=True)
+                ctx.x8 = ((x8, xs, fp8[0]), None)
+            else:
+                u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1])
+            if fp8[1] is not None and ctx.needs_input_grad[3] and fp8[1].wgrad:
+                y, u8, us = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1], keep=True)
+                ctx.x8 = (ctx.x8[0], (u8, us, fp8[1]))
+            elif fp8[1] is not None:
                 y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
             else:
                 y = ops.gemm(u, w2, False, True, b2, res2, ACT_NONE, None, None, False, 0, False, None, -1)
@@ -303,7 +342,9 @@ class _MLPFn(torch.autograd.Function):
         ops = _ext.ops()
         gy2 = gy.reshape(-1, w2.shape[0]).contiguous()
         nig = ctx.needs_input_grad
-        gw2 = _wgrad(gy2, u, w2, True) if nig[3] else None
+        x8_1, x8_2 = ctx.x8
+        ctx.x8 = (None, None)
+        gw2 = _wgrad(gy2, u, w2, True, x8_2) if nig[3] else None
         gb2 = _bias_grad(gy2, ctx.b2, True) if nig[4] else None
         b1 = ctx.b1
         b1_acc = None
@@ -318,7 +359,7 @@ class _MLPFn(torch.autograd.Function):
             gb1 = None
         else:
             gb1 = _bias_grad(dh, b1, True) if nig[2] else None
-        gw1 = _wgrad(dh, x2, w1, True) if nig[1] else None
+        gw1 = _wgrad(dh, x2, w1, True, x8_1) if nig[1] else None
         gx = ops.gemm(dh, w1, False, False, None, None, ACT_NONE, None, None, False, 0, False, None, -1)
         return (gx.reshape(ctx.shp) if nig[0] else None, gw1, gb1, gw2, gb2, None,
                 gy if ctx.has_res else None, None)

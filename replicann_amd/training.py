@@ -308,7 +308,7 @@ class Trainer:
         from .ops import rng as dev_rng
         # fp8 delayed-scaling slots are NOT rolled back: the warm-ups seed them, so the captured step
         # is the steady-state (delayed-scaling) step, not a first step frozen into every replay
-        bufs = [b for n, b in self.model.named_buffers() if not n.endswith("fp8_scales")]
+        bufs = [b for n, b in self.model.named_buffers() if not n.endswith(("fp8_scales", "fp8_gscales"))]
         state = self.opt.state_tensors() + bufs + dev_rng.state_tensors(self.device)
         snap = [t.clone() for t in state]
         count = self.opt.step_count

@@ -1,0 +1,95 @@
+"""fp8 weight gradient (csrc/include/gemm_pk.h, MN-contiguous fp8 operands read by the transposing
+ds_read_b64_tr_b8; csrc/kernels/fp8.hip rn_gemm_fp8_wgrad): dW = dYᵀ·X with dY in e5m2 and X in
+e4m3, both as the step produced them (token-major), fp32 split-K slabs + fixed-order reduction.
+
+Checked against fp32 math on the DEQUANTISED operands (so only the GEMM is under test, not the
+quantisation), for GPT-2-medium shapes, ragged tiles (widths multiples of 16, not of 256), both
+output dtypes, accumulate, and bitwise run-to-run determinism; and the e5m2 quantiser against
+torch's float8_e5m2 cast."""
+
+import pytest
+import torch
+
+from replicann_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (tokens K, M = out features, N = in features)
+    (16384, 3072, 1024),   # GPT-2-medium c_attn (K = 16 sequences)
+    (8192, 4096, 1024),    # c_fc
+    (8192, 1024, 4096),    # mlp c_proj
+    (1024, 400, 272),      # ragged M / N
+    (128, 256, 256),       # one K-tile
+]
+
+
+def _q(dy, x):
+    gs = torch.zeros(4, device=dy.device)
+    dy8 = torch.ops.replicann.bf8_quantize(dy, gs, False)
+    x8, xs = ops.quantize_fp8(x)
+    return dy8, gs, x8, xs
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_fp8_wgrad_vs_fp32_on_dequantised(cuda, shape, out_dtype):
+    K, M, N = shape
+    g = torch.Generator(device="cpu").manual_seed(5)
+    dy = (torch.randn(K, M, generator=g) * 0.01).to(cuda, torch.bfloat16)
+    x = torch.randn(K, N, generator=g).to(cuda, torch.bfloat16)
+    dy8, gs, x8, xs = _q(dy, x)
+    ref = ops.dequantize_bf8(dy8, gs).float().t() @ ops.dequantize_fp8(x8, xs).float()
+    out = torch.zeros(M, N, device=cuda, dtype=out_dtype)
+    torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, out, False, True)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < (2e-5 if out_dtype == torch.float32 else 4e-3), err
+    # accumulate into an existing gradient
+    base = torch.randn(M, N, generator=g).to(cuda, out_dtype)
+    acc = base.clone()
+    torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, acc, True, True)
+    err2 = ((acc.float() - (base.float() + ref)).norm() / (base.float() + ref).norm()).item()
+    assert err2 < (2e-5 if out_dtype == torch.float32 else 4e-3), err2
+    # deterministic (fixed slab order)
+    out2 = torch.zeros_like(out)
+    torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, out2, False, True)
+    assert torch.equal(out, out2)
+
+
+def test_bf8_quantiser_matches_torch_cast(cuda):
+    x = torch.randn(4096, 256, device=cuda).bfloat16() * 3
+    st = torch.zeros(4, device=cuda)
+    q = torch.ops.replicann.bf8_quantize(x, st, False)
+    scale = float(st[0])
+    assert abs(scale - float(x.float().abs().max()) / 57344.0) < 1e-9 + 1e-6 * scale
+    ref = (x.float() / scale).to(torch.float8_e5m2).view(torch.uint8)
+    assert (q != ref).float().mean().item() < 1e-3  # round-to-nearest-even on both sides
+    # delayed pass: scale from the recorded amax (x2 headroom), new amax recorded
+    q2 = torch.ops.replicann.bf8_quantize(x * 0.5, st, True)
+    assert abs(float(st[0]) - 2 * float(x.float().abs().max()) / 57344.0) < 1e-6 * float(st[0]) + 1e-12
+    assert abs(float(st[1]) - 0.5 * float(x.float().abs().max())) < 1e-3 * float(st[1])
+    deq = ops.dequantize_bf8(q2, st).float()
+    assert ((deq - x.float() * 0.5).norm() / (x.float() * 0.5).norm()) < 0.1
+
+
+def test_fp8_model_wgrad_tracks_bf16_wgrad(cuda):
+    """GPT-2 (tiny, fp8 layers) one backward: fp8 weight gradients within fp8 tolerance of the bf16
+    weight-gradient path on the same forward."""
+    import replicann_amd as R
+    from replicann_amd.ops.fp8 import fp8_states
+
+    ids = torch.randint(0, 1000, (8, 128), device=cuda, generator=torch.Generator(device=cuda).manual_seed(2))
+    grads = {}
+    for wg in (False, True):
+        torch.manual_seed(0)
+        m = R.GPT2(R.GPT2Config.tiny(fp8=True)).to(cuda)
+        for p in m.parameters():
+            p.data = p.data.bfloat16()
+        for st in fp8_states(m):
+            st.wgrad = wg
+        m(ids, ids).backward()
+        grads[wg] = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+    names = [n for n in grads[True] if n.endswith(("c_attn.weight", "c_fc.weight", "mlp.c_proj.weight"))]
+    assert names
+    for n in names:
+        a, b = grads[True][n], grads[False][n]
+        assert ((a - b).norm() / b.norm()) < 0.08, n
