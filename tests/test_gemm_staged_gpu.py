@@ -51,8 +51,8 @@ def _run(case, dev, staged):
             bg = torch.zeros(N, device=dev, dtype=torch.bfloat16)
             y = torch.ops.replicann.gemm(A, B, False, False, None, None, act, aux, None, False, 1, False, None, 9, bg)
             extra = bg
-        elif kind == "res":
-            bias = torch.randn(N, device=dev).bfloat16()
+        elif kind == "res":  # (a seeded bias: both runs must see the same one)
+            bias = torch.randn(N, generator=torch.Generator(device="cpu").manual_seed(4)).to(dev, torch.bfloat16)
             y = ops.gemm(A, B, tb=True, bias=bias, residual=aux, cfg=9, split_k=1)
             extra = None
         else:
