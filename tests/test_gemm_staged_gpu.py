@@ -82,7 +82,10 @@ def test_staged_epilogue_bitwise_equal_and_correct(cuda, case):
         ref = h.bfloat16().float() * (0.5 * (1 + t) + 0.5 * x * (1 - t * t) * 0.7978845608 * (1 + 3 * 0.044715 * x * x))
     elif kind == "act3":
         ref = h.bfloat16().float() * (aux.float() > 0).float()
-    else:  # res / acc: the residual / accumulate target added (res also adds a bias: skip that term)
+    elif kind == "res":  # bias + residual
+        bias = torch.randn(N, generator=torch.Generator(device="cpu").manual_seed(4)).to(h.device, torch.bfloat16)
+        ref = h + bias.float() + aux.float()
+    else:  # acc: checked below
         ref = None
     if ref is not None:
         err = (ys.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-6)
