@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--act", type=int, default=0,
                     help="epilogue: 0 none, 2 GELU + pre-activation store (fc fwd), 4 GELU backward reading it")
     ap.add_argument("--bias", action="store_true")
+    ap.add_argument("--res", action="store_true", help="residual epilogue (full-tile operand read)")
     a = ap.parse_args()
     ta, tb = a.layout[0] == "t", a.layout[1] == "t"
     torch.manual_seed(0)
@@ -41,8 +42,9 @@ def main():
     else:
         bias = torch.randn(a.N, device="cuda").bfloat16() if a.bias else None
         pre = torch.randn(a.M, a.N, device="cuda").bfloat16() if a.act else None
+        res = torch.randn(a.M, a.N, device="cuda").bfloat16() if a.res else None
         fn = lambda: ops.gemm(A, B, ta=ta, tb=tb, cfg=a.cfg, split_k=a.split, bias=bias, act=a.act,  # noqa: E731
-                              preact=pre)
+                              preact=pre, residual=res)
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
@@ -54,7 +56,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     print(json.dumps({"M": a.M, "N": a.N, "K": a.K, "layout": a.layout, "cfg": a.cfg, "split": a.split,
-                      "torch": a.torch, "act": a.act, "ms": round(ms, 4),
+                      "torch": a.torch, "act": a.act, "res": a.res,
+                      "staged": int(os.environ.get("REPLICANN_GEMM_STAGED", "1") != "0"), "ms": round(ms, 4),
                       "tflops": round(2 * a.M * a.N * a.K / ms / 1e9, 1)}), flush=True)
 
 

@@ -19,6 +19,12 @@ for r in 1 2; do
   step proxy_graph_$r 300 python bench.py --steps 10 --warmup 3 --ddp on --comm proxy || exit 1
   step proxy_eager_$r 300 python bench.py --steps 10 --warmup 3 --ddp on --comm proxy --graph off || exit 1
 done
+step pmc_staged 600 bash scripts/pmc_staged.sh || exit 1
+python scripts/pmc_summary.py gpurun_out/pmc_stg/*_counter_collection.csv --match gemm_pk > gpurun_out/pmc_staged_summary.txt 2>&1
+step pmc_attn 400 bash scripts/pmc_attn.sh "64 --rounds 1" attn4 || exit 1
+python scripts/pmc_summary.py gpurun_out/pmc_attn/attn4*_counter_collection.csv --match attn > gpurun_out/pmc_attn_summary.txt 2>&1
 step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_4b -o run -- python3 bench.py --steps 3 --warmup 2 || exit 1
 python scripts/prof_steps.py gpurun_out/prof_4b/run_kernel_trace.csv --steps 3 > gpurun_out/prof_4b_steps.txt 2>&1
+step prof_vit 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_4b_vit -o run -- python3 bench.py --model vit-b16 --steps 3 --warmup 2 || exit 1
+python scripts/prof_steps.py gpurun_out/prof_4b_vit/run_kernel_trace.csv --steps 3 > gpurun_out/prof_4b_vit_steps.txt 2>&1
 exit 0

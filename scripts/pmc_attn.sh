@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc_attn
 set -e
-ARGS="${1:-64 --fwd 3 --bwd 1 --rounds 1}"
+ARGS="${1:-64 --rounds 1}"
 TAG="${2:-attn}"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
    --kernel-trace --output-format csv -d gpurun_out/pmc_attn -o ${TAG}_a -- python3 scripts/attn_ab.py $ARGS > /dev/null 2>&1
