@@ -71,39 +71,67 @@ def main():
     print(f"wrote {out} ({os.path.getsize(out) / 2**20:.1f} MiB), cases: {sorted(gx)}")
 
 
-def param_grads(mod, prefix=""):
-    """{state_dict key: .grad} for every parameter (fp16: the fixture travels to the GPU box)."""
-    # (a parameter the path does not use — the encoder's _attn._proj under return_kv, quirk Q5 — has
-    # no .grad: recorded as an empty tensor, and the native path must not produce one either)
-    return {prefix + n: (p.grad.detach().half() if p.grad is not None else torch.empty(0))
-            for n, p in mod.named_parameters()}
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def _block(tr, cls, H, E, seed, dtype, **kw):
+    torch.manual_seed(0)
+    m = refgen.zero_dropout(getattr(tr, cls)(H, E, **kw)).train()
+    m.load_state_dict(refgen.det_state_dict(m, seed), strict=True)
+    m = m.to(dtype)
+    if hasattr(m, "_attn_mask"):
+        m._attn_mask = m._attn_mask.float()  # the reference accepts only an fp32 mask (quirk Q3)
+    return m
+
+
+def _case(tr, i, dtype):
+    name, cls, H, E, T, kw = refgen.GRAD_CASES[i]
+    m = _block(tr, cls, H, E, 600 + i, dtype, **kw)
+    x = refgen.det_input((2, T, E), 700 + i).to(dtype).requires_grad_()
+    y = m(x)
+    y.backward(refgen.det_grad(y.shape, 800 + i).to(dtype))
+    return y.detach(), x.grad, {n: p.grad for n, p in m.named_parameters()}
+
+
+def _cross(tr, dtype):
+    name, H, E, Ts, Tt = refgen.GRAD_CROSS
+    enc = _block(tr, "TransformerEncoder", H, E, 900, dtype)
+    dec = _block(tr, "TransformerCrossDecoder", H, E, 901, dtype, context_size=64)
+    src = refgen.det_input((2, Ts, E), 902).to(dtype).requires_grad_()
+    tgt = refgen.det_input((2, Tt, E), 903).to(dtype).requires_grad_()
+    _, k, v = enc(src, return_kv=True)
+    y = dec(tgt, k, v)
+    y.backward(refgen.det_grad(y.shape, 904).to(dtype))
+    grads = {**{"enc." + n: p.grad for n, p in enc.named_parameters()},
+             **{"dec." + n: p.grad for n, p in dec.named_parameters()}}
+    return y.detach(), src.grad, tgt.grad, grads
+
+
+def _floor(g32, g16):
+    """Per-parameter bf16 floor: the relative L2 error of the REFERENCE's own code run in bf16 (CPU)
+    against its fp32 gradients — what "within bf16 tolerance" means for each gradient."""
+    return torch.tensor([_rel(g16[n], g32[n]) if g32[n] is not None else 0.0 for n in g32])
 
 
 def grad_fixtures(tr):
     """Train mode, all dropout at p = 0: outputs, input gradients and EVERY parameter gradient of the
     reference blocks (the native optimizer consumes the parameter gradients, through the fused-QKV
-    flat-buffer views)."""
+    flat-buffer views), plus each gradient's bf16 floor (the reference itself evaluated in bf16)."""
     fx = {}
     for i, (name, cls, H, E, T, kw) in enumerate(refgen.GRAD_CASES):
-        torch.manual_seed(0)
-        m = refgen.zero_dropout(getattr(tr, cls)(H, E, **kw)).train()
-        m.load_state_dict(refgen.det_state_dict(m, 600 + i), strict=True)
-        x = refgen.det_input((2, T, E), 700 + i)
-        y, (g,) = fwd_bwd(m, x, gseed=800 + i)
-        fx[name] = {"y": y.half(), "gx": g.half(), "params": param_grads(m)}
-    name, H, E, Ts, Tt = refgen.GRAD_CROSS
-    torch.manual_seed(0)
-    enc = refgen.zero_dropout(tr.TransformerEncoder(H, E)).train()
-    dec = refgen.zero_dropout(tr.TransformerCrossDecoder(H, E, context_size=64)).train()
-    enc.load_state_dict(refgen.det_state_dict(enc, 900), strict=True)
-    dec.load_state_dict(refgen.det_state_dict(dec, 901), strict=True)
-    src = refgen.det_input((2, Ts, E), 902).requires_grad_()
-    tgt = refgen.det_input((2, Tt, E), 903).requires_grad_()
-    _, k, v = enc(src, return_kv=True)
-    y = dec(tgt, k, v)
-    y.backward(refgen.det_grad(y.shape, 904))
-    fx[name] = {"y": y.detach().half(), "g_src": src.grad.half(), "g_tgt": tgt.grad.half(),
-                "params": {**param_grads(enc, "enc."), **param_grads(dec, "dec.")}}
+        y, gx, g32 = _case(tr, i, torch.float32)
+        _, _, g16 = _case(tr, i, torch.bfloat16)
+        fx[name] = {"y": y.half(), "gx": gx.half(),
+                    "params": {n: (g.half() if g is not None else torch.empty(0)) for n, g in g32.items()},
+                    "floor_names": list(g32), "floor": _floor(g32, g16)}
+    name = refgen.GRAD_CROSS[0]
+    y, gs, gt, g32 = _cross(tr, torch.float32)
+    _, _, _, g16 = _cross(tr, torch.bfloat16)
+    fx[name] = {"y": y.half(), "g_src": gs.half(), "g_tgt": gt.half(),
+                "params": {n: (g.half() if g is not None else torch.empty(0)) for n, g in g32.items()},
+                "floor_names": list(g32), "floor": _floor(g32, g16)}
     return fx
 
 

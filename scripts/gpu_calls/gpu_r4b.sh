@@ -13,6 +13,10 @@ for r in 1 2; do
   step plain_$r 300 python bench.py --steps 10 --warmup 3 || exit 1
   REPLICANN_GEMM_STAGED=0 step unstaged_$r 300 python bench.py --steps 10 --warmup 3 || exit 1
 done
+for r in 1 2; do
+  REPLICANN_FP8_WGRAD=0 step m8_bf16w_$r 300 python bench.py --model gpt2-medium-fp8 --steps 6 --warmup 3 || exit 1
+  REPLICANN_FP8_WGRAD=1 step m8_fp8w_$r 300 python bench.py --model gpt2-medium-fp8 --steps 6 --warmup 3 || exit 1
+done
 step pmc_staged 600 bash scripts/pmc_staged.sh || exit 1
 python scripts/pmc_summary.py gpurun_out/pmc_stg/*_counter_collection.csv --match gemm_pk > gpurun_out/pmc_staged_summary.txt 2>&1
 step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_4b -o run -- python3 bench.py --steps 3 --warmup 2 || exit 1

@@ -108,9 +108,15 @@ def _train_block(cls, H, E, seed, dev, dtype, flat, **kw):
     return m, fp
 
 
-def _check_param_grads(named, ref, tol, where):
+def _check_param_grads(named, fixture, tol, where):
     """Every state_dict parameter's gradient vs the reference's (relative L2); a parameter the
-    reference path leaves without a gradient must have none (or an all-zero one) here too."""
+    reference path leaves without a gradient must have none (or an all-zero one) here too.
+
+    ``tol`` None = bf16 tolerance per gradient: 1.25 x the error of the REFERENCE's own code run in
+    bf16 against its fp32 gradients (recorded in the fixture; up to 6.5 % on the FFN upscale: with
+    96-160 tokens a few bf16-rounded pre-activations cross the ReLU), at least 2 %."""
+    ref = fixture["params"]
+    floor = dict(zip(fixture["floor_names"], fixture["floor"].tolist()))
     for n, p in named:
         r = ref[n]
         if r.numel() == 0:
@@ -118,7 +124,8 @@ def _check_param_grads(named, ref, tol, where):
             continue
         assert p.grad is not None, (where, n)
         e = rel(p.grad, r)
-        assert e < tol, (where, n, e)
+        t = tol if tol is not None else max(2e-2, 1.25 * floor[n])
+        assert e < t, (where, n, e, t)
 
 
 def _param_case(gfx, i, dev, dtype, flat, tol):
@@ -128,12 +135,13 @@ def _param_case(gfx, i, dev, dtype, flat, tol):
     x = refgen.det_input((2, T_, E), 700 + i).to(dev, dtype).requires_grad_()
     y = m(x)
     y.backward(refgen.det_grad(y.shape, 800 + i).to(dev, dtype))
-    assert rel(y, ref["y"]) < tol, name
-    assert rel(x.grad, ref["gx"]) < tol, name
+    t = tol if tol is not None else 3e-2
+    assert rel(y, ref["y"]) < t, name
+    assert rel(x.grad, ref["gx"]) < t, name
     if fp is not None:  # the gradients ARE the flat buffer (what the fused optimizer reads)
         for p, o, n in fp.segments():
             assert p.grad.data_ptr() == fp.grad[o:o + n].data_ptr()
-    _check_param_grads(m.named_parameters(), ref["params"], tol, name)
+    _check_param_grads(m.named_parameters(), ref, tol, name)
 
 
 def _param_cross(gfx, dev, dtype, flat, tol):
@@ -146,10 +154,11 @@ def _param_cross(gfx, dev, dtype, flat, tol):
     _, k, v = enc(src, return_kv=True)
     y = dec(tgt, k, v)
     y.backward(refgen.det_grad(y.shape, 904).to(dev, dtype))
-    assert rel(y, ref["y"]) < tol
-    assert rel(src.grad, ref["g_src"]) < tol and rel(tgt.grad, ref["g_tgt"]) < tol
+    t = tol if tol is not None else 3e-2
+    assert rel(y, ref["y"]) < t
+    assert rel(src.grad, ref["g_src"]) < t and rel(tgt.grad, ref["g_tgt"]) < t
     named = [("enc." + n, p) for n, p in enc.named_parameters()] + [("dec." + n, p) for n, p in dec.named_parameters()]
-    _check_param_grads(named, ref["params"], tol, name)
+    _check_param_grads(named, ref, tol, name)
 
 
 @pytest.mark.gpu
@@ -158,16 +167,14 @@ def _param_cross(gfx, dev, dtype, flat, tol):
 def test_param_grads_gpu_vs_reference(cuda, gfx, i, flat):
     """Native bf16 training path (fused QKV through the flat-buffer views, fused attention backward,
     LayerNorm backward with the residual gradient, GEMM epilogues, direct accumulation) vs the
-    reference's fp32 parameter gradients.  Tolerance 6e-2 (relative L2): with 128-160 tokens a few
-    bf16-rounded pre-activations land on the other side of the FFN's ReLU, and each such flip moves
-    a whole row of the upscale gradient (measured worst case 4.5 %, the decoder's _ffn._upscale)."""
-    _param_case(gfx, i, cuda, torch.bfloat16, flat, 6e-2)
+    reference's fp32 parameter gradients, each within its bf16 tolerance (_check_param_grads)."""
+    _param_case(gfx, i, cuda, torch.bfloat16, flat, None)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("flat", [False, True], ids=["autograd", "flat"])
 def test_param_grads_cross_gpu_vs_reference(cuda, gfx, flat):
-    _param_cross(gfx, cuda, torch.bfloat16, flat, 6e-2)
+    _param_cross(gfx, cuda, torch.bfloat16, flat, None)
 
 
 @pytest.mark.parametrize("flat", [False, True], ids=["autograd", "flat"])
