@@ -92,6 +92,8 @@ void rn_bf8_dequantize(const void*, long, const float*, void*, hipStream_t);
 long rn_gemm_fp8_wgrad_ws(int, int, int);
 int rn_gemm_fp8_wgrad(const void*, const void*, void*, const float*, const float*, float*, float*, int, int, int, long,
                       long, long, int, int, int, hipStream_t);
+int rn_gemm_fp8_dgrad(const void*, const void*, void*, const float*, const float*, float*, int, int, int, long, long,
+                      long, int, hipStream_t);
 int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
                 int, int, int, long, long, long, int, hipStream_t, void*, float*);
 long rn_bn_ws_floats(int, int);
@@ -978,6 +980,21 @@ void gemm_fp8_wgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const 
     TORCH_CHECK(rc == 0, "gemm_fp8_wgrad: M, N and row strides must be multiples of 16 and K of 128, got M=", M,
                 " N=", N, " K=", K);
 }
+// fp8 data gradient: dY8 [M][K] (e5m2 if a_bf8) · W8 [K][N] (the e4m3 weight as stored) -> bf16 [M][N]
+Tensor gemm_fp8_dgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb, bool a_bf8) {
+    GUARD(a8);
+    TORCH_CHECK(a8.scalar_type() == at::kByte && b8.scalar_type() == at::kByte, "fp8 operands are uint8 storage");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.size(1) == b8.size(0) && a8.stride(1) == 1 && b8.stride(1) == 1);
+    const int M = a8.size(0), K = a8.size(1), N = b8.size(1);
+    Tensor c = at::empty({M, N}, a8.options().dtype(at::kBFloat16));
+    Tensor alpha = at::empty({1}, a8.options().dtype(at::kFloat));
+    if (M == 0) return c;
+    int rc = rn_gemm_fp8_dgrad(a8.data_ptr(), b8.data_ptr(), c.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(),
+                               alpha.data_ptr<float>(), M, N, K, a8.stride(0), b8.stride(0), c.stride(0), a_bf8 ? 1 : 0,
+                               cur_stream());
+    TORCH_CHECK(rc == 0, "gemm_fp8_dgrad: K, N and row strides must be multiples of 16, got K=", K, " N=", N);
+    return c;
+}
 Tensor fp8_dequantize(const Tensor& q, const Tensor& state) {
     GUARD(q);
     Tensor y = at::empty(q.sizes(), q.options().dtype(at::kBFloat16));
@@ -1093,6 +1110,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("bf8_quantize(Tensor x, Tensor(a!) state, bool delayed) -> Tensor");
     m.def("bf8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("gemm_fp8_wgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) out, bool accumulate, bool a_bf8) -> ()");
+    m.def("gemm_fp8_dgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, bool a_bf8) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("gemm_fp8_q8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, int act, Tensor(a!) preact, Tensor(b!) q8_state) -> (Tensor, Tensor)");
     m.def("fp8_quant_many(Tensor flat, Tensor segs, int max_n, Tensor(a!) qbuf, bool roll=True) -> ()");
@@ -1152,6 +1170,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("bf8_quantize", &bf8_quantize);
     m.impl("bf8_dequantize", &bf8_dequantize);
     m.impl("gemm_fp8_wgrad", &gemm_fp8_wgrad);
+    m.impl("gemm_fp8_dgrad", &gemm_fp8_dgrad);
     m.impl("gemm_fp8", &gemm_fp8);
     m.impl("gemm_fp8_q8", &gemm_fp8_q8);
     m.impl("fp8_quant_many", &fp8_quant_many);

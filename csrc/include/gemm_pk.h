@@ -216,6 +216,10 @@ RN_DEV u32x4 pk_rsrc_u(const void* base, uint32_t bytes) {
 RN_DEV void pk_st16(const u32x4 v, const u32x4& rs, uint32_t voff) {
     asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen " RN_PK_ST_POLICY "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+RN_DEV void pk_st8(const u32x2v v, const u32x4& rs, uint32_t voff) {
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
 RN_DEV void pk_st16_nt(const u32x4 v, const u32x4& rs, uint32_t voff) {
     asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
 }
@@ -282,15 +286,21 @@ RN_DEV int pk_deq_take(uint32_t v) {
 template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false,
           bool STG = false>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
-    // FP8: 0 bf16; 1 e4m3 x e4m3; 2 A e5m2 (a gradient) x B e4m3.  Operands both K-contiguous (the
-    // forward) or both MN-contiguous (the weight gradient: fp32 split-K slabs only)
-    static_assert(!FP8 || (AK == BKC && !(DBG & 8)), "fp8: both operands K- or both MN-contiguous");
-    static_assert(!FP8 || AK || SPLIT, "fp8 MN-contiguous: split-K slab output only");
-    constexpr bool F8MN = FP8 && !AK;
+    // FP8: 0 bf16; 1 e4m3 x e4m3; 2 A e5m2 (a gradient) x B e4m3.  Operand layouts: both K-contiguous
+    // (the forward x·Wᵀ), A K- and B MN-contiguous (the data gradient dY·W), both MN-contiguous (the
+    // weight gradient dYᵀ·X: fp32 split-K slabs only)
+    static_assert(!FP8 || !(DBG & 8), "fp8: no DBG 8");
+    static_assert(!FP8 || AK || (!BKC && SPLIT), "fp8 MN-contiguous A: weight gradient (both MN, split-K slabs) only");
+    constexpr bool F8A_MN = FP8 && !AK;   // fp8 MN-contiguous images, read by transposing tr_b8 reads
+    constexpr bool F8B_MN = FP8 && !BKC;
+    constexpr bool F8MN = F8A_MN;  // (A MN implies B MN)
+    // fp8 MN B: each lane holds two runs of 4 output columns (see the epilogue's column map), so a
+    // bf16 output takes two 8-byte stores per fragment row; plain epilogue only
+    static_assert(!F8B_MN || SPLIT || (ACT == ACT_NONE && !F32), "fp8 MN B, bf16 output: plain epilogue only");
+    constexpr int S_EPI = (DBG & 64) ? 0 : pk_epi_stores<ACT, SPLIT, F32>() + ((F8B_MN && !SPLIT) ? 16 : 0);
     static_assert(!DYN || (!FP8 && DBG == 0), "dynamic schedule: bf16 production kernels only");
     static_assert(!STG || (!SPLIT && !F32 && !DYN && !FP8 && DBG == 0), "staged epilogue: bf16 static walk only");
     constexpr int BM = 256, BN = 256;
-    constexpr int S_EPI = (DBG & 64) ? 0 : pk_epi_stores<ACT, SPLIT, F32>();
     constexpr int WY = 6;  // ops younger than a phase's target half-tile: 3 half-tiles × 2 DMA
     static_assert(WY + 1 + S_EPI <= 63, "vmcnt range");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -357,7 +367,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         if (kc) {
             mn = ins * 8 + (lane >> 3);
             k = ((lane & 7) ^ (isA ? swz_kc(mn) : swz_kcp(mn))) * 8;
-        } else if (F8MN) {  // k: byte row 0..127 of the fp8 MN image; mn: byte column
+        } else if (FP8) {  // k: byte row 0..127 of the fp8 MN image; mn: byte column
             k = ins * 8 + (lane >> 3);
             mn = ((lane & 7) ^ swz_f8(k)) * 16;
         } else {
@@ -371,14 +381,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         int mn, k;
         lane_mnk(true, i, mn, k);
         // (fp8 MN: lda / ldb in BYTES, offsets in bytes)
-        a_off[i] = (uint32_t)(F8MN ? (long)k * p.lda + mn : (AK ? (long)mn * p.lda + k : (long)k * p.lda + mn) * 2);
+        a_off[i] = (uint32_t)(F8A_MN ? (long)k * p.lda + mn : (AK ? (long)mn * p.lda + k : (long)k * p.lda + mn) * 2);
         lane_mnk(false, i, mn, k);
-        b_off[i] = (uint32_t)(F8MN ? (long)k * p.ldb + mn : (BKC ? (long)mn * p.ldb + k : (long)k * p.ldb + mn) * 2);
+        b_off[i] = (uint32_t)(F8B_MN ? (long)k * p.ldb + mn : (BKC ? (long)mn * p.ldb + k : (long)k * p.ldb + mn) * 2);
     }
     const long a_step = AK ? (long)BK : (long)BK * p.lda, b_step = BKC ? (long)BK : (long)BK * p.ldb;
     // (fp8 MN: one K-tile = 128 k rows of lda bytes = 64·lda bf16 elements, the a_step formula; the
     // second half-tile starts 128 mn BYTES = 64 bf16 elements in)
-    const long a_half = AK ? 128L * p.lda : (F8MN ? 64L : 128L), b_half = BKC ? 128L * p.ldb : (F8MN ? 64L : 128L);
+    const long a_half = AK ? 128L * p.lda : (F8A_MN ? 64L : 128L), b_half = BKC ? 128L * p.ldb : (F8B_MN ? 64L : 128L);
     // cursor: the K-tile being issued (limits 0 once the block's items are exhausted: every
     // lane then reads out of range and the DMA only zero-fills its slot)
     const bf16* ca = p.A;
@@ -404,8 +414,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     auto cur_set = [&]() {
         int m0, n0, kb, ke, tm;
         item_coords(cu, m0, n0, kb, ke, tm);
-        ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + (F8MN ? m0 / 2 : m0);
-        cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + (F8MN ? n0 / 2 : n0);
+        ca = AK ? p.A + (long)m0 * p.lda + kb : p.A + (long)kb * p.lda + (F8A_MN ? m0 / 2 : m0);
+        cb = BKC ? p.B + (long)n0 * p.ldb + kb : p.B + (long)kb * p.ldb + (F8B_MN ? n0 / 2 : n0);
         cml = p.M - m0;
         cnl = p.N - n0;
         ckl = ke - kb;
@@ -496,7 +506,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                 int mn, kk;
                 lane_mnk(isA, i, mn, kk);
                 const uint32_t o = isA ? a_off[i] : b_off[i];
-                const bool kin = F8MN ? kk < 2 * ckl : kk < ckl;  // (fp8 MN: kk is a k byte, ckl in 2-byte units)
+                const bool f8mn = isA ? F8A_MN : F8B_MN;
+                const bool kin = f8mn ? kk < 2 * ckl : kk < ckl;  // (fp8 MN: kk is a k byte, ckl in 2-byte units)
                 dma16_at(rs, (mn < mnl && kin) ? o : 0xFFFFFFF0u, dst + i * 1024);
             }
         }
@@ -520,11 +531,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     // the B side then in plain column order (fragment j = the wave's columns 16j .. 16j + 15, see the
     // epilogue's column map)
     auto frag_a = [&](const char* half, int mnbase, int s) -> s16x8 {
-        if constexpr (F8MN) return pk_frag8_mn(half, mnbase, s, lane);
+        if constexpr (F8A_MN) return pk_frag8_mn(half, mnbase, s, lane);
         else return pk_frag_a<AK>(half, mnbase, s, lane);
     };
     auto frag_b = [&](const char* half, int j, int s) -> s16x8 {
-        if constexpr (F8MN) return pk_frag8_mn(half, wc * 32 + 16 * j, s, lane);
+        if constexpr (F8B_MN) return pk_frag8_mn(half, wc * 32 + 16 * j, s, lane);
         else return pk_frag_b<BKC>(half, wc * 32, j, s, lane);
     };
 
@@ -541,7 +552,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         // fragments), or for fp8 MN two runs of 4: columns 4G.. (fragment 0) and 16 + 4G.. (fragment 1)
         auto off = [&](int mh, int i, int nh, int es, int dc = 0) -> uint32_t {
             const int r = mh * 128 + wr * 64 + i * 16 + (lane & 15);
-            const int c = nh * 128 + wc * 32 + (F8MN ? 4 : 8) * G + dc;
+            const int c = nh * 128 + wc * 32 + (F8B_MN ? 4 : 8) * G + dc;
             return (r < mlim && c < nlim) ? (uint32_t)(((long)r * ldc + c) * es) : 0xFFFFFFF0u;
         };
         // bias: the wave's 2 × 32 columns through the scalar cache, then each lane picks its 8
@@ -615,7 +626,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 #pragma unroll
                 for (int nh = 0; nh < 2; ++nh) {
                     float v[8];
-                    const bool swp = !BKC && !F8MN && (G & 1);  // bf16 MN image: odd lane groups hold fragment 1 first
+                    const bool swp = !BKC && !F8B_MN && (G & 1);  // bf16 MN image: odd lane groups hold fragment 1 first
 #pragma unroll
                     for (int c = 0; c < 8; ++c) {
                         // compile-time register indices on both sides of the select (a runtime
@@ -625,7 +636,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                     }
                     if constexpr (SPLIT) {
                         const uint32_t o = off(mh, i, nh, 4);
-                        const uint32_t o2 = F8MN ? off(mh, i, nh, 4, 16) : (o == 0xFFFFFFF0u ? o : o + 16);
+                        const uint32_t o2 = F8B_MN ? off(mh, i, nh, 4, 16) : (o == 0xFFFFFFF0u ? o : o + 16);
                         pk_st16((u32x4){__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1]),
                                     __builtin_bit_cast(uint32_t, v[2]), __builtin_bit_cast(uint32_t, v[3])},
                             crs_u, o);
@@ -698,7 +709,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                         const u32x4 ou = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
                                           pk_pack2(v[6], v[7])};
                         if constexpr (DBG & 64) asm volatile("" ::"v"(ou));         // ablation: no stores
-                        else if (p.st_nt & 1) pk_st16_nt(ou, crs_u, o);            // wave-uniform choice
+                        else if constexpr (F8B_MN) {  // columns 4G.. and 16 + 4G..
+                            pk_st8((u32x2v){ou.x, ou.y}, crs_u, o);
+                            pk_st8((u32x2v){ou.z, ou.w}, crs_u, off(mh, i, nh, 2, 16));
+                        } else if (p.st_nt & 1) pk_st16_nt(ou, crs_u, o);          // wave-uniform choice
                         else pk_st16(ou, crs_u, (DBG & 32) ? 0xFFFFFFF0u : o);   // ablation: no traffic
                     }
                 }

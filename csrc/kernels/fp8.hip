@@ -241,6 +241,7 @@ int fp8_gemm_kernel() {
 
 void rn_gemm_launch_pk_fp8(rn_gemm_detail::GemmArgs& a, int act, hipStream_t st);
 void rn_gemm_launch_pk_fp8_wgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
+void rn_gemm_launch_pk_fp8_dgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 
 extern "C" {
 
@@ -360,6 +361,26 @@ int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, 
     a.split = split; a.k_per_split = per * 64; a.out_f32 = out_f32; a.accumulate = accumulate;
     a.slab_step = 1;
     rn_gemm_launch_pk_fp8_wgrad(a, a_bf8, st);
+    return 0;
+}
+
+// C[M,N] (bf16) = sa·sb · A8[M][K] · B8[K][N]: the fp8 data gradient dX = dY·W with dY (A8, e5m2 if
+// a_bf8) K-contiguous and the weight W [out = K][in = N] as stored (the forward's e4m3 weight copy),
+// read transposed.  K, N, lda, ldb, ldc multiples of 16 (bytes for the fp8 operands).
+int rn_gemm_fp8_dgrad(const void* A8, const void* B8, void* C, const float* sa, const float* sb, float* alpha_ws,
+                      int M, int N, int K, long lda, long ldb, long ldc, int a_bf8, hipStream_t st) {
+    if (K % 16 || N % 16 || lda % 16 || ldb % 16 || ldc % 8 || M <= 0) return -1;
+    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
+    rn_gemm_detail::GemmArgs a = {};
+    a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.alpha = alpha_ws;
+    a.M = M; a.N = N; a.K = K / 2;
+    a.lda = lda / 2;  // K-contiguous fp8: bf16-pair units
+    a.ldb = ldb;      // MN-contiguous fp8: bytes
+    a.ldc = ldc;
+    a.tiles_m = (M + 255) / 256;
+    a.tiles_n = (N + 255) / 256;
+    a.split = 1; a.k_per_split = ((K / 2) + 63) / 64 * 64; a.out_f32 = 0; a.accumulate = 0;
+    rn_gemm_launch_pk_fp8_dgrad(a, a_bf8, st);
     return 0;
 }
 

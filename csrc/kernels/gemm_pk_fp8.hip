@@ -23,3 +23,10 @@ void rn_gemm_launch_pk_fp8_wgrad(GemmArgs& a, int a_bf8, hipStream_t st) {
     const int g = (int)std::min<long>((total4 + 255) / 256, 4096);
     splitk_reduce_k<ACT_NONE, true><<<g, 256, 0, st>>>(a);
 }
+
+// fp8 data gradient dX = dY·W: A = dY [M][K] (e5m2 if a_bf8, else e4m3; K-contiguous, as produced),
+// B = W [K][N] (the weight as stored, [out][in] = [K][N]: MN-contiguous, read transposed), bf16 out.
+void rn_gemm_launch_pk_fp8_dgrad(GemmArgs& a, int a_bf8, hipStream_t st) {
+    if (a_bf8) launch_pk_t<true, false, ACT_NONE, false, false, 0, 2>(a, st);
+    else launch_pk_t<true, false, ACT_NONE, false, false, 0, 1>(a, st);
+}

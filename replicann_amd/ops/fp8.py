@@ -25,6 +25,9 @@ E5M2_MAX = 57344.0
 # fp8 weight gradients (dW = dYᵀ·X with dY in e5m2, X the forward's e4m3 copy) of the fp8 layers:
 # REPLICANN_FP8_WGRAD=1 (or Fp8State.wgrad); off by default until measured on the GPU
 FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "0") == "1"
+# fp8 data gradients (dX = dY·W with the same e5m2 dY and the forward's e4m3 weight) of the fp8
+# layers whose dgrad has a plain epilogue: REPLICANN_FP8_DGRAD=1 (or Fp8State.dgrad)
+FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "0") == "1"
 
 
 def quantize_fp8(x):
@@ -66,11 +69,27 @@ def fp8_wgrad_ok(dy2, x8) -> bool:
     return dy2.shape[0] % 128 == 0 and dy2.shape[1] % 16 == 0 and x8.shape[1] % 16 == 0 and dy2.shape[0] > 0
 
 
-def fp8_wgrad(dy2, x8, xs, state, out=None, accumulate=False):
-    """dW = dYᵀ·X in fp8: dY quantised to e5m2 with ``state``'s gradient slot, X = the forward's e4m3
-    copy ``x8`` with scale slot ``xs``.  Accumulates into ``out`` (the flat gradient view) or returns
-    a new bf16 tensor.  CPU: the same quantise → dequantise numerics in fp32."""
-    dy8, gs = state.gquant(dy2)
+def fp8_dgrad_ok(dy2, n_in) -> bool:
+    """Shapes the fp8 data-gradient GEMM takes: both widths % 16."""
+    return dy2.shape[0] > 0 and dy2.shape[1] % 16 == 0 and n_in % 16 == 0
+
+
+def fp8_dgrad(dyq, w8, ws):
+    """dX = dY·W in fp8: ``dyq`` = (e5m2 dY, its scale slot) from :meth:`Fp8State.gquant`, ``w8`` the
+    forward's e4m3 weight [out][in] with scale ``ws`` (read transposed by the kernel: no transposed
+    copy).  Returns bf16 [tokens][in].  CPU: quantise → dequantise numerics in fp32."""
+    dy8, gs = dyq
+    if _ext.use_native(dy8):
+        return _ext.ops().gemm_fp8_dgrad(dy8, w8, gs, ws, True)
+    return (dequantize_bf8(dy8, gs).float() @ dequantize_fp8(w8, ws).float()).to(torch.bfloat16)
+
+
+def fp8_wgrad(dy2, x8, xs, state, out=None, accumulate=False, dyq=None):
+    """dW = dYᵀ·X in fp8: dY quantised to e5m2 with ``state``'s gradient slot (or ``dyq`` = the
+    (e5m2 dY, scale) pair already made for the data gradient), X = the forward's e4m3 copy ``x8``
+    with scale slot ``xs``.  Accumulates into ``out`` (the flat gradient view) or returns a new bf16
+    tensor.  CPU: the same quantise → dequantise numerics in fp32."""
+    dy8, gs = dyq if dyq is not None else state.gquant(dy2)
     if _ext.use_native(dy2):
         if out is None:
             out = torch.zeros(dy2.shape[1], x8.shape[1], device=dy2.device, dtype=torch.bfloat16)
@@ -120,6 +139,8 @@ class Fp8State:
         self.ready = [False, False]
         self.g_ready = False  # gradient slot (fp8 weight gradient's dY) holds a scale
         self.wgrad = FP8_WGRAD
+        self.dgrad = FP8_DGRAD
+        self.w_cached = False  # the last weight quant() came from the optimizer-refreshed cache
         self._offer = None  # (activation tensor, its e4m3 copy) written by the producer kernel
         self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
         self.wcache = None  # Fp8WeightCache holding this GEMM's e4m3 weight (refreshed by the optimizer)
@@ -176,10 +197,17 @@ class Fp8State:
         amax recorded by that kernel); the next quant(x, 0) of the same tensor returns it."""
         self._offer = (x, q)
 
+    @property
+    def fp8_bwd(self):
+        return self.wgrad or self.dgrad
+
     def quant(self, x, i):
+        if i == 1:
+            self.w_cached = False
         if i == 1 and self.wcache is not None:
             q = self.wcache.lookup(self, x)
             if q is not None:
+                self.w_cached = True
                 return q, self.t[1]
         if i == 0 and self._offer is not None:
             src, q = self._offer
@@ -226,17 +254,21 @@ def fp8_forward(x2, weight, bias, res2, act, preact, state: Fp8State, out8: Fp8S
 
     ``out8``: the state of the fp8 GEMM that consumes this output — the epilogue then also writes
     the output in e4m3 with that state's delayed scale and hands it over (no quantisation pass).
-    ``keep``: return (y, x8, scale) — the e4m3 input and a copy of its scale slot, kept for the fp8
-    weight gradient of the backward."""
+    ``keep``: return (y, saved) with saved = (x8, x scale, w8, w scale, state): the e4m3 operands
+    the backward's fp8 weight gradient (x8, if ``state.wgrad``) and data gradient (w8, if
+    ``state.dgrad``) read.  Scale slots a later quant() may roll are copied; the cached weight's slot
+    changes only at the optimizer step, after this backward."""
     xq, xs = state.quant(x2, 0)
-    y = _fp8_forward_q(x2, xq, xs, weight, bias, res2, act, preact, state, out8)
+    wq, ws = state.quant(weight.contiguous(), 1)
+    y = _fp8_forward_q(x2, xq, xs, wq, ws, bias, res2, act, preact, state, out8)
     if keep:
-        return y, xq, xs.clone()
+        x_keep = (xq, xs.clone()) if state.wgrad else (None, None)
+        w_keep = (wq, ws if state.w_cached else ws.clone()) if state.dgrad else (None, None)
+        return y, (*x_keep, *w_keep, state)
     return y
 
 
-def _fp8_forward_q(x2, xq, xs, weight, bias, res2, act, preact, state, out8):
-    wq, ws = state.quant(weight.contiguous(), 1)
+def _fp8_forward_q(x2, xq, xs, wq, ws, bias, res2, act, preact, state, out8):
     if _ext.use_native(x2):
         if (out8 is not None and res2 is None and preact is not None and x2.shape[0] > 0
                 and out8.producer_ready(x2.device)):

@@ -171,10 +171,9 @@ class _LinearFn(torch.autograd.Function):
             from .fp8 import fp8_forward
             if res2 is not None and not res2.is_contiguous():
                 res2 = res2.contiguous()
-            if fp8.wgrad and ctx.needs_input_grad[1]:
-                # keep the e4m3 input (and its scale) for the fp8 weight gradient
-                y, x8, xs = fp8_forward(x2, weight, bias, res2, act, preact, fp8, keep=True)
-                ctx.x8 = (x8, xs, fp8)
+            if fp8.fp8_bwd and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
+                # keep the e4m3 operands for the fp8 weight / data gradients
+                y, ctx.x8 = fp8_forward(x2, weight, bias, res2, act, preact, fp8, keep=True)
             else:
                 y = fp8_forward(x2, weight, bias, res2, act, preact, fp8)
         elif native:
@@ -209,19 +208,24 @@ class _LinearFn(torch.autograd.Function):
             dh, db = _ext.ops().bias_act_grad(gy2, preact if ctx.act != ACT_NONE else None, ctx.act, want_b, db_acc)
         else:
             dh, db = bias_act_grad(gy2, preact, ctx.act, want_b)
+        sv, dyq = _fp8_bwd_operands(ctx, dh, weight)
         if ctx.needs_input_grad[0]:
-            gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp)
+            if dyq is not None and sv[2] is not None:  # fp8 data gradient: e5m2 dY · the e4m3 weight
+                from .fp8 import fp8_dgrad
+                gx = fp8_dgrad(dyq, sv[2], sv[3]).to(x2.dtype).reshape(ctx.shp)
+            else:
+                gx = gemm(dh, weight, out_dtype=x2.dtype).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
             w_acc = _direct_grad(weight) if native else None
-            if ctx.x8 is not None and _fp8_wgrad_ok(dh, ctx.x8[0]):
+            if sv is not None and sv[0] is not None and _fp8_wgrad_ok(dh, sv[0]):
                 # fp8 weight gradient: e5m2 dY · the forward's e4m3 input
                 from .fp8 import fp8_wgrad
-                x8, xs, st = ctx.x8
+                x8, xs, st = sv[0], sv[1], sv[4]
                 if w_acc is not None:
-                    fp8_wgrad(dh, x8, xs, st, out=w_acc, accumulate=True)
+                    fp8_wgrad(dh, x8, xs, st, out=w_acc, accumulate=True, dyq=dyq)
                     _notify(weight)
                 else:
-                    gw = fp8_wgrad(dh, x8, xs, st).to(weight.dtype)
+                    gw = fp8_wgrad(dh, x8, xs, st, dyq=dyq).to(weight.dtype)
             elif w_acc is not None:  # accumulate straight into the flat gradient buffer
                 gemm(dh, x2, ta=True, split_k=-1, out=w_acc, accumulate=True)
                 _notify(weight)
@@ -282,17 +286,33 @@ def _fp8_wgrad_ok(dy2, x8):
     return fp8_wgrad_ok(dy2, x8)
 
 
-def _wgrad(g2, x2, weight, native, x8=None):
+def _fp8_bwd_operands(ctx, dy2, weight):
+    """(saved, dyq): the fp8 forward's kept operands (x8, xs, w8, ws, state) and dY quantised ONCE
+    to e5m2 for whichever of the fp8 data / weight gradients applies (None when neither does)."""
+    sv = ctx.x8
+    ctx.x8 = None
+    if sv is None:
+        return None, None
+    from .fp8 import fp8_dgrad_ok
+    use_d = sv[2] is not None and ctx.needs_input_grad[0] and fp8_dgrad_ok(dy2, weight.shape[1])
+    use_w = sv[0] is not None and ctx.needs_input_grad[1] and _fp8_wgrad_ok(dy2, sv[0])
+    if not (use_d or use_w):
+        return sv, None
+    return sv, sv[4].gquant(dy2)
+
+
+def _wgrad(g2, x2, weight, native, x8=None, dyq=None):
     """Weight gradient g2ᵀ·x2 into the flat gradient view (or returned).  ``x8``: (e4m3 x2, its scale,
-    Fp8State) kept by an fp8 forward → the fp8 weight-gradient GEMM (e5m2 g2)."""
-    if x8 is not None and _fp8_wgrad_ok(g2, x8[0]):
+    Fp8State) kept by an fp8 forward → the fp8 weight-gradient GEMM (e5m2 g2, or ``dyq`` if the data
+    gradient already quantised it)."""
+    if x8 is not None and x8[0] is not None and _fp8_wgrad_ok(g2, x8[0]):
         from .fp8 import fp8_wgrad
         acc = _direct_grad(weight) if native else None
         if acc is not None:
-            fp8_wgrad(g2, x8[0], x8[1], x8[2], out=acc, accumulate=True)
+            fp8_wgrad(g2, x8[0], x8[1], x8[2], out=acc, accumulate=True, dyq=dyq)
             _notify(weight)
             return None
-        return fp8_wgrad(g2, x8[0], x8[1], x8[2]).to(weight.dtype)
+        return fp8_wgrad(g2, x8[0], x8[1], x8[2], dyq=dyq).to(weight.dtype)
     acc = _direct_grad(weight) if native else None
     if acc is not None:
         gemm(g2, x2, ta=True, split_k=-1, out=acc, accumulate=True)
@@ -317,14 +337,16 @@ class _MLPFn(torch.autograd.Function):
         if fp8 is not None:  # (state of layer 1, state of layer 2 or None): e4m3 forward GEMMs
             from .fp8 import fp8_forward
             # layer 2's e4m3 input comes out of layer 1's epilogue (its delayed scale permitting)
-            if ctx.needs_input_grad[1] and fp8[0].wgrad:  # the e4m3 inputs are kept for the fp8 weight gradients
-                u, x8, xs = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1], keep=True)
-                ctx.x8 = ((x8, xs, fp8[0]), None)
+            # the e4m3 operands are kept for the fp8 weight gradients and layer 1's fp8 data gradient
+            # (layer 2's data gradient carries the fused activation backward: bf16)
+            if (ctx.needs_input_grad[1] and fp8[0].wgrad) or (ctx.needs_input_grad[0] and fp8[0].dgrad):
+                u, sv = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1], keep=True)
+                ctx.x8 = (sv, None)
             else:
                 u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1])
             if fp8[1] is not None and ctx.needs_input_grad[3] and fp8[1].wgrad:
-                y, u8, us = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1], keep=True)
-                ctx.x8 = (ctx.x8[0], (u8, us, fp8[1]))
+                y, sv2 = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1], keep=True)
+                ctx.x8 = (ctx.x8[0], sv2)
             elif fp8[1] is not None:
                 y = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1])
             else:
@@ -342,8 +364,9 @@ class _MLPFn(torch.autograd.Function):
         ops = _ext.ops()
         gy2 = gy.reshape(-1, w2.shape[0]).contiguous()
         nig = ctx.needs_input_grad
-        x8_1, x8_2 = ctx.x8
+        sv1, sv2 = ctx.x8
         ctx.x8 = (None, None)
+        x8_2 = (sv2[0], sv2[1], sv2[4]) if sv2 is not None else None
         gw2 = _wgrad(gy2, u, w2, True, x8_2) if nig[3] else None
         gb2 = _bias_grad(gy2, ctx.b2, True) if nig[4] else None
         b1 = ctx.b1
@@ -359,8 +382,19 @@ class _MLPFn(torch.autograd.Function):
             gb1 = None
         else:
             gb1 = _bias_grad(dh, b1, True) if nig[2] else None
-        gw1 = _wgrad(dh, x2, w1, True, x8_1) if nig[1] else None
-        gx = ops.gemm(dh, w1, False, False, None, None, ACT_NONE, None, None, False, 0, False, None, -1)
+        dyq = None
+        if sv1 is not None:
+            from .fp8 import fp8_dgrad, fp8_dgrad_ok
+            use_d = sv1[2] is not None and nig[0] and fp8_dgrad_ok(dh, w1.shape[1])
+            use_w = sv1[0] is not None and nig[1] and _fp8_wgrad_ok(dh, sv1[0])
+            if use_d or use_w:  # dH in e5m2 once, for both
+                dyq = sv1[4].gquant(dh)
+        x8_1 = (sv1[0], sv1[1], sv1[4]) if sv1 is not None else None
+        gw1 = _wgrad(dh, x2, w1, True, x8_1, dyq) if nig[1] else None
+        if dyq is not None and sv1[2] is not None and nig[0]:
+            gx = fp8_dgrad(dyq, sv1[2], sv1[3])
+        else:
+            gx = ops.gemm(dh, w1, False, False, None, None, ACT_NONE, None, None, False, 0, False, None, -1)
         return (gx.reshape(ctx.shp) if nig[0] else None, gw1, gb1, gw2, gb2, None,
                 gy if ctx.has_res else None, None)
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 (call B1, performance): staged vs unstaged GEMM epilogue — sweep, GPT-2-small step A/B,
-# PMC — and the step profile at HEAD
+# PMC — fp8 backward GEMMs (tests, A/B, GPT-2-medium step) and the step profile at HEAD
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 step() {  # step <name> <timeout> cmd...
   local n=$1 t=$2; shift 2
@@ -16,6 +16,11 @@ done
 for r in 1 2; do
   REPLICANN_FP8_WGRAD=0 step m8_bf16w_$r 300 python bench.py --model gpt2-medium-fp8 --steps 6 --warmup 3 || exit 1
   REPLICANN_FP8_WGRAD=1 step m8_fp8w_$r 300 python bench.py --model gpt2-medium-fp8 --steps 6 --warmup 3 || exit 1
+done
+step fp8_bwd_tests 300 python -u -m pytest tests/test_fp8_wgrad_gpu.py -x -v --timeout 120 --timeout-method thread || exit 1
+step fp8_bwd_ab 300 python scripts/fp8_bwd_ab.py 16384 3 || exit 1
+for r in 1 2; do
+  REPLICANN_FP8_WGRAD=1 REPLICANN_FP8_DGRAD=1 step m8_fp8wd_$r 300 python bench.py --model gpt2-medium-fp8 --steps 6 --warmup 3 || exit 1
 done
 step pmc_staged 600 bash scripts/pmc_staged.sh || exit 1
 python scripts/pmc_summary.py gpurun_out/pmc_stg/*_counter_collection.csv --match gemm_pk > gpurun_out/pmc_staged_summary.txt 2>&1

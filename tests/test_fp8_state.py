@@ -79,3 +79,24 @@ def test_fp8_wgrad_cpu_emulation_tracks_bf16_grads():
     for n in fp8_w:
         a, b = grads[True][n].float(), grads[False][n].float()
         assert ((a - b).norm() / b.norm()) < 0.1, n
+
+
+def test_fp8_dgrad_cpu_emulation_tracks_bf16_grads():
+    """fp8 data gradients (e5m2 dY x the forward's e4m3 weight, the weight read transposed) with
+    fp8 weight gradients on the CPU emulation path: the input-side gradients (embeddings, LayerNorm
+    parameters — everything upstream of an fp8 dgrad) stay within fp8 tolerance of the bf16 path, and
+    dY is quantised once per layer for both gradients (one gradient-slot roll per backward)."""
+    ids = torch.randint(0, 1000, (4, 32), generator=torch.Generator().manual_seed(1))
+    grads = {}
+    for mode in ("bf16", "fp8"):
+        m = _model()
+        for st in fp8_states(m):
+            st.wgrad = st.dgrad = mode == "fp8"
+        m(ids, ids).backward()
+        grads[mode] = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        if mode == "fp8":
+            assert all(st.g_ready for st in fp8_states(m))
+    assert set(grads["fp8"]) == set(grads["bf16"])
+    for n in grads["fp8"]:
+        a, b = grads["fp8"][n].float(), grads["bf16"][n].float()
+        assert ((a - b).norm() / b.norm().clamp_min(1e-12)) < 0.15, n
