@@ -79,7 +79,7 @@ void rn_conv_wgrad_tile(int, int, int*, int*);
 int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int, int, int, long, long, long, int, int,
                  int, int, int, int, int, int, int, int, int, long, int, int, int, float*, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
-void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+void rn_col2im(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 void rn_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
@@ -758,16 +758,29 @@ std::tuple<Tensor, Tensor> conv_fwd_implicit_stats(const Tensor& x, const Tensor
                                                    int64_t S, int64_t P) {
     return conv_fwd_implicit_impl(x, w, bias, S, P, true);
 }
-Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t P) {  // stride 1
+// out + accumulate: dx is added into `out` in the GEMM epilogue (a second gradient of the same input)
+static Tensor grad_out(const optional<Tensor>& out, bool accumulate, at::IntArrayRef shape, const Tensor& like,
+                       const char* what) {
+    if (out && out->defined()) {
+        CHECK_BF16(*out); CHECK_CONTIG(*out);
+        TORCH_CHECK(out->sizes() == shape && out->device() == like.device(), what, ": out shape");
+        return *out;
+    }
+    TORCH_CHECK(!accumulate, what, ": accumulate needs out");
+    return at::empty(shape, like.options());
+}
+Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t P, const optional<Tensor>& out,
+                           bool accumulate) {  // stride 1
     CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w); GUARD(dy);
     const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), OC = dy.size(3);
     const int KH = w.size(1), KW = w.size(2), C = w.size(3);
     TORCH_CHECK(w.size(0) == OC && OH == H + 2 * P - KH + 1 && OW == W + 2 * P - KW + 1, "conv dgrad geometry");
-    Tensor dx = at::empty({N, H, W, C}, dy.options());
+    Tensor dx = grad_out(out, accumulate, {N, H, W, C}, dy, "conv dgrad");
     const int M = N * (int)H * (int)W, K = KH * KW * OC;
     if (M == 0) return dx;
     const int rc = rn_conv_gemm(2, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, nullptr, M, C, K, 0, 0, C, OH,
-                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0, 0, nullptr, cur_stream());
+                                OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0,
+                                accumulate ? 1 : 0, nullptr, cur_stream());
     TORCH_CHECK(rc == 0, "implicit conv dgrad: unsupported geometry");
     return dx;
 }
@@ -816,11 +829,11 @@ Tensor im2col(const Tensor& x, int64_t KH, int64_t KW, int64_t S, int64_t P, int
     return cols;
 }
 Tensor col2im(const Tensor& dcols, int64_t N, int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S,
-              int64_t P, int64_t Kp) {
+              int64_t P, int64_t Kp, const optional<Tensor>& out, bool accumulate) {
     CHECK_BF16(dcols); CHECK_CONTIG(dcols); GUARD(dcols);
     const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
-    Tensor dx = at::empty({N, H, W, C}, dcols.options());
-    rn_col2im(dcols.data_ptr(), dx.data_ptr(), N, H, W, C, KH, KW, S, P, OH, OW, Kp, cur_stream());
+    Tensor dx = grad_out(out, accumulate, {N, H, W, C}, dcols, "col2im");
+    rn_col2im(dcols.data_ptr(), dx.data_ptr(), N, H, W, C, KH, KW, S, P, OH, OW, Kp, accumulate ? 1 : 0, cur_stream());
     return dx;
 }
 std::tuple<Tensor, Tensor> maxpool_fwd(const Tensor& x, int64_t K, int64_t S, int64_t P) {
@@ -1090,10 +1103,11 @@ TORCH_LIBRARY(replicann, m) {
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("conv_fwd_implicit(Tensor x, Tensor w, Tensor? bias, int S, int P) -> Tensor");
     m.def("conv_fwd_implicit_stats(Tensor x, Tensor w, Tensor? bias, int S, int P) -> (Tensor, Tensor)");
-    m.def("conv_dgrad_implicit(Tensor dy, Tensor w, int H, int W, int P) -> Tensor");
+    m.def("conv_dgrad_implicit(Tensor dy, Tensor w, int H, int W, int P, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
     m.def("conv_wgrad_implicit(Tensor dy2, Tensor x, int KH, int KW, int S, int P, Tensor(a!)? out=None, "
           "bool accumulate=False) -> Tensor");
-    m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp) -> Tensor");
+    m.def("col2im(Tensor dcols, int N, int H, int W, int C, int KH, int KW, int S, int P, int Kp, Tensor(a!)? out=None, "
+          "bool accumulate=False) -> Tensor");
     m.def("maxpool_fwd(Tensor x, int K, int S, int P) -> (Tensor, Tensor)");
     m.def("maxpool_bwd(Tensor gy, Tensor idx, int H, int W, int K, int S, int P) -> Tensor");
     m.def("avgpool_fwd(Tensor x) -> Tensor");

@@ -132,9 +132,11 @@ __global__ void __launch_bounds__(256) im2col_rows_k(const bf16* __restrict__ x,
 
 // col2im gather for C % 8 == 0: one lane per (pixel, 8-channel chunk), 16-B loads/stores, only
 // the taps whose output position exists (stride-aligned) are visited.
+// accumulate: dx += the gathered sum (the other gradient of a tensor read by two ops, e.g. ResNet's
+// shortcut, added in this pass instead of by a separate add kernel).
 __global__ void __launch_bounds__(256) col2im_vec_k(const bf16* __restrict__ dcols, bf16* __restrict__ dx, int N,
                                                     int H, int W, int C, int KH, int KW, int S, int P, int OH,
-                                                    int OW, int Kp) {
+                                                    int OW, int Kp, int accumulate) {
     const int CV = C / 8;
     const long total = (long)N * H * W * CV;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -144,6 +146,7 @@ __global__ void __launch_bounds__(256) col2im_vec_k(const bf16* __restrict__ dco
         t /= W;
         const int h = t % H, n = t / H;
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (accumulate) load8(dx + i * 8, acc);
         // first kh with (h + P - kh) % S == 0, then every S-th
         for (int kh = (h + P) % S; kh < KH; kh += S) {
             const int oh = (h + P - kh) / S;
@@ -167,7 +170,8 @@ __global__ void __launch_bounds__(256) col2im_vec_k(const bf16* __restrict__ dco
 }
 
 __global__ void __launch_bounds__(256) col2im_k(const bf16* __restrict__ dcols, bf16* __restrict__ dx, int N, int H,
-                                                int W, int C, int KH, int KW, int S, int P, int OH, int OW, int Kp) {
+                                                int W, int C, int KH, int KW, int S, int P, int OH, int OW, int Kp,
+                                                int accumulate) {
     const long total = (long)N * H * W * C;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
         const int c = i % C;
@@ -175,7 +179,7 @@ __global__ void __launch_bounds__(256) col2im_k(const bf16* __restrict__ dcols, 
         const int w = t % W;
         t /= W;
         const int h = t % H, n = t / H;
-        float acc = 0.f;
+        float acc = accumulate ? bf2f(dx[i]) : 0.f;
         for (int kh = 0; kh < KH; ++kh) {
             const int oh_s = h + P - kh;
             if (oh_s < 0 || oh_s % S) continue;
@@ -586,13 +590,14 @@ void rn_im2col(const void* x, void* cols, int N, int H, int W, int C, int KH, in
 }
 
 void rn_col2im(const void* dcols, void* dx, int N, int H, int W, int C, int KH, int KW, int S, int P, int OH, int OW,
-               int Kp, hipStream_t st) {
+               int Kp, int accumulate, hipStream_t st) {
     if (C % 8 == 0 && Kp % 8 == 0) {
         col2im_vec_k<<<gridn((long)N * H * W * C / 8), 256, 0, st>>>((const bf16*)dcols, (bf16*)dx, N, H, W, C, KH, KW,
-                                                                      S, P, OH, OW, Kp);
+                                                                      S, P, OH, OW, Kp, accumulate);
         return;
     }
-    col2im_k<<<gridn((long)N * H * W * C), 256, 0, st>>>((const bf16*)dcols, (bf16*)dx, N, H, W, C, KH, KW, S, P, OH, OW, Kp);
+    col2im_k<<<gridn((long)N * H * W * C), 256, 0, st>>>((const bf16*)dcols, (bf16*)dx, N, H, W, C, KH, KW, S, P, OH, OW,
+                                                          Kp, accumulate);
 }
 
 // idx: one byte per output element (window position of the first maximum); K*K <= 256

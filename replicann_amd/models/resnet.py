@@ -25,8 +25,8 @@ class Conv2d(nn.Module):
         nn.init.normal_(self.weight, std=math.sqrt(2.0 / (k * k * cout)))  # kaiming fan_out
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
 
-    def forward(self, x):
-        return ops.conv2d_nhwc(x, self.weight, self.bias, self.stride, self.padding)
+    def forward(self, x, join=None):
+        return ops.conv2d_nhwc(x, self.weight, self.bias, self.stride, self.padding, join=join)
 
 
 class BatchNorm(nn.Module):
@@ -38,9 +38,9 @@ class BatchNorm(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = momentum, eps
 
-    def forward(self, x, relu=False, residual=None):
+    def forward(self, x, relu=False, residual=None, join=None):
         return ops.batch_norm_nhwc(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                   self.training, self.momentum, self.eps, relu, residual)
+                                   self.training, self.momentum, self.eps, relu, residual, join=join)
 
 
 class BasicBlock(nn.Module):
@@ -54,12 +54,20 @@ class BasicBlock(nn.Module):
         if self.has_down:
             self.down_conv = Conv2d(cin, cout, 1, stride, 0)
             self.down_bn = BatchNorm(cout)
+        self.join_grads = True  # x's two gradients meet inside a kernel (ops.conv.GradJoin)
 
     def forward(self, x):
-        out = self.bn1(self.conv1(x), relu=True)
-        sc = self.down_bn(self.down_conv(x)) if self.has_down else x
-        # relu(bn2(conv2(out)) + sc) in one BatchNorm pass (its backward also returns sc's gradient)
-        return self.bn2(self.conv2(out), relu=True, residual=sc)
+        # x feeds conv1 and the shortcut: its two gradients are summed by the second producing kernel
+        # (conv1's dgrad epilogue / col2im, or the shortcut's) instead of an autograd add
+        join = (ops.GradJoin() if self.join_grads and self.training and x.is_cuda and x.requires_grad
+                and torch.is_grad_enabled() and ops.conv_implicit_ok(self.conv1)
+                and (not self.has_down or ops.conv_implicit_ok(self.down_conv)) else None)
+        out = self.bn1(self.conv1(x, join=join), relu=True)
+        if self.has_down:
+            sc = self.down_bn(self.down_conv(x, join=join))
+            # relu(bn2(conv2(out)) + sc) in one BatchNorm pass (its backward also returns sc's gradient)
+            return self.bn2(self.conv2(out), relu=True, residual=sc)
+        return self.bn2(self.conv2(out), relu=True, residual=x, join=join)
 
 
 class ResNet18(nn.Module):

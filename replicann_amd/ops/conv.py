@@ -36,6 +36,37 @@ def _fused_bn_stats():
     return os.environ.get("REPLICANN_BN_FUSED_STATS", "1") != "0"
 
 
+class GradJoin:
+    """Meeting point of two gradients of one tensor (ResNet: a block input x feeds conv1 and the
+    shortcut).  Autograd would run both producing nodes and then a separate add kernel; with a join
+    the FIRST of the two nodes to run parks its gradient here and returns None for that input, and
+    the SECOND adds its own into it inside its producing kernel (the dgrad GEMM epilogue's
+    accumulate, or the col2im gather) and returns the sum — whatever order the engine picks.
+
+    Both nodes run in any backward that needs x's gradient (each lies on a path from the loss to x).
+    One join per forward call, so gradient accumulation over micro-batches and captured step graphs
+    are unaffected."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
+
+    def settle(self, g):
+        """Result of a node that did NOT fuse the add: park it (first) or add it (second)."""
+        if g is None:
+            return None
+        other = self.take()
+        if other is None:
+            self.g = g
+            return None
+        return other.add_(g)
+
+
 def weight_param(ctx):
     w = ctx.weight
     return w if isinstance(w, torch.nn.Parameter) and w.is_contiguous() else None
@@ -50,14 +81,22 @@ def implicit_ok(C, OC, KH, KW, stride, pad):
     return C % 64 == 0 and OC % 64 == 0 and not (KH == 1 and KW == 1 and stride == 1 and pad == 0)
 
 
+def conv_implicit_ok(conv):
+    """Whether a Conv2d module (weight (OC, KH, KW, C), ``stride``, ``padding``) runs on the
+    implicit-GEMM path."""
+    OC, KH, KW, C = conv.weight.shape
+    return implicit_ok(C, OC, KH, KW, int(conv.stride), int(conv.padding))
+
+
 class _ConvImplicitFn(torch.autograd.Function):
     """conv2d whose GEMM loaders gather the filter taps straight from the NHWC activation:
     fwd (A gathered), wgrad (B gathered, split-K over pixels), dgrad (stride 1: the
     transposed conv, A = dY gathered; stride 2: dcols GEMM + col2im gather)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad):
+    def forward(ctx, x, weight, bias, stride, pad, join=None):
         ops = _ext.ops()
+        ctx.join = join
         x = x.contiguous()
         w = weight.contiguous()
         if _fused_bn_stats() and any(ctx.needs_input_grad[:2]):
@@ -92,13 +131,17 @@ class _ConvImplicitFn(torch.autograd.Function):
             else:
                 gw = ops.conv_wgrad_implicit(gy2, x, KH, KW, ctx.stride, ctx.pad).reshape(OC, KH, KW, C)
         if ctx.needs_input_grad[0]:
+            join, ctx.join = ctx.join, None
+            acc = join.take() if join is not None else None  # the other gradient of x, if it came first
             if ctx.stride == 1:
-                gx = ops.conv_dgrad_implicit(gy, w, H, W, ctx.pad)
+                gx = ops.conv_dgrad_implicit(gy, w, H, W, ctx.pad, acc, acc is not None)
             else:
                 K = KH * KW * C
                 dcols = gemm(gy2, w.reshape(OC, K), out_dtype=x.dtype)
-                gx = ops.col2im(dcols, N, H, W, C, KH, KW, ctx.stride, ctx.pad, K)
-        return gx, gw, gb, None, None
+                gx = ops.col2im(dcols, N, H, W, C, KH, KW, ctx.stride, ctx.pad, K, acc, acc is not None)
+            if join is not None and acc is None:  # first of the two: park it for the other node
+                join.g, gx = gx, None
+        return gx, gw, gb, None, None, None
 
 
 class _ConvFn(torch.autograd.Function):
@@ -143,12 +186,16 @@ class _ConvFn(torch.autograd.Function):
         return gx, gw, gb, None, None
 
 
-def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0):
-    """x (N,H,W,C), weight (OC,KH,KW,C) → (N,OH,OW,OC)."""
+def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, join=None):
+    """x (N,H,W,C), weight (OC,KH,KW,C) → (N,OH,OW,OC).
+
+    ``join``: a :class:`GradJoin` shared with the other consumer of ``x`` whose backward also
+    produces x's gradient (implicit-GEMM path; ignored elsewhere)."""
     if _ext.use_native(x):
         OC, KH, KW, C = weight.shape
         if implicit_ok(C, OC, KH, KW, int(stride), int(padding)):
-            return _ConvImplicitFn.apply(x, weight, bias, int(stride), int(padding))
+            return _ConvImplicitFn.apply(x, weight, bias, int(stride), int(padding), join)
+        assert join is None, "gradient joins need the implicit-GEMM convolution"
         return _ConvFn.apply(x, weight, bias, int(stride), int(padding))
     y = F.conv2d(x.permute(0, 3, 1, 2), weight.permute(0, 3, 1, 2), bias, stride, padding)
     return y.permute(0, 2, 3, 1)

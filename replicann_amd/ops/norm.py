@@ -113,8 +113,9 @@ def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, 
 # --------------------------------------------------------------------------
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual, join=None):
         # x: (N, H, W, C) contiguous channels-last storage
+        ctx.join = join  # GradJoin of the residual's gradient (see ops.conv.GradJoin)
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         r2 = residual.reshape(-1, C).contiguous() if residual is not None else None
@@ -147,20 +148,26 @@ class _BatchNormFn(torch.autograd.Function):
                                                     rstd, ctx.relu, ctx.has_res,
                                                     dw_acc if direct else None, db_acc if direct else None)
         gr = gres.reshape(ctx.shp) if ctx.has_res else None
+        if ctx.join is not None:
+            gr = ctx.join.settle(gr)
+            ctx.join = None
         if direct:  # the reduction added dw / db into the flat gradient views
             _notify(pw)
             _notify(pb)
-            return dx.reshape(ctx.shp), None, None, None, None, None, None, None, gr
-        return dx.reshape(ctx.shp), dw.to(weight.dtype), db.to(bias.dtype), None, None, None, None, None, gr
+            return dx.reshape(ctx.shp), None, None, None, None, None, None, None, gr, None
+        return dx.reshape(ctx.shp), dw.to(weight.dtype), db.to(bias.dtype), None, None, None, None, None, gr, None
 
 
 def batch_norm_nhwc(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5,
-                    relu=False, residual=None):
+                    relu=False, residual=None, join=None):
     """BatchNorm over (N,H,W) of an NHWC tensor; optional fused residual add and ReLU:
-    y = [relu](BN(x) [+ residual])  (ResNet's block output in one pass)."""
+    y = [relu](BN(x) [+ residual])  (ResNet's block output in one pass).  ``join``: a
+    :class:`~replicann_amd.ops.conv.GradJoin` that meets the residual's gradient with the other
+    consumer's (training, GPU)."""
     if _ext.use_native(x):
         if training:
-            return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual)
+            return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
+                                      join if residual is not None else None)
         C = x.shape[-1]
         r2 = residual.reshape(-1, C).contiguous() if residual is not None else None
         y = _ext.ops().batchnorm_eval(x.reshape(-1, C).contiguous(), weight, bias, running_mean, running_var,
