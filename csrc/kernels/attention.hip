@@ -477,8 +477,9 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
 // per query fragment against an all-ones A operand — instead of 32 v_add_f32 per tile.  Both
 // trade VALU issue slots, which bound this kernel at head_dim 64, for idle MFMA / scalar slots;
 // l then sums the bf16-rounded P that also feeds P·V.
-template <bool CAUSAL, int OCC, bool LEAN = false>
+template <bool CAUSAL, int OCC, bool LEAN = false, int QI = 2>
 __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
+    constexpr int QW = 16 * QI, QBLK = 64 * QI;  // queries per wave / per block
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -486,9 +487,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     // grid (B*H, blocks): the block index varies SLOWEST, so under causal masking every head's
     // heaviest query block is dispatched before any lighter one (longest-first over the grid)
     int bh, qb;
-    blk_map(p, (p.Tq + 127) / 128, CAUSAL, bh, qb);
+    blk_map(p, (p.Tq + QBLK - 1) / QBLK, CAUSAL, bh, qb);
     const int b = bh / p.H, h = bh % p.H;
-    const int q0 = qb * 128 + wave * 32;
+    const int q0 = qb * QBLK + wave * QW;
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
 
@@ -497,11 +498,11 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
 
     int kv_end = p.Tk;
-    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    if (CAUSAL) kv_end = min(p.Tk, qb * QBLK + QBLK + off);
     const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
     // tiles [0, nfull): every key visible to every query of the block (and Tk-complete)
     int nfull = p.Tk / 64;
-    if (CAUSAL) nfull = min(nfull, max(0, (qb * 128 + off + 1) / 64));
+    if (CAUSAL) nfull = min(nfull, max(0, (qb * QBLK + off + 1) / 64));
     nfull = min(nfull, nkv);
 #define Kt(i) (smem + (i) * 16384)
 #define Vt(i) (smem + 8192 + (i) * 16384)
@@ -509,19 +510,22 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         stage64_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
         stage64_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
-    s16x8 qf[2][2];
+    s16x8 qf[QI][2];
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi)
+    for (int qi = 0; qi < QI; ++qi)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int row = q0 + qi * 16 + c;
             qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
         }
-    asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]));
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-    f32x4 oacc[2][4];
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi)
+    for (int qi = 0; qi < QI; ++qi) asm volatile("" : "+v"(qf[qi][0]), "+v"(qf[qi][1]));
+    float m[QI], l[QI];
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) { m[qi] = -INFINITY; l[qi] = 0.f; }
+    f32x4 oacc[QI][4];
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi)
 #pragma unroll
         for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const short one = 0x3F80;  // bf16 1.0
@@ -533,10 +537,10 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         const char* kt = Kt(cur);
         const char* vt = Vt(cur);
         const int kv0 = t * 64;
-        f32x4 sacc[2][4];
+        f32x4 sacc[QI][4];
         s16x8 ka[4][2];
         [[maybe_unused]] bool moved = false;
-        [[maybe_unused]] float alph[2];
+        [[maybe_unused]] float alph[QI];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             ka[j][0] = rowfragx(kt, j, 0, fo);
@@ -545,11 +549,11 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
+            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
+            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
         // V^T fragments for the PV product, in flight during the softmax
         s16x8 va[2][4];
 #pragma unroll
@@ -558,7 +562,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
             for (int jd = 0; jd < 4; ++jd) va[s][jd] = colfragx(vt, s, jd, fo);
         if constexpr (MASKED) {
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) {
+            for (int qi = 0; qi < QI; ++qi) {
                 const int qg = q0 + qi * 16 + c;
                 const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
 #pragma unroll
@@ -569,7 +573,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
             }
         }
 #pragma unroll
-        for (int qi = 0; qi < 2; ++qi) {
+        for (int qi = 0; qi < QI; ++qi) {
             float tmax = -INFINITY;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -609,31 +613,33 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         if constexpr (LEAN) {
             if (__builtin_amdgcn_ballot_w64(moved)) {  // wave-uniform
 #pragma unroll
-                for (int qi = 0; qi < 2; ++qi) {
+                for (int qi = 0; qi < QI; ++qi) {
                     l[qi] *= alph[qi];
 #pragma unroll
                     for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alph[qi];
                 }
             }
         }
-        f32x4 lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        f32x4 lsum[QI];
+#pragma unroll
+        for (int qi = 0; qi < QI; ++qi) lsum[qi] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            s16x8 pb[2];
+            s16x8 pb[QI];
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
+            for (int qi = 0; qi < QI; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
 #pragma unroll
             for (int jd = 0; jd < 4; ++jd)
 #pragma unroll
-                for (int qi = 0; qi < 2; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
+                for (int qi = 0; qi < QI; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
             if constexpr (LEAN) {
 #pragma unroll
-                for (int qi = 0; qi < 2; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
+                for (int qi = 0; qi < QI; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
             }
         }
         if constexpr (LEAN) {
 #pragma unroll
-            for (int qi = 0; qi < 2; ++qi) l[qi] += lsum[qi][0];  // every row of P·1 holds the sum
+            for (int qi = 0; qi < QI; ++qi) l[qi] += lsum[qi][0];  // every row of P·1 holds the sum
         }
     };
     auto sync_prefetch = [&](int t) {
@@ -652,14 +658,14 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     }
     for (; t < nkv; ++t) {
         sync_prefetch(t);
-        if (CAUSAL && t * 64 > q0 + 31 + off) continue;  // wave-uniform: every query of this wave precedes the tile
+        if (CAUSAL && t * 64 > q0 + QW - 1 + off) continue;  // wave-uniform: every query of this wave precedes the tile
         tile(t, std::true_type{});
     }
 #undef Kt
 #undef Vt
     bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
+    for (int qi = 0; qi < QI; ++qi) {
         const float lt = LEAN ? l[qi] : sum4groups(l[qi]);  // LEAN: P·1 already summed over all 64 keys
         const int qg = q0 + qi * 16 + c;
         const float inv = lt > 0.f ? 1.f / lt : 0.f;
@@ -1328,6 +1334,18 @@ void attn_bwd_mfma(AttnArgs& a, hipStream_t st) {
 // the MFMA kernels' requirements: D ∈ {32, 64, 128} and 16-B aligned rows (strides in elements)
 bool mfma_head(int D) { return D == 32 || D == 64 || D == 128; }
 
+// D = 64 plain causal backward: query / key groups per wave of the dQ / dK-dV kernels (A/B knobs)
+int bwd_groups(const char* var) {
+    const char* e = std::getenv(var);
+    return (e && e[0] == '4') ? 4 : 2;
+}
+
+// D = 64 plain forward: query fragments per wave (REPLICANN_ATTN_FWD_QI=4: 64 queries per wave, A/B)
+int fwd_qi() {
+    const char* e = std::getenv("REPLICANN_ATTN_FWD_QI");  // read per launch (same-process A/B tests)
+    return (e && e[0] == '4') ? 4 : 2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1354,7 +1372,10 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         // plain causal / non-causal: the split-loop v2 kernel with the LEAN softmax bookkeeping
         // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
         if (!bias && p_drop == 0.f) {
-            if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
+            if (causal && fwd_qi() == 4) {  // 64 queries per wave: each K / V fragment read feeds 4 query fragments
+                dim3 g4(B * H * ((Tq + 255) / 256));
+                attn_fwd64v2_k<true, 2, true, 4><<<g4, 256, 32768, st>>>(a);
+            } else if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
             else attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
@@ -1400,14 +1421,20 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         // plain causal / non-causal: two 64-query groups per wave in dQ (bwd -11 % at GPT-2-small
         // shapes) and two 64-key groups per wave in dK/dV (-2.4 %, occupancy 2 at 240 VGPRs);
         // bias / dropout: one group per wave
-        if (!bias && p_drop == 0.f) {
+        if (!bias && p_drop == 0.f && causal && bwd_groups("REPLICANN_ATTN_DQ_QG") == 4) {
+            dim3 g2c(B * H * ((Tq + 255) / 256));  // 4 query groups per wave (A/B)
+            attn_bwd_dq64_k<true, false, false, 1, 4><<<g2c, 256, 32768, st>>>(a);
+        } else if (!bias && p_drop == 0.f) {
             dim3 g2b(B * H * ((Tq + 127) / 128));
             if (causal) attn_bwd_dq64_k<true, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
             else attn_bwd_dq64_k<false, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         }
-        if (!bias && p_drop == 0.f) {
+        if (!bias && p_drop == 0.f && causal && bwd_groups("REPLICANN_ATTN_DKDV_KG") == 4) {
+            dim3 g1c(B * H * ((Tk + 255) / 256));  // 4 key groups per wave, one wave per SIMD (A/B)
+            attn_bwd_dkdv64_k<true, false, false, 1, 4><<<g1c, 256, 36864, st>>>(a);
+        } else if (!bias && p_drop == 0.f) {
             dim3 g1b(B * H * ((Tk + 127) / 128));
             if (causal) attn_bwd_dkdv64_k<true, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
             else attn_bwd_dkdv64_k<false, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);

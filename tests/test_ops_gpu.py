@@ -373,16 +373,19 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("fwd,dq,dkdv", [("1", "1", "1"), ("2", "1", "1"), ("3", "1", "2"), ("3", "2", "1"), ("3", "2", "2")])
-def test_attention_kernel_variants(cuda, monkeypatch, fwd, dq, dkdv):
-    """Both D=64 forward kernels (REPLICANN_ATTN_FWD) and the backward against the fp32 reference, incl.
-    Tq != Tk (causal offset, ragged key blocks) so the masked / unmasked tile loops all run."""
-    monkeypatch.setenv("REPLICANN_ATTN_FWD", fwd)
-    monkeypatch.setenv("REPLICANN_ATTN_DQ", dq)  # dQ kernel: 1 or 2 query groups per wave
-    monkeypatch.setenv("REPLICANN_ATTN_DKDV", dkdv)  # dK/dV kernel: 1 or 2 key groups per wave
+@pytest.mark.parametrize("qi,qg,kg", [("2", "2", "2"), ("4", "2", "2"), ("2", "4", "2"), ("2", "2", "4"), ("4", "4", "4")])
+def test_attention_kernel_variants(cuda, monkeypatch, qi, qg, kg):
+    """The causal D=64 kernels with 32 / 64 queries per wave in the forward (REPLICANN_ATTN_FWD_QI) and
+    2 / 4 query (dQ) and key (dK/dV) groups per wave in the backward (REPLICANN_ATTN_DQ_QG / _DKDV_KG)
+    against the fp32 reference: full, diagonal and ragged tiles, Tq != Tk (causal offset), partial last
+    blocks; non-causal runs the default kernels."""
+    monkeypatch.setenv("REPLICANN_ATTN_FWD_QI", qi)
+    monkeypatch.setenv("REPLICANN_ATTN_DQ_QG", qg)
+    monkeypatch.setenv("REPLICANN_ATTN_DKDV_KG", kg)
     torch.manual_seed(70)
     _attn_check(2, 320, 3, 64, True)
     _attn_check(1, 100, 2, 64, True, Tk=260)
+    _attn_check(1, 1024, 2, 64, True)
     _attn_check(1, 130, 2, 64, False, Tk=70)
 
 
@@ -454,13 +457,13 @@ def test_attention_packed_grad(cuda):
     assert rel_err(o, of) < 2e-2 and rel_err(qkv.grad, qf.grad) < 4e-2
 
 
-@pytest.mark.parametrize("causal,T,dq", [(True, 256, "1"), (False, 200, "1"), (True, 320, "2"), (False, 200, "2")])
-@pytest.mark.parametrize("dkdv", ["1", "2"])
+@pytest.mark.parametrize("causal,T,dq", [(True, 256, "2"), (False, 200, "2"), (True, 320, "4"), (True, 200, "4")])
+@pytest.mark.parametrize("dkdv", ["2", "4"])
 def test_attention_packed_qkv_bias_grad(cuda, monkeypatch, causal, T, dq, dkdv):
     """Σ_rows dQKV (the c_attn bias gradient) reduced inside the attention backward kernels
-    (incl. the two-query-group dQ kernel with an odd number of 64-query blocks)."""
-    monkeypatch.setenv("REPLICANN_ATTN_DQ", dq)
-    monkeypatch.setenv("REPLICANN_ATTN_DKDV", dkdv)
+    (incl. the 2- and 4-group dQ / dK-dV kernels with a partial last block; 4 groups: causal only)."""
+    monkeypatch.setenv("REPLICANN_ATTN_DQ_QG", dq)
+    monkeypatch.setenv("REPLICANN_ATTN_DKDV_KG", dkdv)
     from replicann_amd.utils.flat import FlatParams
     torch.manual_seed(11)
     B, H, D = 3, 4, 64
