@@ -682,6 +682,241 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     }
 }
 
+// ------------------------- forward, software-pipelined (no bias / dropout) -------------------------
+// The v2 loop keeps each tile's chain S = Q·Kᵀ → row max → exp2 → P·V inside one iteration: the
+// softmax VALU waits for the QKᵀ MFMAs and the PV MFMAs wait for the VALU, so with the block's waves
+// held together by the per-tile barrier most of a wave's time is dependency stalls
+// (profiles/attention_pmc_r1d.txt: WAIT_INST_ANY ≈ 36 % of wave cycles).  Here step t issues the
+// QKᵀ MFMAs of tile t + 1 first and then runs tile t's softmax and PV: the two chains are
+// independent, so the scheduler has MFMA work to place under the exp2 / max / pack VALU.
+//   * K / V tiles stream through a 3-slot LDS ring (the step reads K of t + 1 and V of t while tile
+//     t + 2 lands): step t waits for tile t + 1 (issued one step earlier), barriers, then issues
+//     tile t + 2 into the slot of tile t − 1, which every wave finished with in step t − 1;
+//   * full tiles run pipelined (unrolled by two: the two S accumulators swap roles without copies),
+//     the diagonal / ragged tiles after them run one tile per step as in v2;
+//   * LEAN softmax bookkeeping (ballot-gated rescale, P·1 row sums on the matrix cores) as v2's
+//     variant 3; same per-element math, so O and the LSE are bitwise those of v2.
+template <bool CAUSAL, int OCC, int QI = 2, int SCHED = 0>
+__global__ void __launch_bounds__(256, OCC) attn_fwd64p_k(AttnArgs p) {
+    constexpr int QW = 16 * QI, QBLK = 64 * QI;  // queries per wave / per block
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const FragOff fo = make_fragoff(lane);
+    int bh, qb;
+    blk_map(p, (p.Tq + QBLK - 1) / QBLK, CAUSAL, bh, qb);
+    const int b = bh / p.H, h = bh % p.H;
+    const int q0 = qb * QBLK + wave * QW;
+    const int off = p.Tk - p.Tq;
+    const float sl2 = p.scale * LOG2E;
+
+    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
+    const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + h * p.k_sh);
+    const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
+
+    int kv_end = p.Tk;
+    if (CAUSAL) kv_end = min(p.Tk, qb * QBLK + QBLK + off);
+    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
+    int nfull = p.Tk / 64;
+    if (CAUSAL) nfull = min(nfull, max(0, (qb * QBLK + off + 1) / 64));
+    nfull = min(nfull, nkv);
+    // ring slot of tile t: K at [0, 8K), V at [8K, 16K) of the slot's 16 KiB
+    auto kslot = [&](int t) -> const char* { return smem + (t % 3) * 16384; };
+    auto vslot = [&](int t) -> const char* { return smem + (t % 3) * 16384 + 8192; };
+    auto stage = [&](int t) {
+        stage64_async(krs, p.k_st, t * 64, p.Tk, kslot(t), wave, lane);
+        stage64_async(vrs, p.v_st, t * 64, p.Tk, vslot(t), wave, lane);
+    };
+    if (nkv > 0) stage(0);
+    if (nkv > 1) stage(1);
+    s16x8 qf[QI][2];
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int row = q0 + qi * 16 + c;
+            qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
+        }
+    float m[QI], l[QI];
+    f32x4 oacc[QI][4];
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) {
+        m[qi] = -INFINITY;
+        l[qi] = 0.f;
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const short one = 0x3F80;  // bf16 1.0
+    const s16x8 ones = {one, one, one, one, one, one, one, one};
+
+    // S = Q·Kᵀ of tile t (lane: key kv0 + 16j + 4g + r of query q0 + 16qi + c)
+    auto qk = [&](int t, f32x4 (&sacc)[QI][4]) {
+        const char* kt = kslot(t);
+        s16x8 ka[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ka[j][0] = rowfragx(kt, j, 0, fo);
+            ka[j][1] = rowfragx(kt, j, 1, fo);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
+    };
+    // online softmax of tile t's scores + O += P·V_t (LEAN bookkeeping, see v2)
+    auto softmax_pv = [&](int t, f32x4 (&sacc)[QI][4], auto masked_c) {
+        constexpr bool MASKED = decltype(masked_c)::value;
+        const char* vt = vslot(t);
+        const int kv0 = t * 64;
+        s16x8 va[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) va[s][jd] = colfragx(vt, s, jd, fo);
+        if constexpr (MASKED) {
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) {
+                const int qg = q0 + qi * 16 + c;
+                const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (kv0 + j * 16 + 4 * g + r > lim) sacc[qi][j][r] = -INFINITY;
+            }
+        }
+        bool moved = false;
+        float alph[QI];
+#pragma unroll
+        for (int qi = 0; qi < QI; ++qi) {
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sacc[qi][j][r]);
+            tmax = max4groups(tmax);
+            const float mn = fmaxf(m[qi], tmax);
+            float alpha, nms;
+            if constexpr (MASKED) {
+                const float ms = (mn == -INFINITY) ? 0.f : mn;  // fully-masked rows stay at p = 0
+                alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m[qi] - ms) * sl2);
+                nms = -ms * sl2;
+            } else {
+                alpha = __builtin_amdgcn_exp2f((m[qi] - mn) * sl2);
+                nms = -mn * sl2;
+            }
+            moved |= (mn != m[qi]);
+            alph[qi] = alpha;
+            m[qi] = mn;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sacc[qi][j][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[qi][j][r], sl2, nms));
+        }
+        if constexpr (SCHED == 1 && !MASKED) {
+            // keep the exp2 results here (LLVM otherwise sinks them past the rescale branch below)
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(sacc[qi][j]));
+            // one scheduling region from the next tile's K reads to here: K fragment reads first,
+            // then each of the next tile's 8·QI QKᵀ MFMAs followed by a slice of this tile's softmax
+            // VALU (the V^T reads ride in between), so the MFMAs run under the exp2 / max work
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+            for (int i = 0; i < 8 * QI; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+                if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(moved)) {  // wave-uniform
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) {
+                l[qi] *= alph[qi];
+#pragma unroll
+                for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alph[qi];
+            }
+        }
+        f32x4 lsum[QI];
+#pragma unroll
+        for (int qi = 0; qi < QI; ++qi) lsum[qi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            s16x8 pb[QI];
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd)
+#pragma unroll
+                for (int qi = 0; qi < QI; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
+#pragma unroll
+            for (int qi = 0; qi < QI; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
+        }
+#pragma unroll
+        for (int qi = 0; qi < QI; ++qi) l[qi] += lsum[qi][0];
+    };
+    // step head: tiles <= t + 1 landed (every wave's DMA: wait + barrier), slot of t - 1 refilled
+    auto head = [&](int t) {
+        vm_wait_all();
+        __syncthreads();
+        if (t + 2 < nkv) stage(t + 2);
+    };
+    using F = std::false_type;
+    vm_wait_all();
+    __syncthreads();
+    f32x4 sA[QI][4], sB[QI][4];
+    if (nfull > 0) qk(0, sA);
+    int t = 0;
+    for (; t + 2 < nfull; t += 2) {  // S of t + 1 and t + 2 (both full) under the softmax of t, t + 1
+        head(t);
+        qk(t + 1, sB);
+        softmax_pv(t, sA, F{});
+        head(t + 1);
+        qk(t + 2, sA);
+        softmax_pv(t + 1, sB, F{});
+    }
+    if (t + 1 < nfull) {
+        head(t);
+        qk(t + 1, sB);
+        softmax_pv(t, sA, F{});
+        head(t + 1);
+        softmax_pv(t + 1, sB, F{});
+        t += 2;
+    } else if (t < nfull) {
+        head(t);
+        softmax_pv(t, sA, F{});
+        t += 1;
+    }
+    for (; t < nkv; ++t) {  // diagonal / ragged tiles, one per step
+        head(t);
+        if (CAUSAL && t * 64 > q0 + QW - 1 + off) continue;  // wave-uniform: the whole tile is masked
+        qk(t, sA);
+        softmax_pv(t, sA, std::true_type{});
+    }
+    bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) {
+        const float lt = l[qi];  // P·1 already summed over the 64 keys of every tile
+        const int qg = q0 + qi * 16 + c;
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        if (qg < p.Tq) {
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) {
+                bf16x4 o4 = {(bf16)(oacc[qi][jd][0] * inv), (bf16)(oacc[qi][jd][1] * inv),
+                             (bf16)(oacc[qi][jd][2] * inv), (bf16)(oacc[qi][jd][3] * inv)};
+                *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
+            }
+            if (g == 0)
+                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * sl2 + log2f(lt)) : INFINITY;  // base 2
+        }
+    }
+}
+
 // ============================== backward, D = 64 ==============================
 // delta[b,h,q] = sum_d dO * O  — one thread per (b, q, h) row of D = 64 (8 x 16-B loads each)
 __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
@@ -1340,6 +1575,12 @@ int bwd_groups(const char* var) {
     return (e && e[0] == '4') ? 4 : 2;
 }
 
+// D = 64 plain forward: software-pipelined kernel (REPLICANN_ATTN_FWD_PIPE=1, A/B)
+int fwd_pipe() {
+    const char* e = std::getenv("REPLICANN_ATTN_FWD_PIPE");
+    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+}
+
 // D = 64 plain forward: query fragments per wave (REPLICANN_ATTN_FWD_QI=4: 64 queries per wave, A/B)
 int fwd_qi() {
     const char* e = std::getenv("REPLICANN_ATTN_FWD_QI");  // read per launch (same-process A/B tests)
@@ -1372,7 +1613,13 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         // plain causal / non-causal: the split-loop v2 kernel with the LEAN softmax bookkeeping
         // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
         if (!bias && p_drop == 0.f) {
-            if (causal && fwd_qi() == 4) {  // 64 queries per wave: each K / V fragment read feeds 4 query fragments
+            if (fwd_pipe() == 2) {  // + sched-group interleave of those MFMAs with the softmax VALU
+                if (causal) attn_fwd64p_k<true, 2, 2, 1><<<grid, 256, 49152, st>>>(a);
+                else attn_fwd64p_k<false, 2, 2, 1><<<grid, 256, 49152, st>>>(a);
+            } else if (fwd_pipe() == 1) {  // software-pipelined QKᵀ of the next tile under this tile's softmax (A/B)
+                if (causal) attn_fwd64p_k<true, 2><<<grid, 256, 49152, st>>>(a);
+                else attn_fwd64p_k<false, 2><<<grid, 256, 49152, st>>>(a);
+            } else if (causal && fwd_qi() == 4) {  // 64 queries per wave: each K / V fragment read feeds 4 query fragments
                 dim3 g4(B * H * ((Tq + 255) / 256));
                 attn_fwd64v2_k<true, 2, true, 4><<<g4, 256, 32768, st>>>(a);
             } else if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);

@@ -373,8 +373,10 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("qi,qg,kg", [("2", "2", "2"), ("4", "2", "2"), ("2", "4", "2"), ("2", "2", "4"), ("4", "4", "4")])
-def test_attention_kernel_variants(cuda, monkeypatch, qi, qg, kg):
+@pytest.mark.parametrize("qi,qg,kg,pipe", [("2", "2", "2", "0"), ("4", "2", "2", "0"), ("2", "4", "2", "0"),
+                                            ("2", "2", "4", "0"), ("4", "4", "4", "0"), ("2", "2", "2", "1"),
+                                            ("2", "2", "2", "2")])
+def test_attention_kernel_variants(cuda, monkeypatch, qi, qg, kg, pipe):
     """The causal D=64 kernels with 32 / 64 queries per wave in the forward (REPLICANN_ATTN_FWD_QI) and
     2 / 4 query (dQ) and key (dK/dV) groups per wave in the backward (REPLICANN_ATTN_DQ_QG / _DKDV_KG)
     against the fp32 reference: full, diagonal and ragged tiles, Tq != Tk (causal offset), partial last
@@ -382,6 +384,7 @@ def test_attention_kernel_variants(cuda, monkeypatch, qi, qg, kg):
     monkeypatch.setenv("REPLICANN_ATTN_FWD_QI", qi)
     monkeypatch.setenv("REPLICANN_ATTN_DQ_QG", qg)
     monkeypatch.setenv("REPLICANN_ATTN_DKDV_KG", kg)
+    monkeypatch.setenv("REPLICANN_ATTN_FWD_PIPE", pipe)  # software-pipelined forward (1; 2: + sched groups)
     torch.manual_seed(70)
     _attn_check(2, 320, 3, 64, True)
     _attn_check(1, 100, 2, 64, True, Tk=260)
