@@ -1160,6 +1160,219 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
     }
 }
 
+// dK, dV, software-pipelined (no bias / dropout, D = 64; the forward's attn_fwd64p_k scheme): step t
+// issues the S = Q·Kᵀ and dP = dO·Vᵀ MFMAs of query tile t + 1 before tile t's P / dS VALU and its
+// dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS MFMAs, so the exp2 / multiply work of one tile has the next tile's
+// MFMAs beside it instead of waiting on its own.  Q / dO / lse / delta tiles stream through a 3-slot
+// ring (step t reads slots t and t + 1 while t + 2 lands); the diagonal head and the ragged tail run
+// one tile per step as in attn_bwd_dkdv64_k.  Same per-element math and summation order: dK / dV are
+// bitwise those of attn_bwd_dkdv64_k<…, KG>.
+template <bool CAUSAL, int OCC, int KG>
+__global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64p_k(AttnArgs p) {
+    constexpr int D = 64, NS = kNS<D>, NJ = kNJ<D>, TB = kTB<D>, SLOT = 2 * TB + 2048;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const FragOffT<D> fo = make_fragoff<D>(lane);
+    constexpr int KB = 64 * KG;
+    int bh, kb;
+    blk_map(p, (p.Tk + KB - 1) / KB, false, bh, kb);
+    const int b = bh / p.H, h = bh % p.H;
+    const int kvw = kb * KB + wave * 16;
+    int kvl[KG];
+#pragma unroll
+    for (int u = 0; u < KG; ++u) kvl[u] = kvw + 64 * u + c;
+    const int off = p.Tk - p.Tq;
+    const float sl2 = p.scale * LOG2E;
+    const u32x4 qrs = make_rsrc_sgpr(p.q + b * p.q_sb + h * p.q_sh);
+    const u32x4 ors = make_rsrc_sgpr(p.dout + b * p.do_sb + h * p.do_sh);
+    const u32x4 lrs = make_rsrc_sgpr(p.lse + ((long)b * p.H + h) * p.Tq, (uint32_t)p.Tq * 4);
+    const u32x4 drs = make_rsrc_sgpr(p.delta + ((long)b * p.H + h) * p.Tq, (uint32_t)p.Tq * 4);
+    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
+    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
+    int qt0 = 0;
+    if (CAUSAL) qt0 = max(0, (kb * KB - off)) / 64;
+    const int nqt = (p.Tq + 63) / 64;
+    // slot of query tile t: Q [0, TB), dO [TB, 2TB), lse [2TB, 2TB + 1K), delta [2TB + 1K, 2TB + 2K)
+    auto slot = [&](int t) -> char* { return smem + ((t - qt0) % 3) * SLOT; };
+    auto stage = [&](int qt) {
+        char* sl = slot(qt);
+        stage64_async<D>(qrs, p.q_st, qt * 64, p.Tq, sl, wave, lane);
+        stage64_async<D>(ors, p.do_st, qt * 64, p.Tq, sl + TB, wave, lane);
+        if (wave < 2) {
+            const int r = qt * 64 + lane * 4;
+            const uint32_t voff = (lane < 16 && r < p.Tq) ? (uint32_t)(r * 4) : 0xFFFFFFF0u;
+            dma16_async(wave == 0 ? lrs : drs, voff, lds_addr(sl + 2 * TB + (wave == 0 ? 0 : 1024)));
+        }
+    };
+    if (qt0 < nqt) stage(qt0);
+    if (qt0 + 1 < nqt) stage(qt0 + 1);
+
+    s16x8 kf[KG][NS], vf[KG][NS];
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            kf[u][s] = gload16(kbase + (long)kvl[u] * p.k_st + s * 32 + g * 8, kvl[u] < p.Tk);
+            vf[u][s] = gload16(vbase + (long)kvl[u] * p.v_st + s * 32 + g * 8, kvl[u] < p.Tk);
+        }
+    }
+    f32x4 dvacc[KG][NJ], dkacc[KG][NJ];
+#pragma unroll
+    for (int u = 0; u < KG; ++u)
+#pragma unroll
+        for (int jd = 0; jd < NJ; ++jd) { dvacc[u][jd] = (f32x4){0, 0, 0, 0}; dkacc[u][jd] = (f32x4){0, 0, 0, 0}; }
+    auto masked_tile = [&](int qt) {
+        return (qt * 64 + 64 > p.Tq) || (kb * KB + KB > p.Tk) || (CAUSAL && kb * KB + KB - 1 > qt * 64 + off);
+    };
+    // raw S and dP of query tile qt (lane: query 64qt + 16qi + 4g + r, key kvl[u])
+    auto sdp = [&](int qt, f32x4 (&sa)[KG][4], f32x4 (&da)[KG][4]) {
+        const char* qt_ = slot(qt);
+        const char* ot_ = qt_ + TB;
+#pragma unroll
+        for (int qi = 0; qi < 4; ++qi) {
+            s16x8 af[NS], of[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                af[s] = rowfragx(qt_, qi, s, fo);
+                of[s] = rowfragx(ot_, qi, s, fo);
+            }
+#pragma unroll
+            for (int u = 0; u < KG; ++u) {
+                f32x4 x = {0, 0, 0, 0}, y = {0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < NS; ++s) x = MFMA(af[s], kf[u][s], x, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) y = MFMA(of[s], vf[u][s], y, 0, 0, 0);
+                sa[u][qi] = x;
+                da[u][qi] = y;
+            }
+        }
+    };
+    // P and dS of tile qt in place of its S / dP, then dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS
+    auto grad = [&](int qt, f32x4 (&sa)[KG][4], f32x4 (&da)[KG][4], auto masked_c) {
+        constexpr bool MASKED = decltype(masked_c)::value;
+        const char* qt_ = slot(qt);
+        const char* ot_ = qt_ + TB;
+        const float* lt_ = reinterpret_cast<const float*>(qt_ + 2 * TB);
+        const float* dt_ = reinterpret_cast<const float*>(qt_ + 2 * TB + 1024);
+        const int q0 = qt * 64;
+#pragma unroll
+        for (int qi = 0; qi < 4; ++qi) {
+            const int ql = qi * 16 + 4 * g;
+            const float4 l4 = *reinterpret_cast<const float4*>(lt_ + ql);
+            const float4 d4 = *reinterpret_cast<const float4*>(dt_ + ql);
+            const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int u = 0; u < KG; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(sa[u][qi][r] * sl2 - ls[r]);
+                    float pd = pv, dsv = pv * (da[u][qi][r] - dl[r]);
+                    if constexpr (MASKED) {
+                        const int qg = q0 + ql + r;
+                        if (kvl[u] >= p.Tk || qg >= p.Tq || (CAUSAL && kvl[u] > qg + off)) pd = dsv = 0.f;
+                    }
+                    sa[u][qi][r] = pd;
+                    da[u][qi][r] = dsv;
+                }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            s16x8 pb[KG], sb[KG];
+#pragma unroll
+            for (int u = 0; u < KG; ++u) {
+                pb[u] = pack_p(sa[u][2 * ks], sa[u][2 * ks + 1]);
+                sb[u] = pack_p(da[u][2 * ks], da[u][2 * ks + 1]);
+            }
+#pragma unroll
+            for (int jd = 0; jd < NJ; ++jd) {
+                const s16x8 ao = colfragx(ot_, ks, jd, fo);
+#pragma unroll
+                for (int u = 0; u < KG; ++u) dvacc[u][jd] = MFMA(ao, pb[u], dvacc[u][jd], 0, 0, 0);
+                const s16x8 aq = colfragx(qt_, ks, jd, fo);
+#pragma unroll
+                for (int u = 0; u < KG; ++u) dkacc[u][jd] = MFMA(aq, sb[u], dkacc[u][jd], 0, 0, 0);
+            }
+        }
+    };
+    auto head = [&](int t) {  // tiles <= t + 1 landed for every wave; slot of t - 1 refilled with t + 2
+        vm_wait_all();
+        __syncthreads();
+        if (t + 2 < nqt) stage(t + 2);
+    };
+    using F = std::false_type;
+    using T = std::true_type;
+    vm_wait_all();
+    __syncthreads();
+    f32x4 sA[KG][4], dA[KG][4], sB[KG][4], dB[KG][4];
+    int qm = qt0;
+    while (qm < nqt && masked_tile(qm)) ++qm;  // [qt0, qm): diagonal head
+    int qe = qm;
+    while (qe < nqt && !masked_tile(qe)) ++qe;  // [qm, qe): unmasked; [qe, nqt): ragged tail
+    int t = qt0;
+    for (; t < qm; ++t) {
+        head(t);
+        if (CAUSAL && t * 64 + 63 + off < kvw) continue;  // wave-uniform: every query precedes this wave's keys
+        sdp(t, sA, dA);
+        grad(t, sA, dA, T{});
+    }
+    if (t < qe) sdp(t, sA, dA);
+    for (; t + 2 < qe; t += 2) {
+        head(t);
+        sdp(t + 1, sB, dB);
+        grad(t, sA, dA, F{});
+        head(t + 1);
+        sdp(t + 2, sA, dA);
+        grad(t + 1, sB, dB, F{});
+    }
+    if (t + 1 < qe) {
+        head(t);
+        sdp(t + 1, sB, dB);
+        grad(t, sA, dA, F{});
+        head(t + 1);
+        grad(t + 1, sB, dB, F{});
+        t += 2;
+    } else if (t < qe) {
+        head(t);
+        grad(t, sA, dA, F{});
+        t += 1;
+    }
+    for (; t < nqt; ++t) {
+        head(t);
+        sdp(t, sA, dA);
+        grad(t, sA, dA, T{});
+    }
+    if (p.bsum) {
+        const int E = p.H * D, nb64 = (p.Tk + 63) / 64;
+#pragma unroll
+        for (int u = 0; u < KG; ++u) {
+            const int blk = kb * KG + u;
+            if (blk < nb64) {
+                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * D;
+                block_colsum64<D>(dkacc[u], p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
+                block_colsum64<D>(dvacc[u], 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+        if (kvl[u] < p.Tk) {
+            bf16* dkp = p.dk + b * p.dk_sb + (long)kvl[u] * p.dk_st + h * p.dk_sh;
+            bf16* dvp = p.dv + b * p.dv_sb + (long)kvl[u] * p.dv_st + h * p.dv_sh;
+#pragma unroll
+            for (int jd = 0; jd < NJ; ++jd) {
+                bf16x4 k4 = {(bf16)(dkacc[u][jd][0] * p.scale), (bf16)(dkacc[u][jd][1] * p.scale),
+                             (bf16)(dkacc[u][jd][2] * p.scale), (bf16)(dkacc[u][jd][3] * p.scale)};
+                bf16x4 v4 = {(bf16)dvacc[u][jd][0], (bf16)dvacc[u][jd][1], (bf16)dvacc[u][jd][2],
+                             (bf16)dvacc[u][jd][3]};
+                *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
+                *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
+            }
+        }
+    }
+}
+
 // dQ: grid (B*H, ceil(Tq/(64·QG))); query group qg (< QG) of wave w owns queries
 // qb·64·QG + 64·qg + 16w + (lane&15).  With QG = 2 every K / V fragment read from LDS feeds
 // the MFMAs of two query groups (half the LDS reads per MFMA) and each wave carries two
@@ -1575,6 +1788,13 @@ int bwd_groups(const char* var) {
     return (e && e[0] == '4') ? 4 : 2;
 }
 
+// D = 64 plain dK/dV: software-pipelined kernel (REPLICANN_ATTN_DKDV_PIPE=1: one key group per wave,
+// occupancy 2; 2: two key groups, occupancy 1; A/B)
+int bwd_dkdv_pipe() {
+    const char* e = std::getenv("REPLICANN_ATTN_DKDV_PIPE");
+    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+}
+
 // D = 64 plain forward: software-pipelined kernel (REPLICANN_ATTN_FWD_PIPE=1, A/B)
 int fwd_pipe() {
     const char* e = std::getenv("REPLICANN_ATTN_FWD_PIPE");
@@ -1678,7 +1898,17 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         } else {
             RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         }
-        if (!bias && p_drop == 0.f && causal && bwd_groups("REPLICANN_ATTN_DKDV_KG") == 4) {
+        if (!bias && p_drop == 0.f && bwd_dkdv_pipe()) {  // software-pipelined dK/dV (A/B)
+            if (bwd_dkdv_pipe() == 2) {  // 2 key groups per wave, one wave per SIMD
+                dim3 g1b(B * H * ((Tk + 127) / 128));
+                if (causal) attn_bwd_dkdv64p_k<true, 1, 2><<<g1b, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
+                else attn_bwd_dkdv64p_k<false, 1, 2><<<g1b, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
+            } else {
+                dim3 g1a(B * H * ((Tk + 63) / 64));
+                if (causal) attn_bwd_dkdv64p_k<true, 2, 1><<<g1a, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
+                else attn_bwd_dkdv64p_k<false, 2, 1><<<g1a, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
+            }
+        } else if (!bias && p_drop == 0.f && causal && bwd_groups("REPLICANN_ATTN_DKDV_KG") == 4) {
             dim3 g1c(B * H * ((Tk + 255) / 256));  // 4 key groups per wave, one wave per SIMD (A/B)
             attn_bwd_dkdv64_k<true, false, false, 1, 4><<<g1c, 256, 36864, st>>>(a);
         } else if (!bias && p_drop == 0.f) {
