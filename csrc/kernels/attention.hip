@@ -682,241 +682,6 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
     }
 }
 
-// ------------------------- forward, software-pipelined (no bias / dropout) -------------------------
-// The v2 loop keeps each tile's chain S = Q·Kᵀ → row max → exp2 → P·V inside one iteration: the
-// softmax VALU waits for the QKᵀ MFMAs and the PV MFMAs wait for the VALU, so with the block's waves
-// held together by the per-tile barrier most of a wave's time is dependency stalls
-// (profiles/attention_pmc_r1d.txt: WAIT_INST_ANY ≈ 36 % of wave cycles).  Here step t issues the
-// QKᵀ MFMAs of tile t + 1 first and then runs tile t's softmax and PV: the two chains are
-// independent, so the scheduler has MFMA work to place under the exp2 / max / pack VALU.
-//   * K / V tiles stream through a 3-slot LDS ring (the step reads K of t + 1 and V of t while tile
-//     t + 2 lands): step t waits for tile t + 1 (issued one step earlier), barriers, then issues
-//     tile t + 2 into the slot of tile t − 1, which every wave finished with in step t − 1;
-//   * full tiles run pipelined (unrolled by two: the two S accumulators swap roles without copies),
-//     the diagonal / ragged tiles after them run one tile per step as in v2;
-//   * LEAN softmax bookkeeping (ballot-gated rescale, P·1 row sums on the matrix cores) as v2's
-//     variant 3; same per-element math, so O and the LSE are bitwise those of v2.
-template <bool CAUSAL, int OCC, int QI = 2, int SCHED = 0>
-__global__ void __launch_bounds__(256, OCC) attn_fwd64p_k(AttnArgs p) {
-    constexpr int QW = 16 * QI, QBLK = 64 * QI;  // queries per wave / per block
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const FragOff fo = make_fragoff(lane);
-    int bh, qb;
-    blk_map(p, (p.Tq + QBLK - 1) / QBLK, CAUSAL, bh, qb);
-    const int b = bh / p.H, h = bh % p.H;
-    const int q0 = qb * QBLK + wave * QW;
-    const int off = p.Tk - p.Tq;
-    const float sl2 = p.scale * LOG2E;
-
-    const bf16* qbase = p.q + b * p.q_sb + h * p.q_sh;
-    const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + h * p.k_sh);
-    const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + h * p.v_sh);
-
-    int kv_end = p.Tk;
-    if (CAUSAL) kv_end = min(p.Tk, qb * QBLK + QBLK + off);
-    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
-    int nfull = p.Tk / 64;
-    if (CAUSAL) nfull = min(nfull, max(0, (qb * QBLK + off + 1) / 64));
-    nfull = min(nfull, nkv);
-    // ring slot of tile t: K at [0, 8K), V at [8K, 16K) of the slot's 16 KiB
-    auto kslot = [&](int t) -> const char* { return smem + (t % 3) * 16384; };
-    auto vslot = [&](int t) -> const char* { return smem + (t % 3) * 16384 + 8192; };
-    auto stage = [&](int t) {
-        stage64_async(krs, p.k_st, t * 64, p.Tk, kslot(t), wave, lane);
-        stage64_async(vrs, p.v_st, t * 64, p.Tk, vslot(t), wave, lane);
-    };
-    if (nkv > 0) stage(0);
-    if (nkv > 1) stage(1);
-    s16x8 qf[QI][2];
-#pragma unroll
-    for (int qi = 0; qi < QI; ++qi)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int row = q0 + qi * 16 + c;
-            qf[qi][s] = gload16(qbase + (long)row * p.q_st + s * 32 + g * 8, row < p.Tq);
-        }
-    float m[QI], l[QI];
-    f32x4 oacc[QI][4];
-#pragma unroll
-    for (int qi = 0; qi < QI; ++qi) {
-        m[qi] = -INFINITY;
-        l[qi] = 0.f;
-#pragma unroll
-        for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    const short one = 0x3F80;  // bf16 1.0
-    const s16x8 ones = {one, one, one, one, one, one, one, one};
-
-    // S = Q·Kᵀ of tile t (lane: key kv0 + 16j + 4g + r of query q0 + 16qi + c)
-    auto qk = [&](int t, f32x4 (&sacc)[QI][4]) {
-        const char* kt = kslot(t);
-        s16x8 ka[4][2];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            ka[j][0] = rowfragx(kt, j, 0, fo);
-            ka[j][1] = rowfragx(kt, j, 1, fo);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
-    };
-    // online softmax of tile t's scores + O += P·V_t (LEAN bookkeeping, see v2)
-    auto softmax_pv = [&](int t, f32x4 (&sacc)[QI][4], auto masked_c) {
-        constexpr bool MASKED = decltype(masked_c)::value;
-        const char* vt = vslot(t);
-        const int kv0 = t * 64;
-        s16x8 va[2][4];
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int jd = 0; jd < 4; ++jd) va[s][jd] = colfragx(vt, s, jd, fo);
-        if constexpr (MASKED) {
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi) {
-                const int qg = q0 + qi * 16 + c;
-                const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (kv0 + j * 16 + 4 * g + r > lim) sacc[qi][j][r] = -INFINITY;
-            }
-        }
-        bool moved = false;
-        float alph[QI];
-#pragma unroll
-        for (int qi = 0; qi < QI; ++qi) {
-            float tmax = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sacc[qi][j][r]);
-            tmax = max4groups(tmax);
-            const float mn = fmaxf(m[qi], tmax);
-            float alpha, nms;
-            if constexpr (MASKED) {
-                const float ms = (mn == -INFINITY) ? 0.f : mn;  // fully-masked rows stay at p = 0
-                alpha = (m[qi] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m[qi] - ms) * sl2);
-                nms = -ms * sl2;
-            } else {
-                alpha = __builtin_amdgcn_exp2f((m[qi] - mn) * sl2);
-                nms = -mn * sl2;
-            }
-            moved |= (mn != m[qi]);
-            alph[qi] = alpha;
-            m[qi] = mn;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) sacc[qi][j][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[qi][j][r], sl2, nms));
-        }
-        if constexpr (SCHED == 1 && !MASKED) {
-            // keep the exp2 results here (LLVM otherwise sinks them past the rescale branch below)
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(sacc[qi][j]));
-            // one scheduling region from the next tile's K reads to here: K fragment reads first,
-            // then each of the next tile's 8·QI QKᵀ MFMAs followed by a slice of this tile's softmax
-            // VALU (the V^T reads ride in between), so the MFMAs run under the exp2 / max work
-            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-            for (int i = 0; i < 8 * QI; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-                if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-            }
-        }
-        if (__builtin_amdgcn_ballot_w64(moved)) {  // wave-uniform
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi) {
-                l[qi] *= alph[qi];
-#pragma unroll
-                for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] *= alph[qi];
-            }
-        }
-        f32x4 lsum[QI];
-#pragma unroll
-        for (int qi = 0; qi < QI; ++qi) lsum[qi] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            s16x8 pb[QI];
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
-#pragma unroll
-            for (int jd = 0; jd < 4; ++jd)
-#pragma unroll
-                for (int qi = 0; qi < QI; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
-#pragma unroll
-            for (int qi = 0; qi < QI; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
-        }
-#pragma unroll
-        for (int qi = 0; qi < QI; ++qi) l[qi] += lsum[qi][0];
-    };
-    // step head: tiles <= t + 1 landed (every wave's DMA: wait + barrier), slot of t - 1 refilled
-    auto head = [&](int t) {
-        vm_wait_all();
-        __syncthreads();
-        if (t + 2 < nkv) stage(t + 2);
-    };
-    using F = std::false_type;
-    vm_wait_all();
-    __syncthreads();
-    f32x4 sA[QI][4], sB[QI][4];
-    if (nfull > 0) qk(0, sA);
-    int t = 0;
-    for (; t + 2 < nfull; t += 2) {  // S of t + 1 and t + 2 (both full) under the softmax of t, t + 1
-        head(t);
-        qk(t + 1, sB);
-        softmax_pv(t, sA, F{});
-        head(t + 1);
-        qk(t + 2, sA);
-        softmax_pv(t + 1, sB, F{});
-    }
-    if (t + 1 < nfull) {
-        head(t);
-        qk(t + 1, sB);
-        softmax_pv(t, sA, F{});
-        head(t + 1);
-        softmax_pv(t + 1, sB, F{});
-        t += 2;
-    } else if (t < nfull) {
-        head(t);
-        softmax_pv(t, sA, F{});
-        t += 1;
-    }
-    for (; t < nkv; ++t) {  // diagonal / ragged tiles, one per step
-        head(t);
-        if (CAUSAL && t * 64 > q0 + QW - 1 + off) continue;  // wave-uniform: the whole tile is masked
-        qk(t, sA);
-        softmax_pv(t, sA, std::true_type{});
-    }
-    bf16* obase = p.o + b * p.o_sb + h * p.o_sh;
-#pragma unroll
-    for (int qi = 0; qi < QI; ++qi) {
-        const float lt = l[qi];  // P·1 already summed over the 64 keys of every tile
-        const int qg = q0 + qi * 16 + c;
-        const float inv = lt > 0.f ? 1.f / lt : 0.f;
-        if (qg < p.Tq) {
-#pragma unroll
-            for (int jd = 0; jd < 4; ++jd) {
-                bf16x4 o4 = {(bf16)(oacc[qi][jd][0] * inv), (bf16)(oacc[qi][jd][1] * inv),
-                             (bf16)(oacc[qi][jd][2] * inv), (bf16)(oacc[qi][jd][3] * inv)};
-                *reinterpret_cast<bf16x4*>(obase + (long)qg * p.o_st + jd * 16 + 4 * g) = o4;
-            }
-            if (g == 0)
-                p.lse[((long)b * p.H + h) * p.Tq + qg] = (lt > 0.f) ? (m[qi] * sl2 + log2f(lt)) : INFINITY;  // base 2
-        }
-    }
-}
-
 // ============================== backward, D = 64 ==============================
 // delta[b,h,q] = sum_d dO * O  — one thread per (b, q, h) row of D = 64 (8 x 16-B loads each)
 __global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
@@ -1136,219 +901,6 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
         for (int u = 0; u < KG; ++u) {
             const int blk = kb * KG + u;
             if (blk < nb64) {  // block-uniform
-                float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * D;
-                block_colsum64<D>(dkacc[u], p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
-                block_colsum64<D>(dvacc[u], 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
-            }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < KG; ++u) {
-        if (kvl[u] < p.Tk) {
-            bf16* dkp = p.dk + b * p.dk_sb + (long)kvl[u] * p.dk_st + h * p.dk_sh;
-            bf16* dvp = p.dv + b * p.dv_sb + (long)kvl[u] * p.dv_st + h * p.dv_sh;
-#pragma unroll
-            for (int jd = 0; jd < NJ; ++jd) {
-                bf16x4 k4 = {(bf16)(dkacc[u][jd][0] * p.scale), (bf16)(dkacc[u][jd][1] * p.scale),
-                             (bf16)(dkacc[u][jd][2] * p.scale), (bf16)(dkacc[u][jd][3] * p.scale)};
-                bf16x4 v4 = {(bf16)dvacc[u][jd][0], (bf16)dvacc[u][jd][1], (bf16)dvacc[u][jd][2],
-                             (bf16)dvacc[u][jd][3]};
-                *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
-                *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
-            }
-        }
-    }
-}
-
-// dK, dV, software-pipelined (no bias / dropout, D = 64; the forward's attn_fwd64p_k scheme): step t
-// issues the S = Q·Kᵀ and dP = dO·Vᵀ MFMAs of query tile t + 1 before tile t's P / dS VALU and its
-// dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS MFMAs, so the exp2 / multiply work of one tile has the next tile's
-// MFMAs beside it instead of waiting on its own.  Q / dO / lse / delta tiles stream through a 3-slot
-// ring (step t reads slots t and t + 1 while t + 2 lands); the diagonal head and the ragged tail run
-// one tile per step as in attn_bwd_dkdv64_k.  Same per-element math and summation order: dK / dV are
-// bitwise those of attn_bwd_dkdv64_k<…, KG>.
-template <bool CAUSAL, int OCC, int KG>
-__global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv64p_k(AttnArgs p) {
-    constexpr int D = 64, NS = kNS<D>, NJ = kNJ<D>, TB = kTB<D>, SLOT = 2 * TB + 2048;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const FragOffT<D> fo = make_fragoff<D>(lane);
-    constexpr int KB = 64 * KG;
-    int bh, kb;
-    blk_map(p, (p.Tk + KB - 1) / KB, false, bh, kb);
-    const int b = bh / p.H, h = bh % p.H;
-    const int kvw = kb * KB + wave * 16;
-    int kvl[KG];
-#pragma unroll
-    for (int u = 0; u < KG; ++u) kvl[u] = kvw + 64 * u + c;
-    const int off = p.Tk - p.Tq;
-    const float sl2 = p.scale * LOG2E;
-    const u32x4 qrs = make_rsrc_sgpr(p.q + b * p.q_sb + h * p.q_sh);
-    const u32x4 ors = make_rsrc_sgpr(p.dout + b * p.do_sb + h * p.do_sh);
-    const u32x4 lrs = make_rsrc_sgpr(p.lse + ((long)b * p.H + h) * p.Tq, (uint32_t)p.Tq * 4);
-    const u32x4 drs = make_rsrc_sgpr(p.delta + ((long)b * p.H + h) * p.Tq, (uint32_t)p.Tq * 4);
-    const bf16* kbase = p.k + b * p.k_sb + h * p.k_sh;
-    const bf16* vbase = p.v + b * p.v_sb + h * p.v_sh;
-    int qt0 = 0;
-    if (CAUSAL) qt0 = max(0, (kb * KB - off)) / 64;
-    const int nqt = (p.Tq + 63) / 64;
-    // slot of query tile t: Q [0, TB), dO [TB, 2TB), lse [2TB, 2TB + 1K), delta [2TB + 1K, 2TB + 2K)
-    auto slot = [&](int t) -> char* { return smem + ((t - qt0) % 3) * SLOT; };
-    auto stage = [&](int qt) {
-        char* sl = slot(qt);
-        stage64_async<D>(qrs, p.q_st, qt * 64, p.Tq, sl, wave, lane);
-        stage64_async<D>(ors, p.do_st, qt * 64, p.Tq, sl + TB, wave, lane);
-        if (wave < 2) {
-            const int r = qt * 64 + lane * 4;
-            const uint32_t voff = (lane < 16 && r < p.Tq) ? (uint32_t)(r * 4) : 0xFFFFFFF0u;
-            dma16_async(wave == 0 ? lrs : drs, voff, lds_addr(sl + 2 * TB + (wave == 0 ? 0 : 1024)));
-        }
-    };
-    if (qt0 < nqt) stage(qt0);
-    if (qt0 + 1 < nqt) stage(qt0 + 1);
-
-    s16x8 kf[KG][NS], vf[KG][NS];
-#pragma unroll
-    for (int u = 0; u < KG; ++u) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            kf[u][s] = gload16(kbase + (long)kvl[u] * p.k_st + s * 32 + g * 8, kvl[u] < p.Tk);
-            vf[u][s] = gload16(vbase + (long)kvl[u] * p.v_st + s * 32 + g * 8, kvl[u] < p.Tk);
-        }
-    }
-    f32x4 dvacc[KG][NJ], dkacc[KG][NJ];
-#pragma unroll
-    for (int u = 0; u < KG; ++u)
-#pragma unroll
-        for (int jd = 0; jd < NJ; ++jd) { dvacc[u][jd] = (f32x4){0, 0, 0, 0}; dkacc[u][jd] = (f32x4){0, 0, 0, 0}; }
-    auto masked_tile = [&](int qt) {
-        return (qt * 64 + 64 > p.Tq) || (kb * KB + KB > p.Tk) || (CAUSAL && kb * KB + KB - 1 > qt * 64 + off);
-    };
-    // raw S and dP of query tile qt (lane: query 64qt + 16qi + 4g + r, key kvl[u])
-    auto sdp = [&](int qt, f32x4 (&sa)[KG][4], f32x4 (&da)[KG][4]) {
-        const char* qt_ = slot(qt);
-        const char* ot_ = qt_ + TB;
-#pragma unroll
-        for (int qi = 0; qi < 4; ++qi) {
-            s16x8 af[NS], of[NS];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                af[s] = rowfragx(qt_, qi, s, fo);
-                of[s] = rowfragx(ot_, qi, s, fo);
-            }
-#pragma unroll
-            for (int u = 0; u < KG; ++u) {
-                f32x4 x = {0, 0, 0, 0}, y = {0, 0, 0, 0};
-#pragma unroll
-                for (int s = 0; s < NS; ++s) x = MFMA(af[s], kf[u][s], x, 0, 0, 0);
-#pragma unroll
-                for (int s = 0; s < NS; ++s) y = MFMA(of[s], vf[u][s], y, 0, 0, 0);
-                sa[u][qi] = x;
-                da[u][qi] = y;
-            }
-        }
-    };
-    // P and dS of tile qt in place of its S / dP, then dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS
-    auto grad = [&](int qt, f32x4 (&sa)[KG][4], f32x4 (&da)[KG][4], auto masked_c) {
-        constexpr bool MASKED = decltype(masked_c)::value;
-        const char* qt_ = slot(qt);
-        const char* ot_ = qt_ + TB;
-        const float* lt_ = reinterpret_cast<const float*>(qt_ + 2 * TB);
-        const float* dt_ = reinterpret_cast<const float*>(qt_ + 2 * TB + 1024);
-        const int q0 = qt * 64;
-#pragma unroll
-        for (int qi = 0; qi < 4; ++qi) {
-            const int ql = qi * 16 + 4 * g;
-            const float4 l4 = *reinterpret_cast<const float4*>(lt_ + ql);
-            const float4 d4 = *reinterpret_cast<const float4*>(dt_ + ql);
-            const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-            for (int u = 0; u < KG; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(sa[u][qi][r] * sl2 - ls[r]);
-                    float pd = pv, dsv = pv * (da[u][qi][r] - dl[r]);
-                    if constexpr (MASKED) {
-                        const int qg = q0 + ql + r;
-                        if (kvl[u] >= p.Tk || qg >= p.Tq || (CAUSAL && kvl[u] > qg + off)) pd = dsv = 0.f;
-                    }
-                    sa[u][qi][r] = pd;
-                    da[u][qi][r] = dsv;
-                }
-        }
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            s16x8 pb[KG], sb[KG];
-#pragma unroll
-            for (int u = 0; u < KG; ++u) {
-                pb[u] = pack_p(sa[u][2 * ks], sa[u][2 * ks + 1]);
-                sb[u] = pack_p(da[u][2 * ks], da[u][2 * ks + 1]);
-            }
-#pragma unroll
-            for (int jd = 0; jd < NJ; ++jd) {
-                const s16x8 ao = colfragx(ot_, ks, jd, fo);
-#pragma unroll
-                for (int u = 0; u < KG; ++u) dvacc[u][jd] = MFMA(ao, pb[u], dvacc[u][jd], 0, 0, 0);
-                const s16x8 aq = colfragx(qt_, ks, jd, fo);
-#pragma unroll
-                for (int u = 0; u < KG; ++u) dkacc[u][jd] = MFMA(aq, sb[u], dkacc[u][jd], 0, 0, 0);
-            }
-        }
-    };
-    auto head = [&](int t) {  // tiles <= t + 1 landed for every wave; slot of t - 1 refilled with t + 2
-        vm_wait_all();
-        __syncthreads();
-        if (t + 2 < nqt) stage(t + 2);
-    };
-    using F = std::false_type;
-    using T = std::true_type;
-    vm_wait_all();
-    __syncthreads();
-    f32x4 sA[KG][4], dA[KG][4], sB[KG][4], dB[KG][4];
-    int qm = qt0;
-    while (qm < nqt && masked_tile(qm)) ++qm;  // [qt0, qm): diagonal head
-    int qe = qm;
-    while (qe < nqt && !masked_tile(qe)) ++qe;  // [qm, qe): unmasked; [qe, nqt): ragged tail
-    int t = qt0;
-    for (; t < qm; ++t) {
-        head(t);
-        if (CAUSAL && t * 64 + 63 + off < kvw) continue;  // wave-uniform: every query precedes this wave's keys
-        sdp(t, sA, dA);
-        grad(t, sA, dA, T{});
-    }
-    if (t < qe) sdp(t, sA, dA);
-    for (; t + 2 < qe; t += 2) {
-        head(t);
-        sdp(t + 1, sB, dB);
-        grad(t, sA, dA, F{});
-        head(t + 1);
-        sdp(t + 2, sA, dA);
-        grad(t + 1, sB, dB, F{});
-    }
-    if (t + 1 < qe) {
-        head(t);
-        sdp(t + 1, sB, dB);
-        grad(t, sA, dA, F{});
-        head(t + 1);
-        grad(t + 1, sB, dB, F{});
-        t += 2;
-    } else if (t < qe) {
-        head(t);
-        grad(t, sA, dA, F{});
-        t += 1;
-    }
-    for (; t < nqt; ++t) {
-        head(t);
-        sdp(t, sA, dA);
-        grad(t, sA, dA, T{});
-    }
-    if (p.bsum) {
-        const int E = p.H * D, nb64 = (p.Tk + 63) / 64;
-#pragma unroll
-        for (int u = 0; u < KG; ++u) {
-            const int blk = kb * KG + u;
-            if (blk < nb64) {
                 float* row = p.bsum + ((long)b * nb64 + blk) * 3 * E + h * D;
                 block_colsum64<D>(dkacc[u], p.scale, reinterpret_cast<float*>(smem), row + E, wave, lane);
                 block_colsum64<D>(dvacc[u], 1.f, reinterpret_cast<float*>(smem), row + 2 * E, wave, lane);
@@ -1782,31 +1334,6 @@ void attn_bwd_mfma(AttnArgs& a, hipStream_t st) {
 // the MFMA kernels' requirements: D ∈ {32, 64, 128} and 16-B aligned rows (strides in elements)
 bool mfma_head(int D) { return D == 32 || D == 64 || D == 128; }
 
-// D = 64 plain causal backward: query / key groups per wave of the dQ / dK-dV kernels (A/B knobs)
-int bwd_groups(const char* var) {
-    const char* e = std::getenv(var);
-    return (e && e[0] == '4') ? 4 : 2;
-}
-
-// D = 64 plain dK/dV: software-pipelined kernel (REPLICANN_ATTN_DKDV_PIPE=1: one key group per wave,
-// occupancy 2; 2: two key groups, occupancy 1; A/B)
-int bwd_dkdv_pipe() {
-    const char* e = std::getenv("REPLICANN_ATTN_DKDV_PIPE");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-}
-
-// D = 64 plain forward: software-pipelined kernel (REPLICANN_ATTN_FWD_PIPE=1, A/B)
-int fwd_pipe() {
-    const char* e = std::getenv("REPLICANN_ATTN_FWD_PIPE");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-}
-
-// D = 64 plain forward: query fragments per wave (REPLICANN_ATTN_FWD_QI=4: 64 queries per wave, A/B)
-int fwd_qi() {
-    const char* e = std::getenv("REPLICANN_ATTN_FWD_QI");  // read per launch (same-process A/B tests)
-    return (e && e[0] == '4') ? 4 : 2;
-}
-
 }  // namespace
 
 extern "C" {
@@ -1833,16 +1360,7 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         // plain causal / non-causal: the split-loop v2 kernel with the LEAN softmax bookkeeping
         // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
         if (!bias && p_drop == 0.f) {
-            if (fwd_pipe() == 2) {  // + sched-group interleave of those MFMAs with the softmax VALU
-                if (causal) attn_fwd64p_k<true, 2, 2, 1><<<grid, 256, 49152, st>>>(a);
-                else attn_fwd64p_k<false, 2, 2, 1><<<grid, 256, 49152, st>>>(a);
-            } else if (fwd_pipe() == 1) {  // software-pipelined QKᵀ of the next tile under this tile's softmax (A/B)
-                if (causal) attn_fwd64p_k<true, 2><<<grid, 256, 49152, st>>>(a);
-                else attn_fwd64p_k<false, 2><<<grid, 256, 49152, st>>>(a);
-            } else if (causal && fwd_qi() == 4) {  // 64 queries per wave: each K / V fragment read feeds 4 query fragments
-                dim3 g4(B * H * ((Tq + 255) / 256));
-                attn_fwd64v2_k<true, 2, true, 4><<<g4, 256, 32768, st>>>(a);
-            } else if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
+            if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
             else attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
@@ -1888,30 +1406,14 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         // plain causal / non-causal: two 64-query groups per wave in dQ (bwd -11 % at GPT-2-small
         // shapes) and two 64-key groups per wave in dK/dV (-2.4 %, occupancy 2 at 240 VGPRs);
         // bias / dropout: one group per wave
-        if (!bias && p_drop == 0.f && causal && bwd_groups("REPLICANN_ATTN_DQ_QG") == 4) {
-            dim3 g2c(B * H * ((Tq + 255) / 256));  // 4 query groups per wave (A/B)
-            attn_bwd_dq64_k<true, false, false, 1, 4><<<g2c, 256, 32768, st>>>(a);
-        } else if (!bias && p_drop == 0.f) {
+        if (!bias && p_drop == 0.f) {
             dim3 g2b(B * H * ((Tq + 127) / 128));
             if (causal) attn_bwd_dq64_k<true, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
             else attn_bwd_dq64_k<false, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_bwd_dq64_k, g2, 32768, st, a);
         }
-        if (!bias && p_drop == 0.f && bwd_dkdv_pipe()) {  // software-pipelined dK/dV (A/B)
-            if (bwd_dkdv_pipe() == 2) {  // 2 key groups per wave, one wave per SIMD
-                dim3 g1b(B * H * ((Tk + 127) / 128));
-                if (causal) attn_bwd_dkdv64p_k<true, 1, 2><<<g1b, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
-                else attn_bwd_dkdv64p_k<false, 1, 2><<<g1b, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
-            } else {
-                dim3 g1a(B * H * ((Tk + 63) / 64));
-                if (causal) attn_bwd_dkdv64p_k<true, 2, 1><<<g1a, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
-                else attn_bwd_dkdv64p_k<false, 2, 1><<<g1a, 256, 3 * (2 * kTB<64> + 2048), st>>>(a);
-            }
-        } else if (!bias && p_drop == 0.f && causal && bwd_groups("REPLICANN_ATTN_DKDV_KG") == 4) {
-            dim3 g1c(B * H * ((Tk + 255) / 256));  // 4 key groups per wave, one wave per SIMD (A/B)
-            attn_bwd_dkdv64_k<true, false, false, 1, 4><<<g1c, 256, 36864, st>>>(a);
-        } else if (!bias && p_drop == 0.f) {
+        if (!bias && p_drop == 0.f) {
             dim3 g1b(B * H * ((Tk + 127) / 128));
             if (causal) attn_bwd_dkdv64_k<true, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);
             else attn_bwd_dkdv64_k<false, false, false, 2, 2><<<g1b, 256, 36864, st>>>(a);

@@ -12,7 +12,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from replicann_amd import ops  # noqa: E402
+from replicann_amd import _ext, ops  # noqa: E402
 
 SHAPES = [  # (name, N, K, layout, act, residual)
     ("proj_fwd", 768, 768, "nt", 0, True),
@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
     modes = [int(x) for x in a.staged.split(",")]
+    _ext.ops()  # load the library: torch.ops.replicann.* below are used before any op call
     torch.manual_seed(0)
     for name, N, K, lay, act, res in SHAPES:
         if a.shapes and name not in a.shapes.split(","):

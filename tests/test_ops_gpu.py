@@ -373,20 +373,11 @@ def test_attention_d64_long(cuda):
     _attn_check(1, 1024, 2, 64, True)
 
 
-@pytest.mark.parametrize("qi,qg,kg,pipe", [("2", "2", "2", "0"), ("4", "2", "2", "0"), ("2", "4", "2", "0"),
-                                            ("2", "2", "4", "0"), ("4", "4", "4", "0"), ("2", "2", "2", "1"),
-                                            ("2", "2", "2", "2"), ("2", "2", "2", "d1"), ("2", "2", "2", "d2")])
-def test_attention_kernel_variants(cuda, monkeypatch, qi, qg, kg, pipe):
-    """The causal D=64 kernels with 32 / 64 queries per wave in the forward (REPLICANN_ATTN_FWD_QI) and
-    2 / 4 query (dQ) and key (dK/dV) groups per wave in the backward (REPLICANN_ATTN_DQ_QG / _DKDV_KG)
-    against the fp32 reference: full, diagonal and ragged tiles, Tq != Tk (causal offset), partial last
-    blocks; non-causal runs the default kernels."""
-    monkeypatch.setenv("REPLICANN_ATTN_FWD_QI", qi)
-    monkeypatch.setenv("REPLICANN_ATTN_DQ_QG", qg)
-    monkeypatch.setenv("REPLICANN_ATTN_DKDV_KG", kg)
-    # software-pipelined forward (1; 2: + sched groups) / dK-dV (d1: one key group, d2: two)
-    monkeypatch.setenv("REPLICANN_ATTN_FWD_PIPE", pipe if not pipe.startswith("d") else "0")
-    monkeypatch.setenv("REPLICANN_ATTN_DKDV_PIPE", pipe[1:] if pipe.startswith("d") else "0")
+def test_attention_d64_causal_offsets(cuda):
+    """The causal D=64 kernels (forward, dQ, dK/dV) against the fp32 reference: full, diagonal and
+    ragged tiles, Tq != Tk (causal offset), partial last blocks; a non-causal ragged case.
+    (The round-4 arms — 64 queries per wave, a software-pipelined forward / dK-dV, 4 query / key
+    groups per wave — measured slower and were removed: profiles/attention_arms_r4e.txt.)"""
     torch.manual_seed(70)
     _attn_check(2, 320, 3, 64, True)
     _attn_check(1, 100, 2, 64, True, Tk=260)
@@ -462,14 +453,10 @@ def test_attention_packed_grad(cuda):
     assert rel_err(o, of) < 2e-2 and rel_err(qkv.grad, qf.grad) < 4e-2
 
 
-@pytest.mark.parametrize("causal,T,dq", [(True, 256, "2"), (False, 200, "2"), (True, 320, "4"), (True, 200, "4")])
-@pytest.mark.parametrize("dkdv", ["2", "4", "p1", "p2"])
-def test_attention_packed_qkv_bias_grad(cuda, monkeypatch, causal, T, dq, dkdv):
+@pytest.mark.parametrize("causal,T", [(True, 256), (False, 200), (True, 320), (True, 200)])
+def test_attention_packed_qkv_bias_grad(cuda, causal, T):
     """Σ_rows dQKV (the c_attn bias gradient) reduced inside the attention backward kernels
-    (incl. the 2- and 4-group dQ / dK-dV kernels with a partial last block; 4 groups: causal only)."""
-    monkeypatch.setenv("REPLICANN_ATTN_DQ_QG", dq)
-    monkeypatch.setenv("REPLICANN_ATTN_DKDV_KG", dkdv if not dkdv.startswith("p") else "2")
-    monkeypatch.setenv("REPLICANN_ATTN_DKDV_PIPE", dkdv[1:] if dkdv.startswith("p") else "0")
+    (incl. an odd number of 64-row blocks: a partial last two-group block)."""
     from replicann_amd.utils.flat import FlatParams
     torch.manual_seed(11)
     B, H, D = 3, 4, 64

