@@ -1,6 +1,5 @@
 #!/bin/bash
-# round 4 (call F): re-run the GPU tests whose tolerances were re-derived, the pipelined dK/dV arms
-# (tests + A/B), then the staged-epilogue performance pass: M-sweep of the fused-epilogue shapes,
+# round 4 (call F): re-run the GPU tests whose tolerances were re-derived and the attention tests, then the staged-epilogue performance pass: M-sweep of the fused-epilogue shapes,
 # GPT-2-small step staged vs unstaged, and the step profile at HEAD.
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 PT="python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider"
@@ -8,16 +7,10 @@ fault() { grep -q "illegal memory access\|hipErrorIllegalAddress\|HSA_STATUS_ERR
 timeout -k 10 300 $PT tests/test_reference_parity_gpu.py tests/test_resnet_join_gpu.py > gpurun_out/t_fixed.log 2>&1; rc=$?
 echo "=== t_fixed rc=$rc"; grep -E "passed|failed" gpurun_out/t_fixed.log | tail -1; grep -E "^E   .*Error|FAILED" gpurun_out/t_fixed.log | head
 fault gpurun_out/t_fixed.log && exit 2
-timeout -k 10 300 $PT tests/test_ops_gpu.py -k "kernel_variants or qkv_bias_grad" > gpurun_out/t_dkdvp.log 2>&1; rc=$?
+timeout -k 10 300 $PT tests/test_ops_gpu.py -k "attention" > gpurun_out/t_dkdvp.log 2>&1; rc=$?
 echo "=== t_dkdvp rc=$rc"; grep -E "passed|failed" gpurun_out/t_dkdvp.log | tail -1; grep -E "FAILED" gpurun_out/t_dkdvp.log | head
 fault gpurun_out/t_dkdvp.log && exit 2
 [ $rc -ne 0 ] && exit 1
-for r in 1 2 3; do
-  for pp in 0 1 2; do
-    REPLICANN_ATTN_DKDV_PIPE=$pp timeout -k 10 120 python scripts/attn_ab.py 64 --rounds 3 > gpurun_out/attn_dkdvp_${pp}_$r.log 2>&1 || { echo "attn_ab $pp failed"; exit 1; }
-    echo "dkdv_pipe=$pp r$r: $(grep -o '"op": "attn_bwd".*"tflops": [0-9.]*' gpurun_out/attn_dkdvp_${pp}_$r.log | sed 's/, "B".*"ms"/ ms/')"
-  done
-done
 step() {  # step <name> <timeout> cmd...
   local n=$1 t=$2; shift 2
   timeout -k 10 $t "$@" > gpurun_out/$n.log 2>&1; local rc=$?
