@@ -30,11 +30,12 @@ def main():
     ap.add_argument("--shapes", default=None, help="comma-separated subset of the shape names")
     ap.add_argument("--m", default="16384,32768,65536,131072,262144")
     ap.add_argument("--cfg", type=int, default=9, help="tile config (9 = persistent; -1 = autotuned pick)")
-    ap.add_argument("--staged", default="1", help="comma list of staged-epilogue modes to interleave (1 on, 0 off)")
+    ap.add_argument("--staged", default="0", help="comma list of staged-epilogue modes to interleave (1 on, 0 off)")
     ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
     modes = [int(x) for x in a.staged.split(",")]
     _ext.ops()  # load the library: torch.ops.replicann.* below are used before any op call
+    staged0 = int(torch.ops.replicann.gemm_get_staged())
     torch.manual_seed(0)
     for name, N, K, lay, act, res in SHAPES:
         if a.shapes and name not in a.shapes.split(","):
@@ -59,7 +60,7 @@ def main():
                         fn()
                 g.replay()
                 graphs[md] = g
-            torch.ops.replicann.gemm_set_staged(1)
+            torch.ops.replicann.gemm_set_staged(staged0)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             for rnd in range(a.rounds):
