@@ -770,6 +770,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         __syncthreads();  // no DMA in flight yet: a plain barrier drains nothing
         deq = __builtin_amdgcn_readfirstlane(ring[1]);
     }
+    if (p.stagger > 0) {  // A/B: desynchronise the blocks' epilogues (block phase 0..3)
+        const int n = ((blockIdx.x >> 3) & 3) * p.stagger;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     int c_s = 0;  // compute side: sequence number of its item (ring slot), and the item
     int c_u = unit_of(0);  // (dynamic: the cursor is never more than one item ahead, nk >= 5)
     cu = c_u;
@@ -1181,6 +1185,10 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
         cus = cu_n;
     }
     a.st_nt = rn_gemm_st_nt(a);
+    {
+        static const int stg = [] { const char* e = std::getenv("REPLICANN_GEMM_STAGGER"); return e ? std::atoi(e) : 0; }();
+        a.stagger = (a.tiles_m * a.tiles_n * a.split > 2 * 256) ? stg : 0;  // several items per block only
+    }
     const int reserve = rn_gemm_get_reserve();
     if (reserve > 0 && reserve < cus) cus -= reserve;
     if (!DYN) a.sched = nullptr;
