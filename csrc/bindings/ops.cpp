@@ -58,8 +58,6 @@ void rn_sgd(void*, float*, const void*, int, float*, const uint8_t*, float*, lon
 long rn_gemm_ws_floats(int, int, int);
 void rn_gemm_set_sched(int);
 int rn_gemm_get_sched();
-void rn_gemm_set_staged(int);
-int rn_gemm_get_staged();
 void rn_gemm_set_reserve(int);
 int rn_gemm_get_reserve();
 int rn_gemm_sched_init(int);
@@ -1132,8 +1130,6 @@ TORCH_LIBRARY(replicann, m) {
     m.def("gemm_tuning_table() -> str");
     m.def("gemm_tuning_load(str table) -> int");
     m.def("gemm_set_sched(int mode) -> ()");
-    m.def("gemm_set_staged(int mode) -> ()");
-    m.def("gemm_get_staged() -> int");
     m.def("gemm_get_sched() -> int");
     m.def("gemm_set_reserve(int cus) -> ()");
     m.def("gemm_get_reserve() -> int");
@@ -1193,8 +1189,6 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
 // persistent-GEMM schedule knobs (csrc/include/gemm_pk.h: dynamic tile queue, CU reservation)
 void gemm_set_sched(int64_t m) { rn_gemm_set_sched((int)m); }
 int64_t gemm_get_sched() { return rn_gemm_get_sched(); }
-void gemm_set_staged(int64_t m) { rn_gemm_set_staged((int)m); }
-int64_t gemm_get_staged() { return rn_gemm_get_staged(); }
 void gemm_set_reserve(int64_t r) { rn_gemm_set_reserve((int)r); }
 int64_t gemm_get_reserve() { return rn_gemm_get_reserve(); }
 int64_t gemm_sched_init(int64_t dev) { return rn_gemm_sched_init((int)dev); }
@@ -1203,8 +1197,6 @@ TORCH_LIBRARY_IMPL(replicann, CompositeExplicitAutograd, m) {
     m.impl("native_version", &native_version);
     m.impl("gemm_set_sched", &gemm_set_sched);
     m.impl("gemm_get_sched", &gemm_get_sched);
-    m.impl("gemm_set_staged", &gemm_set_staged);
-    m.impl("gemm_get_staged", &gemm_get_staged);
     m.impl("gemm_set_reserve", &gemm_set_reserve);
     m.impl("gemm_get_reserve", &gemm_get_reserve);
     m.impl("gemm_sched_init", &gemm_sched_init);

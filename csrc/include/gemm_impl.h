@@ -68,9 +68,6 @@ struct GemmArgs {
     // for outputs larger than the 256 MiB Infinity Cache, e.g. the LM-head logits: such a stream
     // cannot stay resident and would only evict the operand panels the main loop re-reads)
     int st_nt;
-    // persistent kernel only: start-delay unit (s_sleep(127) rounds) of the block phase
-    // ((blockIdx >> 3) & 3), spreading the epilogue bursts of a lock-stepped grid (A/B)
-    int stagger;
     // split-K reduction only: slab s lives at ws + s·slab_step·M·N (<= 1: contiguous slabs); set when
     // a group pre-reduction (splitk_group_k) left its partial sums in every slab_step-th slab
     int slab_step;

@@ -39,9 +39,13 @@
 // Epilogue operand reads (residual, saved activation): the full-tile read at the end of an item
 // waits behind a vmcnt(0) that also drains the next item's in-flight operand DMA (≈ 15-20 % of a
 // K = 768 tile, profiles/gemm_epilogue_aux_r3k.txt).  An L2 prefetch of that tile during the
-// item's last K-tiles (extra LDS-DMA into scratch LDS) changed nothing — the drain, not the
-// latency of the aux bytes, is the cost — and holding the tile in registers ahead of time does
-// not fit the 256-VGPR budget (it spills).
+// item's last K-tiles (extra LDS-DMA into scratch LDS) changed nothing, holding the tile in
+// registers ahead of time does not fit the 256-VGPR budget (it spills), and streaming it through
+// the operand ring as two extra K-tiles (round 4) was slower on every such shape (fc2 + residual
+// 269 → 312 us, fc1 act-backward dgrad 403 → 412 us: profiles/gemm_staged_ab_r4f.txt,
+// gemm_staged_pmc_r4g.txt) and was removed.  Staggering the blocks' start so their epilogues do
+// not coincide (all 256 CUs read / store their tiles in lock step) was no better either
+// (profiles/gemm_stagger_ab_r4i.txt).
 //
 // Tile schedule (DYN instantiations; chosen per launch while the queue is enabled — by the data-
 // parallel reducer whenever collectives can run beside the backward, rn_gemm_set_sched): the grid
@@ -283,8 +287,7 @@ RN_DEV int pk_deq_take(uint32_t v) {
 }
 #pragma clang diagnostic pop
 
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false,
-          bool STG = false>
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false>
 __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     // FP8: 0 bf16; 1 e4m3 x e4m3; 2 A e5m2 (a gradient) x B e4m3.  Operand layouts: both K-contiguous
     // (the forward x·Wᵀ), A K- and B MN-contiguous (the data gradient dY·W), both MN-contiguous (the
@@ -299,7 +302,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     static_assert(!F8B_MN || SPLIT || (ACT == ACT_NONE && !F32), "fp8 MN B, bf16 output: plain epilogue only");
     constexpr int S_EPI = (DBG & 64) ? 0 : pk_epi_stores<ACT, SPLIT, F32>() + ((F8B_MN && !SPLIT) ? 16 : 0);
     static_assert(!DYN || (!FP8 && DBG == 0), "dynamic schedule: bf16 production kernels only");
-    static_assert(!STG || (!SPLIT && !F32 && !DYN && !FP8 && DBG == 0), "staged epilogue: bf16 static walk only");
     constexpr int BM = 256, BN = 256;
     constexpr int WY = 6;  // ops younger than a phase's target half-tile: 3 half-tiles × 2 DMA
     static_assert(WY + 1 + S_EPI <= 63, "vmcnt range");
@@ -404,13 +406,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
                   : 0u;
     };
     bool in_loop = false;
-    // STG: the epilogue operand of the item just finished (saved pre-activation / residual /
-    // accumulate target) is streamed as 2 extra K-tiles after the item's last operand K-tile
-    // (caux = 0, 1; -1 = operand K-tiles): cax = its 256x256 tile, caml/canl its valid extent
-    [[maybe_unused]] const bf16* const aux_src =
-        STG ? (act_bwd(ACT) ? p.pre : (p.res ? p.res : (const bf16*)p.C)) : nullptr;
-    [[maybe_unused]] int caux = -1, caml = 0, canl = 0;
-    [[maybe_unused]] const bf16* cax = nullptr;
     auto cur_set = [&]() {
         int m0, n0, kb, ke, tm;
         item_coords(cu, m0, n0, kb, ke, tm);
@@ -424,20 +419,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     auto cur_adv = [&]() {
         ++ct;
         if (cu < 0) return;  // exhausted: every later DMA only zero-fills its slot
-        if constexpr (STG) {
-            if (caux >= 0) {  // inside the finished item's epilogue-operand K-tiles
-                if (++caux < 2) return;
-                caux = -1;
-                cu = unit_of(++cs);
-                if (cu >= 0) {
-                    cur_set();
-                } else {
-                    cml = cnl = ckl = 0;
-                    intr = 0u;
-                }
-                return;
-            }
-        }
         if (++ckt < nk) {
             ca += a_step;
             cb += b_step;
@@ -446,15 +427,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             return;
         }
         ckt = 0;
-        if constexpr (STG) {  // the item's operands are all issued: its epilogue operand follows
-            int m0, n0, kb, ke, tm;
-            item_coords(cu, m0, n0, kb, ke, tm);
-            cax = aux_src + (long)m0 * p.ldc + n0;
-            caml = p.M - m0;
-            canl = p.N - n0;
-            caux = 0;
-            return;
-        }
         cu = unit_of(++cs);
         if (cu >= 0) {
             cur_set();
@@ -470,22 +442,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             if (in_loop) return;
         }
         const uint32_t dst = lds0 + (uint32_t)(((ct & 1) * 4 + H) * PK_HALF);
-        if constexpr (STG) {
-            if (caux >= 0) {
-                // epilogue-operand half-tile H of aux K-tile caux: quadrant (mh = caux, nh = H >> 1),
-                // fragment rows i = 2·(H & 1) + j of this wave — exactly the 16 B per lane the same
-                // lane's epilogue reads (lane-linear, so only this wave ever reads its 2 KiB)
-                const u32x4 rs = rsrc_sgpr(cax);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int r = caux * 128 + wr * 64 + ((H & 1) * 2 + j) * 16 + (lane & 15);
-                    const int c = (H >> 1) * 128 + wc * 32 + 8 * (lane >> 4);
-                    const bool ok = r < caml && c < canl;
-                    dma16_at(rs, ok ? (uint32_t)(((long)r * p.ldc + c) * 2) : 0xFFFFFFF0u, dst + j * 1024);
-                }
-                return;
-            }
-        }
         const bool isA = (H == 0 || H == 3);
         const bf16* base = isA ? (H == 3 ? ca + a_half : ca) : (H == 2 ? cb + b_half : cb);
         const int mnl = isA ? (H == 3 ? cml - 128 : cml) : (H == 2 ? cnl - 128 : cnl);
@@ -770,10 +726,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
         __syncthreads();  // no DMA in flight yet: a plain barrier drains nothing
         deq = __builtin_amdgcn_readfirstlane(ring[1]);
     }
-    if (p.stagger > 0) {  // A/B: desynchronise the blocks' epilogues (block phase 0..3)
-        const int n = ((blockIdx.x >> 3) & 3) * p.stagger;
-        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-    }
     int c_s = 0;  // compute side: sequence number of its item (ring slot), and the item
     int c_u = unit_of(0);  // (dynamic: the cursor is never more than one item ahead, nk >= 5)
     cu = c_u;
@@ -803,22 +755,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     // phase wait: σ ≤ φ+2 must have landed (this wave's DMA); younger = the 3 half-tiles
     // issued in the previous 3 phases (6 ops) plus, within 4 phases of an epilogue, its stores,
     // plus in q1-q3 (XW) wave 0's schedule atomic of this K-tile
-    // STG: stores issued per epilogue pseudo-phase (2 fragment rows: output [+ pre-activation]) and
-    // the column-sum stores of the last one; a phase's wait lets the ops of the 3 phases before it
-    // stay in flight: 6 DMA + the stores among them (exact counts: vmcnt retires in order)
-    constexpr int STG_EP = 2 * (1 + (act_fwd(ACT) ? 1 : 0));
-    constexpr int STG_CS = act_bwd(ACT) ? 4 : 0;
-    static_assert(WY + 3 * STG_EP + STG_CS <= 63, "vmcnt range");
     auto phase_wait = [&](auto xw) {
         if constexpr (DBG & 2) return;
-        if constexpr (STG) {
-            if (since_epi == 0) vm_wait<WY + 3 * STG_EP + STG_CS>();
-            else if (since_epi == 1) vm_wait<WY + 2 * STG_EP + STG_CS>();
-            else if (since_epi == 2) vm_wait<WY + STG_EP + STG_CS>();
-            else vm_wait<WY>();
-            ++since_epi;
-            return;
-        }
         constexpr bool XW = decltype(xw)::value;
         if (since_epi < 4) {
             if (DYN && XW && wave == 0) vm_wait<WY + 1 + S_EPI>();
@@ -900,158 +838,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     }                                                                                                  \
     sync_mma_end();
 
-    // ---- STG: the epilogue as 8 pseudo-phases (2 pseudo K-tiles) of the half-tile stream ----
-    // Pseudo-phase (A, Q) takes quadrant (mh = A, nh = Q >> 1), fragment rows i = 2·(Q & 1) + 0/1: its
-    // epilogue operand was streamed into half-tile Q of pseudo K-tile A (issued 6 phases earlier,
-    // BEFORE the next item's operands, so a counted wait retires it and the next item's DMA stays in
-    // flight — the unstaged epilogue's full-tile read sat behind a vmcnt(0) that drained it).  Each
-    // pseudo-phase keeps the stream going (one half-tile) and the main loop's two barriers, so the
-    // DMA placement rules and the wave-group stagger hold across the epilogue unchanged.  Outputs are
-    // bitwise those of the unstaged epilogue (same per-element math; per nh the column sums add the
-    // rows in the same mh-major order).
-    auto staged_epilogue = [&](int u, int m0, int n0, int tm) {
-        if constexpr (STG) {
-            const int mlim = p.M - m0, nlim = p.N - n0;
-            const long ldc = p.ldc;
-            const u32x4 crs_u = pk_rsrc_u((char*)p.C + ((long)m0 * ldc + n0) * 2, 0x7FFFFFF0u);
-            const u32x4 prs = pk_rsrc_u(act_fwd(ACT) && p.pre ? (void*)(p.pre + (long)m0 * ldc + n0) : nullptr,
-                                        act_fwd(ACT) && p.pre ? 0x7FFFFFF0u : 0u);
-            auto off = [&](int mh, int i, int nh) -> uint32_t {
-                const int r = mh * 128 + wr * 64 + i * 16 + (lane & 15);
-                const int c = nh * 128 + wc * 32 + 8 * G;
-                return (r < mlim && c < nlim) ? (uint32_t)(((long)r * ldc + c) * 2) : 0xFFFFFFF0u;
-            };
-            float bias[2][8];
-            float csum[2][8];
-#pragma unroll
-            for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-                for (int t = 0; t < 8; ++t) bias[nh][t] = csum[nh][t] = 0.f;
-            auto pseudo = [&](auto ac, auto qc) {
-                constexpr int A = decltype(ac)::value, Q = decltype(qc)::value, P = A * 4 + Q;
-                constexpr int E1 = P >= 1 ? STG_EP : 0, E2 = P >= 2 ? STG_EP : 0, E3 = P >= 3 ? STG_EP : 0;
-                vm_wait<WY + E1 + E2 + E3>();
-                const char* sl = smem + (((u + 1 + A) & 1) * 4 + Q) * PK_HALF + wave * 2048 + lane * 16;
-                const u32x4 av0 = *reinterpret_cast<const u32x4*>(sl);
-                const u32x4 av1 = *reinterpret_cast<const u32x4*>(sl + 1024);
-                if constexpr (P == 0) {
-                    // bias: the wave's 2 × 32 columns through the scalar cache (retired by the
-                    // lgkmcnt(0) below), each lane picks its 8
-                    if (!act_bwd(ACT) && p.bias) {
-#pragma unroll
-                        for (int nh = 0; nh < 2; ++nh) {
-                            const int cb = n0 + nh * 128 + wc * 32;
-                            if (cb + 32 <= p.N) {
-                                const __attribute__((address_space(4))) u32x4* bp =
-                                    (const __attribute__((address_space(4))) u32x4*)(p.bias + cb);
-                                u32x4 b0 = bp[0], b1 = bp[1], b2 = bp[2], b3 = bp[3];
-                                asm volatile("" : "+s"(b0), "+s"(b1), "+s"(b2), "+s"(b3));
-                                const u32x4 bsel = G == 0 ? b0 : (G == 1 ? b1 : (G == 2 ? b2 : b3));
-                                pk_unpack8(bsel, bias[nh]);
-                            } else if (cb + 8 * G < p.N) {
-                                const u32x4 bu = *reinterpret_cast<const u32x4*>(p.bias + cb + 8 * G);
-                                pk_unpack8(bu, bias[nh]);
-                            }
-                        }
-                    }
-                }
-                if constexpr (Q == 0) issue_h(H2{});
-                else if constexpr (Q == 1) issue_h(H3{});
-                else if constexpr (Q == 2) {
-                    cur_adv();
-                    issue_h(H0{});
-                } else issue_h(H1{});
-                sync_mma_begin();
-                constexpr int mh = A, nh = Q >> 1;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int i = (Q & 1) * 2 + j;
-                    float v[8];
-                    const bool swp = !BKC && (G & 1);
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) {
-                        const float x0 = acc[mh][nh][i][c >> 2][c & 3], x1 = acc[mh][nh][i][(c >> 2) ^ 1][c & 3];
-                        v[c] = (swp ? x1 : x0) * alpha;
-                    }
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) v[c] += bias[nh][c];
-                    if constexpr (act_fwd(ACT)) {
-                        const u32x4 pu = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
-                                          pk_pack2(v[6], v[7])};
-                        if constexpr (ACT == ACT_GELU_D) {
-                            pk_unpack8(pu, v);
-                            float d[8];
-#pragma unroll
-                            for (int c = 0; c < 8; ++c) v[c] = gelu_and_grad_f(v[c], d[c]);
-                            const u32x4 du = {pk_pack2(d[0], d[1]), pk_pack2(d[2], d[3]), pk_pack2(d[4], d[5]),
-                                              pk_pack2(d[6], d[7])};
-                            pk_st16(du, prs, off(mh, i, nh));
-                        } else {
-                            pk_st16(pu, prs, off(mh, i, nh));
-                            if (p.pre) pk_unpack8(pu, v);
-#pragma unroll
-                            for (int c = 0; c < 8; ++c) v[c] = act_f<ACT>(v[c]);
-                        }
-                    }
-                    float ax[8];
-                    pk_unpack8(j == 0 ? av0 : av1, ax);
-                    if constexpr (act_bwd(ACT)) {
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) {
-                            v[c] = (float)(bf16)v[c] * act_grad_f<ACT>(ax[c]);
-                            csum[nh][c] += (float)(bf16)v[c];
-                        }
-                    } else {
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) v[c] += ax[c];
-                    }
-                    const u32x4 ou = {pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]),
-                                      pk_pack2(v[6], v[7])};
-                    if (p.st_nt & 1) pk_st16_nt(ou, crs_u, off(mh, i, nh));
-                    else pk_st16(ou, crs_u, off(mh, i, nh));
-                }
-                if constexpr (P == 7 && act_bwd(ACT)) {
-                    // per-wave column sums of the stored dH (as the unstaged epilogue)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) {
-                            float sv = csum[h][c];
-                            sv += __shfl_xor(sv, 1, 64);
-                            sv += __shfl_xor(sv, 2, 64);
-                            sv += __shfl_xor(sv, 4, 64);
-                            sv += __shfl_xor(sv, 8, 64);
-                            csum[h][c] = sv;
-                        }
-                    float* cpb = p.colpart ? p.colpart + ((long)tm * 2 + wr) * p.N + n0 : nullptr;
-                    const u32x4 cprs = pk_rsrc_u(cpb, cpb ? 0x7FFFFFF0u : 0u);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int c = h * 128 + wc * 32 + 8 * G;
-                        const uint32_t o = ((lane & 15) == 0 && c < nlim) ? (uint32_t)(c * 4) : 0xFFFFFFF0u;
-                        pk_st16((u32x4){__builtin_bit_cast(uint32_t, csum[h][0]), __builtin_bit_cast(uint32_t, csum[h][1]),
-                                        __builtin_bit_cast(uint32_t, csum[h][2]), __builtin_bit_cast(uint32_t, csum[h][3])},
-                                cprs, o);
-                        pk_st16((u32x4){__builtin_bit_cast(uint32_t, csum[h][4]), __builtin_bit_cast(uint32_t, csum[h][5]),
-                                        __builtin_bit_cast(uint32_t, csum[h][6]), __builtin_bit_cast(uint32_t, csum[h][7])},
-                                cprs, o == 0xFFFFFFF0u ? o : o + 16);
-                    }
-                }
-                sync_mma_end();
-            };
-            using A0 = std::integral_constant<int, 0>;
-            using A1 = std::integral_constant<int, 1>;
-            pseudo(A0{}, H0{});
-            pseudo(A0{}, H1{});
-            pseudo(A0{}, H2{});
-            pseudo(A0{}, H3{});
-            pseudo(A1{}, H0{});
-            pseudo(A1{}, H1{});
-            pseudo(A1{}, H2{});
-            pseudo(A1{}, H3{});
-        }
-        (void)u; (void)m0; (void)n0; (void)tm;
-    };
 
     // static walk: the block's item count is known (bid + s·grid < items)
     const int n_static = DYN ? 0 : ((items - bid + grid - 1) / grid) * nk;
@@ -1084,9 +870,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
             // retire wave 0's schedule op of this K-tile (issued before q0's DMA: 8 younger ops);
             // every other op this waits for, the next q0 wait would wait for anyway
             if constexpr (DYN) vm_wait<8>();
-            if constexpr (STG) {
-                staged_epilogue(u, c_m0, c_n0, c_tm);
-            } else if constexpr (!(DBG & 4)) {
+            if constexpr (!(DBG & 4)) {
                 epilogue(c_m0, c_n0, c_tm, c_sid);
             } else {  // keep the accumulators (and the MFMAs feeding them) alive
 #pragma unroll
@@ -1162,10 +946,9 @@ inline int* pk_sched_slot(const GemmArgs& a, hipStream_t st) {
     return rn_gemm_sched_slot(dev, st);
 }
 
-template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false,
-          bool STG = false>
+template <bool AK, bool BKC, int ACT, bool SPLIT, bool F32, int DBG = 0, int FP8 = 0, bool DYN = false>
 void launch_pk_t(GemmArgs& a, hipStream_t st) {
-    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8, DYN, STG>;
+    auto kern = gemm_pk<AK, BKC, ACT, SPLIT, F32, DBG, FP8, DYN>;
     static int attr_dev = -1;  // the >64 KiB LDS opt-in, per device the process launches on
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -1185,10 +968,6 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
         cus = cu_n;
     }
     a.st_nt = rn_gemm_st_nt(a);
-    {
-        static const int stg = [] { const char* e = std::getenv("REPLICANN_GEMM_STAGGER"); return e ? std::atoi(e) : 0; }();
-        a.stagger = (a.tiles_m * a.tiles_n * a.split > 2 * 256) ? stg : 0;  // several items per block only
-    }
     const int reserve = rn_gemm_get_reserve();
     if (reserve > 0 && reserve < cus) cus -= reserve;
     if (!DYN) a.sched = nullptr;

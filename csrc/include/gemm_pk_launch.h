@@ -5,42 +5,14 @@
 #pragma once
 #include "gemm_pk.h"
 
-extern "C" int rn_gemm_get_staged();
 
 namespace rn_gemm_detail {
 
-// Staged epilogue (gemm_pk.h, STG): an epilogue that reads a full output-shaped operand — the saved
-// pre-activation of an activation backward, a residual, or a bf16 accumulate target (exactly one of
-// them) — streams it through the operand ring instead of reading it behind a vmcnt(0) drain.
-// REPLICANN_GEMM_STAGED=0 keeps the unstaged epilogue (A/B).
-inline bool pk_staged_on() { return rn_gemm_get_staged() != 0; }
-inline bool pk_staged(const GemmArgs& a, int act) {
-    if (!pk_staged_on() || a.split > 1 || a.out_f32 || a.q8) return false;
-    if (act_bwd(act)) return a.pre && !a.res && !a.accumulate;
-    return act == ACT_NONE && ((a.res != nullptr) != (a.accumulate != 0));
-}
 
 template <bool AK, bool BKC, bool DYN>
 void pk_launch_layout(GemmArgs& a, int act, hipStream_t st) {
     constexpr bool dgrad = AK && !BKC;  // activation-backward epilogues: dY·W layout only
     constexpr bool fwd = AK && BKC;     // saved-derivative GELU: x·Wᵀ layout only
-    if constexpr (!DYN) {
-        if (pk_staged(a, act)) {
-            switch (act) {
-                case ACT_NONE: launch_pk_t<AK, BKC, ACT_NONE, false, false, 0, false, false, true>(a, st); return;
-                case ACT_MUL_BWD:
-                    if constexpr (dgrad) { launch_pk_t<AK, BKC, ACT_MUL_BWD, false, false, 0, false, false, true>(a, st); return; }
-                    break;
-                case ACT_GELU_BWD:
-                    if constexpr (dgrad) { launch_pk_t<AK, BKC, ACT_GELU_BWD, false, false, 0, false, false, true>(a, st); return; }
-                    break;
-                case ACT_RELU_BWD:
-                    if constexpr (dgrad) { launch_pk_t<AK, BKC, ACT_RELU_BWD, false, false, 0, false, false, true>(a, st); return; }
-                    break;
-                default: break;
-            }
-        }
-    }
     if (a.split > 1) {
         launch_pk_t<AK, BKC, ACT_NONE, true, true, 0, false, DYN>(a, st);
         return;

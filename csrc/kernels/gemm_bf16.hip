@@ -127,21 +127,6 @@ int rn_gemm_get_sched() {
     }
     return v;
 }
-// staged epilogue of the persistent GEMM (gemm_pk_launch.h pk_staged): off unless
-// REPLICANN_GEMM_STAGED=1 — measured slower on the shapes it targets (profiles/gemm_staged_ab_r4f.txt:
-// fc2 fwd + residual 269 → 312 us, fc1 act-backward dgrad 403 → 412 us, GPT-2-small step 62.9 → 63.7 ms);
-// the setter exists for same-process A/B tests
-static std::atomic<int> g_staged{-1};
-void rn_gemm_set_staged(int m) { g_staged = m ? 1 : 0; }
-int rn_gemm_get_staged() {
-    int v = g_staged.load();
-    if (v < 0) {
-        const char* e = std::getenv("REPLICANN_GEMM_STAGED");
-        v = (e && e[0] == '1') ? 1 : 0;
-        g_staged = v;
-    }
-    return v;
-}
 void rn_gemm_set_reserve(int r) { g_reserve = r < 0 ? 0 : (r > 128 ? 128 : r & ~7); }
 int rn_gemm_get_reserve() { return g_reserve.load(); }
 

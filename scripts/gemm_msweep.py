@@ -30,12 +30,9 @@ def main():
     ap.add_argument("--shapes", default=None, help="comma-separated subset of the shape names")
     ap.add_argument("--m", default="16384,32768,65536,131072,262144")
     ap.add_argument("--cfg", type=int, default=9, help="tile config (9 = persistent; -1 = autotuned pick)")
-    ap.add_argument("--staged", default="0", help="comma list of staged-epilogue modes to interleave (1 on, 0 off)")
     ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
-    modes = [int(x) for x in a.staged.split(",")]
     _ext.ops()  # load the library: torch.ops.replicann.* below are used before any op call
-    staged0 = int(torch.ops.replicann.gemm_get_staged())
     torch.manual_seed(0)
     for name, N, K, lay, act, res in SHAPES:
         if a.shapes and name not in a.shapes.split(","):
@@ -48,33 +45,27 @@ def main():
             pre = (torch.rand(M, N, device="cuda").bfloat16() if act in (3, 4, 6)  # read by the epilogue
                    else torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if act else None)
             fn = lambda: ops.gemm(A, B, ta=ta, tb=tb, residual=R, act=act, preact=pre, cfg=a.cfg)  # noqa: E731
-            graphs = {}
-            for md in modes:  # one graph per mode: the staged choice is made at launch (capture) time
-                torch.ops.replicann.gemm_set_staged(md)
-                for _ in range(3):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(a.iters):
                     fn()
-                torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for _ in range(a.iters):
-                        fn()
-                g.replay()
-                graphs[md] = g
-            torch.ops.replicann.gemm_set_staged(staged0)
+            g.replay()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             for rnd in range(a.rounds):
-                for md in modes:
-                    e0.record()
-                    graphs[md].replay()
-                    e1.record()
-                    torch.cuda.synchronize()
-                    ms = e0.elapsed_time(e1) / a.iters
-                    tiles = -(-M // 256) * -(-N // 256)
-                    print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "cfg": a.cfg, "staged": md,
-                                      "tiles_per_cu": round(tiles / 256, 2), "us": round(ms * 1e3, 2),
-                                      "tflops": round(2 * M * N * K / ms / 1e9, 1)}), flush=True)
-            del A, B, R, pre, graphs
+                e0.record()
+                g.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                tiles = -(-M // 256) * -(-N // 256)
+                print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "cfg": a.cfg,
+                                  "tiles_per_cu": round(tiles / 256, 2), "us": round(ms * 1e3, 2),
+                                  "tflops": round(2 * M * N * K / ms / 1e9, 1)}), flush=True)
+            del A, B, R, pre, g
 
 
 if __name__ == "__main__":
