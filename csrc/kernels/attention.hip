@@ -683,26 +683,6 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
 }
 
 // ============================== backward, D = 64 ==============================
-// delta[b,h,q] = sum_d dO * O  — one thread per (b, q, h) row of D = 64 (8 x 16-B loads each)
-__global__ void __launch_bounds__(256) attn_delta_k(AttnArgs p) {
-    const long i = blockIdx.x * 256L + threadIdx.x;
-    if (i >= (long)p.B * p.Tq * p.H) return;
-    const int h = i % p.H;
-    const long bq = i / p.H;
-    const int q = bq % p.Tq, b = bq / p.Tq;
-    const bf16* dp = p.dout + b * p.do_sb + (long)q * p.do_st + h * p.do_sh;
-    const bf16* op = p.o + b * p.o_sb + (long)q * p.o_st + h * p.o_sh;
-    float s = 0.f;
-    for (int ch = 0; ch < p.D / 8; ++ch) {
-        float a[8], o[8];
-        load8(dp + ch * 8, a);
-        load8(op + ch * 8, o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += a[j] * o[j];
-    }
-    const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + q] = s;
-}
-
 // dK, dV: grid (B*H, ceil(Tk/(64·KG))); key group u (< KG) of wave w owns keys
 // kb·64·KG + 64·u + 16w + (lane&15).  KG = 2: every Q / dO fragment read from LDS feeds both key
 // groups' MFMAs and each wave carries two independent S → P → dS chains (as in the dQ kernel).
@@ -804,10 +784,12 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
             const int ql = qi * 16 + 4 * g;
             const float4 l4 = *reinterpret_cast<const float4*>(lt_ + ql);
             const float4 d4 = *reinterpret_cast<const float4*>(dt_ + ql);
-            const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+            // the dQ kernel stored −δ: without dropout it is the dP accumulator's start value
+            const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, nd[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int u = 0; u < KG; ++u) {
                 f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
+                if constexpr (!DROP) da = (f32x4){nd[0], nd[1], nd[2], nd[3]};
 #pragma unroll
                 for (int s = 0; s < NS; ++s) sa = MFMA(af[s], kf[u][s], sa, 0, 0, 0);
 #pragma unroll
@@ -815,12 +797,15 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int qg = q0 + ql + r;
-                    float x = sa[r] * sl2;
+                    float x = __builtin_fmaf(sa[r], sl2, -ls[r]);  // lse in base-2 units: one FMA
                     if constexpr (BIAS) {
                         if (qg < p.Tq && kvl[u] < p.Tk)
                             x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qg) * p.Tk + kvl[u]] * LOG2E;
                     }
-                    float pv = __builtin_amdgcn_exp2f(x - ls[r]);  // lse in base-2 units: one FMA with x
+                    // masked scores: exponent −inf, so P = 0 and dS = 0 follow (one select per element)
+                    if constexpr (MASKED)
+                        if (kvl[u] >= p.Tk || qg >= p.Tq || (CAUSAL && kvl[u] > qg + off)) x = -INFINITY;
+                    float pv = __builtin_amdgcn_exp2f(x);
                     float dpv = da[r];
                     float pd = pv;
                     if constexpr (DROP) {
@@ -829,23 +814,9 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
                         dpv = keep ? dpv * rd : 0.f;
                     }
                     pq[u][qi][r] = pd;
-                    dsq[u][qi][r] = pv * (dpv - dl[r]);
+                    dsq[u][qi][r] = DROP ? pv * (dpv + nd[r]) : pv * dpv;
                 }
             }
-        }
-        if constexpr (MASKED) {
-#pragma unroll
-            for (int u = 0; u < KG; ++u)
-#pragma unroll
-                for (int qi = 0; qi < 4; ++qi)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int qg = q0 + qi * 16 + 4 * g + r;
-                        if (kvl[u] >= p.Tk || qg >= p.Tq || (CAUSAL && kvl[u] > qg + off)) {
-                            pq[u][qi][r] = 0.f;
-                            dsq[u][qi][r] = 0.f;
-                        }
-                    }
         }
         // dV^T[d][kv] += dO^T[d][q] Pd[q][kv];  dK^T[d][kv] += Q^T[d][q] dS[q][kv]
 #pragma unroll
@@ -974,7 +945,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
                 part += (float)__builtin_bit_cast(bf16, (short)of[j]) * (float)__builtin_bit_cast(bf16, (short)df[u][s][j]);
         }
         dl[u] = sum4groups(part);
-        if (qok[u] && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qgl[u]] = dl[u];
+        // stored NEGATED: the dK/dV kernel starts its dP accumulators at −δ (dP − δ from the MFMA)
+        if (qok[u] && g == 0) const_cast<float*>(p.delta)[((long)b * p.H + h) * p.Tq + qgl[u]] = -dl[u];
 #pragma unroll
         for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(qf[u][s]), "+v"(df[u][s]));
         asm volatile("" : "+v"(dl[u]));  // loads retired here
@@ -1025,7 +997,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             }
 #pragma unroll
             for (int u = 0; u < QG; ++u) {
-                f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
+                // without dropout the dP accumulator starts at −δ: dS = P ⊙ (dP − δ) is one multiply
+                const float d0 = DROP ? 0.f : -dl[u];
+                f32x4 sa = {0, 0, 0, 0}, da = {d0, d0, d0, d0};
 #pragma unroll
                 for (int s = 0; s < NS; ++s) sa = MFMA(kr[s], qf[u][s], sa, 0, 0, 0);
 #pragma unroll
@@ -1033,31 +1007,23 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int kvj = kv0 + j * 16 + 4 * g + r;
-                    float x = sa[r] * sl2;
+                    float x = __builtin_fmaf(sa[r], sl2, -lse2[u]);
                     if constexpr (BIAS) {
                         if (qok[u] && kvj < p.Tk)
                             x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qgl[u]) * p.Tk + kvj] * LOG2E;
                     }
-                    float pv = __builtin_amdgcn_exp2f(x - lse2[u]);
+                    // masked scores: exponent −inf, so dS = 0 (rows past Tq: lse = +inf does the same)
+                    if constexpr (MASKED)
+                        if (kvj >= p.Tk || (CAUSAL && kvj > qgl[u] + off)) x = -INFINITY;
+                    float pv = __builtin_amdgcn_exp2f(x);
                     float dpv = da[r];
                     if constexpr (DROP) {
                         const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qgl[u], kvj)) >= p.p_drop;
                         dpv = keep ? dpv * rd : 0.f;
                     }
-                    dsv[u][j][r] = pv * (dpv - dl[u]);
+                    dsv[u][j][r] = DROP ? pv * (dpv - dl[u]) : pv * dpv;
                 }
             }
-        }
-        if constexpr (MASKED) {
-#pragma unroll
-            for (int u = 0; u < QG; ++u)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int kvj = kv0 + j * 16 + 4 * g + r;
-                        if (kvj >= p.Tk || !qok[u] || (CAUSAL && kvj > qgl[u] + off)) dsv[u][j][r] = 0.f;
-                    }
         }
         // dQ^T[d][q] += K^T[d][kv] dS^T[kv][q]
 #pragma unroll
