@@ -997,9 +997,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             }
 #pragma unroll
             for (int u = 0; u < QG; ++u) {
-                // without dropout the dP accumulator starts at −δ: dS = P ⊙ (dP − δ) is one multiply
-                const float d0 = DROP ? 0.f : -dl[u];
-                f32x4 sa = {0, 0, 0, 0}, da = {d0, d0, d0, d0};
+                f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
 #pragma unroll
                 for (int s = 0; s < NS; ++s) sa = MFMA(kr[s], qf[u][s], sa, 0, 0, 0);
 #pragma unroll
@@ -1007,23 +1005,31 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int kvj = kv0 + j * 16 + 4 * g + r;
-                    float x = __builtin_fmaf(sa[r], sl2, -lse2[u]);
+                    float x = sa[r] * sl2;
                     if constexpr (BIAS) {
                         if (qok[u] && kvj < p.Tk)
                             x += p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qgl[u]) * p.Tk + kvj] * LOG2E;
                     }
-                    // masked scores: exponent −inf, so dS = 0 (rows past Tq: lse = +inf does the same)
-                    if constexpr (MASKED)
-                        if (kvj >= p.Tk || (CAUSAL && kvj > qgl[u] + off)) x = -INFINITY;
-                    float pv = __builtin_amdgcn_exp2f(x);
+                    float pv = __builtin_amdgcn_exp2f(x - lse2[u]);
                     float dpv = da[r];
                     if constexpr (DROP) {
                         const bool keep = hash_uniform(p.seed, drop_idx(p, b, h, qgl[u], kvj)) >= p.p_drop;
                         dpv = keep ? dpv * rd : 0.f;
                     }
-                    dsv[u][j][r] = DROP ? pv * (dpv - dl[u]) : pv * dpv;
+                    dsv[u][j][r] = pv * (dpv - dl[u]);  // (a −δ accumulator start here costs occupancy 3 → 2)
                 }
             }
+        }
+        if constexpr (MASKED) {  // (the dK/dV kernel's −inf-exponent form costs this kernel occupancy 3 → 2)
+#pragma unroll
+            for (int u = 0; u < QG; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int kvj = kv0 + j * 16 + 4 * g + r;
+                        if (kvj >= p.Tk || !qok[u] || (CAUSAL && kvj > qgl[u] + off)) dsv[u][j][r] = 0.f;
+                    }
         }
         // dQ^T[d][q] += K^T[d][kv] dS^T[kv][q]
 #pragma unroll
