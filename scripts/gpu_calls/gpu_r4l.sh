@@ -5,6 +5,9 @@
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 fault() { grep -q "illegal memory access\|hipErrorIllegalAddress\|HSA_STATUS_ERROR\|Memory access fault" "$1"; }
 PT="python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 300 $PT tests/test_ops_gpu.py tests/test_determinism_gpu.py -k "attention or attn or determin" > gpurun_out/l_attn.log 2>&1; rc=$?
+echo "=== l_attn rc=$rc $(grep -E 'passed|failed' gpurun_out/l_attn.log | tail -1)"; grep -E "FAILED" gpurun_out/l_attn.log | head
+fault gpurun_out/l_attn.log && exit 2
 timeout -k 10 300 $PT tests/test_convergence_gpu.py tests/test_resnet_join_gpu.py -k "resnet or join or block" > gpurun_out/l_tests.log 2>&1; rc=$?
 echo "=== l_tests rc=$rc $(grep -E 'passed|failed' gpurun_out/l_tests.log | tail -1)"; grep -E "FAILED" gpurun_out/l_tests.log | head
 fault gpurun_out/l_tests.log && exit 2
