@@ -771,6 +771,16 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
         const char* ot_ = Ot(cur);
         const float* lt_ = reinterpret_cast<const float*>(Lt(cur));
         const float* dt_ = reinterpret_cast<const float*>(Dt(cur));
+        // masked tiles: a (key group u, 16-query fragment qi) block of this wave with no visible
+        // (key, query) pair — past Tk / Tq, or wholly above the causal diagonal — skips its MFMAs and
+        // VALU (wave-uniform; P = dS = 0 there).  The diagonal's upper blocks and the ragged tail of a
+        // T = 197 sequence (ViT) are most of such a tile.
+        auto live = [&](int u, int qi) -> bool {
+            if constexpr (!MASKED) return true;
+            const int k0 = kvw + 64 * u, qa = q0 + qi * 16;
+            if (k0 >= p.Tk || qa >= p.Tq) return false;
+            return !(CAUSAL && k0 > min(qa + 15, p.Tq - 1) + off);
+        };
         f32x4 pq[KG][4], dsq[KG][4];
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
@@ -788,6 +798,11 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
             const float ls[4] = {l4.x, l4.y, l4.z, l4.w}, nd[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int u = 0; u < KG; ++u) {
+                if (MASKED && !live(u, qi)) {
+                    pq[u][qi] = (f32x4){0, 0, 0, 0};
+                    dsq[u][qi] = (f32x4){0, 0, 0, 0};
+                    continue;
+                }
                 f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
                 if constexpr (!DROP) da = (f32x4){nd[0], nd[1], nd[2], nd[3]};
 #pragma unroll
@@ -821,6 +836,12 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
         // dV^T[d][kv] += dO^T[d][q] Pd[q][kv];  dK^T[d][kv] += Q^T[d][q] dS[q][kv]
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
+            if constexpr (MASKED) {  // both 16-query fragments of this k-step dead for every key group
+                bool any = false;
+#pragma unroll
+                for (int u = 0; u < KG; ++u) any = any || live(u, 2 * ks) || live(u, 2 * ks + 1);
+                if (!any) continue;
+            }
             s16x8 pb[KG], sb[KG];
 #pragma unroll
             for (int u = 0; u < KG; ++u) {
@@ -986,6 +1007,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         const int kv0 = t * 64;
         const char* kt = Kt(cur);
         const char* vt = Vt(cur);
+        // masked tiles: a (query group u, 16-key block j) of this wave with no visible pair skips
+        // its MFMAs and VALU (wave-uniform; dS = 0 there), as in the dK/dV kernel
+        auto live = [&](int u, int j) -> bool {
+            if constexpr (!MASKED) return true;
+            const int qa = qb * QB + 64 * u + wave * 16, k0 = kv0 + 16 * j;
+            if (qa >= p.Tq || k0 >= p.Tk) return false;
+            return !(CAUSAL && k0 > min(qa + 15, p.Tq - 1) + off);
+        };
         f32x4 dsv[QG][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -997,6 +1026,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             }
 #pragma unroll
             for (int u = 0; u < QG; ++u) {
+                if (MASKED && !live(u, j)) {
+                    dsv[u][j] = (f32x4){0, 0, 0, 0};
+                    continue;
+                }
                 f32x4 sa = {0, 0, 0, 0}, da = {0, 0, 0, 0};
 #pragma unroll
                 for (int s = 0; s < NS; ++s) sa = MFMA(kr[s], qf[u][s], sa, 0, 0, 0);
@@ -1034,6 +1067,12 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
         // dQ^T[d][q] += K^T[d][kv] dS^T[kv][q]
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
+            if constexpr (MASKED) {  // both 16-key blocks of this k-step dead for every query group
+                bool any = false;
+#pragma unroll
+                for (int u = 0; u < QG; ++u) any = any || live(u, 2 * ks) || live(u, 2 * ks + 1);
+                if (!any) continue;
+            }
             s16x8 sb[QG];
 #pragma unroll
             for (int u = 0; u < QG; ++u) sb[u] = pack_p(dsv[u][2 * ks], dsv[u][2 * ks + 1]);
