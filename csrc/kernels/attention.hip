@@ -541,19 +541,42 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         s16x8 ka[4][2];
         [[maybe_unused]] bool moved = false;
         [[maybe_unused]] float alph[QI];
+        // masked tiles: a (16-query fragment qi, 16-key block j) of this wave with no visible pair —
+        // past Tq / Tk (the ragged tail of a T = 197 sequence) or wholly above the causal diagonal —
+        // skips its QKᵀ and P·V MFMAs (wave-uniform; its scores are −inf, so P = 0 there)
+        auto live = [&](int qi, int j) -> bool {
+            if constexpr (!MASKED) return true;
+            const int qa = q0 + qi * 16, k0 = kv0 + j * 16;
+            if (qa >= p.Tq || k0 >= p.Tk) return false;
+            return !(CAUSAL && k0 > min(qa + 15, p.Tq - 1) + off);
+        };
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             ka[j][0] = rowfragx(kt, j, 0, fo);
             ka[j][1] = rowfragx(kt, j, 1, fo);
         }
+        if constexpr (MASKED) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
+                for (int qi = 0; qi < QI; ++qi) {
+                    if (live(qi, j)) {
+                        sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
+                        sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
+                    } else {
+                        sacc[qi][j] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                    }
+                }
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
+                for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][0], qf[qi][0], ((f32x4){0.f, 0.f, 0.f, 0.f}), 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int qi = 0; qi < QI; ++qi) sacc[qi][j] = MFMA(ka[j][1], qf[qi][1], sacc[qi][j], 0, 0, 0);
+        }
         // V^T fragments for the PV product, in flight during the softmax
         s16x8 va[2][4];
 #pragma unroll
@@ -628,13 +651,23 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
             s16x8 pb[QI];
 #pragma unroll
             for (int qi = 0; qi < QI; ++qi) pb[qi] = pack_p(sacc[qi][2 * s], sacc[qi][2 * s + 1]);
+            if constexpr (MASKED) {  // skip (qi, k-step) pairs whose 32 keys are all dead for qi
 #pragma unroll
-            for (int jd = 0; jd < 4; ++jd)
+                for (int qi = 0; qi < QI; ++qi) {
+                    if (!(live(qi, 2 * s) || live(qi, 2 * s + 1))) continue;
 #pragma unroll
-                for (int qi = 0; qi < QI; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
-            if constexpr (LEAN) {
+                    for (int jd = 0; jd < 4; ++jd) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
+                    if constexpr (LEAN) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
+                }
+            } else {
 #pragma unroll
-                for (int qi = 0; qi < QI; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
+                for (int jd = 0; jd < 4; ++jd)
+#pragma unroll
+                    for (int qi = 0; qi < QI; ++qi) oacc[qi][jd] = MFMA(va[s][jd], pb[qi], oacc[qi][jd], 0, 0, 0);
+                if constexpr (LEAN) {
+#pragma unroll
+                    for (int qi = 0; qi < QI; ++qi) lsum[qi] = MFMA(ones, pb[qi], lsum[qi], 0, 0, 0);
+                }
             }
         }
         if constexpr (LEAN) {
