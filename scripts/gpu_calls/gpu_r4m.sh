@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 (call M): attention backward skips dead (group, 16-row block) pieces of masked tiles (causal
+# round 4 (call M): attention forward + backward skip dead (group, 16-row block) pieces of masked tiles (causal
 # diagonal upper blocks, ragged tails): fp32-reference + determinism tests, then A/B against the previous
 # library (ab/_C_prev.so) at GPT-2-small (causal T = 1024) and ViT-B/16 (T = 197) shapes and on both steps.
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -14,7 +14,7 @@ for r in 1 2 3; do
     lib $l
     timeout -k 10 120 python scripts/attn_ab.py 64 --rounds 3 > gpurun_out/m_gpt_${l}_$r.log 2>&1 || { echo "attn_ab failed"; exit 1; }
     timeout -k 10 120 python scripts/attn_ab.py 512 --T 197 --noncausal --rounds 3 > gpurun_out/m_vit_${l}_$r.log 2>&1 || { echo "attn_ab vit failed"; exit 1; }
-    echo "$l r$r gpt: $(grep -o '"op": "attn_bwd".*"tflops": [0-9.]*' gpurun_out/m_gpt_${l}_$r.log | sed 's/, "B".*"ms"/ ms/')  vit: $(grep -o '"op": "[a-z_]*".*"tflops": [0-9.]*' gpurun_out/m_vit_${l}_$r.log | sed 's/, "B".*"ms"/ ms/' | tr '\n' ' ')"
+    echo "$l r$r gpt: $(grep -o '"op": "[a-z_]*".*"tflops": [0-9.]*' gpurun_out/m_gpt_${l}_$r.log | sed 's/, "B".*"ms"/ ms/' | tr '\n' ' ')  vit: $(grep -o '"op": "[a-z_]*".*"tflops": [0-9.]*' gpurun_out/m_vit_${l}_$r.log | sed 's/, "B".*"ms"/ ms/' | tr '\n' ' ')"
   done
 done
 unset REPLICANN_SO
