@@ -23,10 +23,13 @@ from .linear import _act_ref, _pre_ref
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
 # fp8 weight gradients (dW = dYᵀ·X with dY in e5m2, X the forward's e4m3 copy) of the fp8 layers:
-# REPLICANN_FP8_WGRAD=1 (or Fp8State.wgrad); off by default until measured on the GPU
+# REPLICANN_FP8_WGRAD=1 (or Fp8State.wgrad).  Opt-in: measured on the MI355X without a step gain
+# (GPT-2-medium 1.03x the bf16 model with or without it; per-shape fp8 wgrad 0.57-0.99x bf16 —
+# profiles/fp8_bwd_r4g.txt), and the loss trajectory moves 2.0 % from bf16 against 1.8 % without
 FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "0") == "1"
 # fp8 data gradients (dX = dY·W with the same e5m2 dY and the forward's e4m3 weight) of the fp8
-# layers whose dgrad has a plain epilogue: REPLICANN_FP8_DGRAD=1 (or Fp8State.dgrad)
+# layers whose dgrad has a plain epilogue: REPLICANN_FP8_DGRAD=1 (or Fp8State.dgrad); opt-in for the
+# same reason (per shape 0.79-1.19x bf16, step +1 % with both on)
 FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "0") == "1"
 
 
