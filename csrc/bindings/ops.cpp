@@ -45,6 +45,8 @@ void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_
 void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int, hipStream_t);
 void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
 void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, int, hipStream_t);
+void rn_vit_join_fwd(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
+void rn_vit_join_bwd(const void*, void*, void*, void*, int, int, int, hipStream_t);
 void rn_emb_bwd_acc(const int64_t*, const void*, float*, unsigned*, void*, void*, int, int, int, int, hipStream_t);
 void rn_emb_bwd_acc_det(const int64_t*, const void*, void*, unsigned*, void*, void*, int, int, int, int, hipStream_t);
 void rn_emb_bwd(const int64_t*, const void*, float*, void*, void*, int, int, int, int, int, hipStream_t);
@@ -536,6 +538,29 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optiona
 }
 
 // ------------------------------------------------------------------ embedding
+// ViT token join: x[b] = concat(cls, patch[b]) + pos — patch (B, P, E), cls (E), pos (P + 1, E), all bf16
+Tensor vit_join_fwd(const Tensor& patch, const Tensor& cls, const Tensor& pos) {
+    CHECK_BF16(patch); CHECK_CONTIG(patch); CHECK_BF16(cls); CHECK_CONTIG(cls); CHECK_BF16(pos); CHECK_CONTIG(pos);
+    GUARD(patch);
+    TORCH_CHECK(patch.dim() == 3, "vit_join_fwd: patch must be (B, P, E)");
+    const int B = patch.size(0), P = patch.size(1), E = patch.size(2);
+    TORCH_CHECK(E % 8 == 0 && cls.numel() == E && pos.numel() == (long)(P + 1) * E, "vit_join_fwd: shapes");
+    Tensor out = at::empty({B, P + 1, E}, patch.options());
+    if (B) rn_vit_join_fwd(patch.data_ptr(), cls.data_ptr(), pos.data_ptr(), out.data_ptr(), B, P, E, cur_stream());
+    return out;
+}
+// backward: returns dpatch (B, P, E); gcls (E) and gpos (P + 1, E) are ACCUMULATED into (bf16)
+Tensor vit_join_bwd(const Tensor& dx, const Tensor& gcls, const Tensor& gpos) {
+    CHECK_BF16(dx); CHECK_CONTIG(dx); CHECK_BF16(gcls); CHECK_CONTIG(gcls); CHECK_BF16(gpos); CHECK_CONTIG(gpos);
+    GUARD(dx);
+    TORCH_CHECK(dx.dim() == 3, "vit_join_bwd: dx must be (B, P + 1, E)");
+    const int B = dx.size(0), P = dx.size(1) - 1, E = dx.size(2);
+    TORCH_CHECK(P >= 0 && E % 8 == 0 && gcls.numel() == E && gpos.numel() == (long)(P + 1) * E, "vit_join_bwd: shapes");
+    Tensor dpatch = at::empty({B, P, E}, dx.options());
+    if (B) rn_vit_join_bwd(dx.data_ptr(), dpatch.data_ptr(), gcls.data_ptr(), gpos.data_ptr(), B, P, E, cur_stream());
+    return dpatch;
+}
+
 Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const optional<Tensor>& wpe) {
     CHECK_BF16(wte); CHECK_CONTIG(wte); GUARD(wte);
     TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous());
@@ -1082,6 +1107,8 @@ TORCH_LIBRARY(replicann, m) {
     m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd, "
           "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None, Tensor(c!)? dxs_accum=None) -> (Tensor, Tensor, Tensor)");
     m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
+    m.def("vit_join_fwd(Tensor patch, Tensor cls, Tensor pos) -> Tensor");
+    m.def("vit_join_bwd(Tensor dx, Tensor(a!) gcls, Tensor(b!) gpos) -> Tensor");
     m.def("embedding_bwd(Tensor dx, Tensor ids, int V, int Tp) -> (Tensor, Tensor)");
     m.def("embedding_bwd_acc(Tensor dx, Tensor ids, Tensor(a!) gwte, Tensor(b!)? gwpe) -> ()");
     m.def("sumsq(Tensor g, Tensor(a!) normbuf) -> ()");
@@ -1152,6 +1179,8 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("layernorm_fwd_q8", &layernorm_fwd_q8);
     m.impl("layernorm_bwd", &layernorm_bwd);
     m.impl("embedding_fwd", &embedding_fwd);
+    m.impl("vit_join_fwd", &vit_join_fwd);
+    m.impl("vit_join_bwd", &vit_join_bwd);
     m.impl("embedding_bwd", &embedding_bwd);
     m.impl("embedding_bwd_acc", &embedding_bwd_acc);
     m.impl("sumsq", &sumsq);

@@ -357,6 +357,70 @@ void rn_emb_bwd_acc(const int64_t* ids, const void* dx, float* d32, unsigned* ow
     if (gwpe) emb_pos_acc_k<<<rn_cdiv((long)T * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)gwpe, B, T, E);
 }
 
+// ---- ViT token join: x[b, 0] = cls + pos[0], x[b, 1 + p] = patch[b, p] + pos[1 + p] ----
+// (replaces torch.cat + broadcast add in the forward and the slice copy + two batch reductions of
+// their backward: one pass each way)
+__global__ void __launch_bounds__(256) vit_join_fwd_k(const bf16* __restrict__ patch, const bf16* __restrict__ cls,
+                                                      const bf16* __restrict__ pos, bf16* __restrict__ out, int B, int P,
+                                                      int E) {
+    const long i = blockIdx.x * 256L + threadIdx.x;  // one 8-element chunk
+    const int e8 = E / 8;
+    if (i >= (long)B * (P + 1) * e8) return;
+    const int c = (int)(i % e8);
+    const long bt = i / e8;
+    const int t = (int)(bt % (P + 1));
+    const long b = bt / (P + 1);
+    float x[8], q[8];
+    load8((t == 0 ? cls : patch + (b * P + t - 1) * E) + c * 8, x);
+    load8(pos + (long)t * E + c * 8, q);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += q[j];
+    store8(out + bt * E + c * 8, x);
+}
+
+// backward: dpatch[b, p] = dx[b, 1 + p]; gpos[t] += Σ_b dx[b, t]; gcls += Σ_b dx[b, 0].
+// grid (P + 1, ceil(E / 256)); 256 threads = 32 column chunks of 8 × 8 batch lanes, one LDS merge
+// of the 8 lane partials (fixed order: deterministic).
+__global__ void __launch_bounds__(256) vit_join_bwd_k(const bf16* __restrict__ dx, bf16* __restrict__ dpatch,
+                                                      bf16* __restrict__ gcls, bf16* __restrict__ gpos, int B, int P,
+                                                      int E) {
+    __shared__ float part[8][32 * 8];
+    const int t = blockIdx.x, cg = threadIdx.x & 31, bl = threadIdx.x >> 5;
+    const int col = (blockIdx.y * 32 + cg) * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (col < E) {
+        for (int b = bl; b < B; b += 8) {
+            float v[8];
+            load8(dx + ((long)b * (P + 1) + t) * E + col, v);
+            if (t > 0) store8(dpatch + ((long)b * P + t - 1) * E + col, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += v[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[bl][cg * 8 + j] = acc[j];
+    __syncthreads();
+    if (bl == 0 && col < E) {
+        float s[8], g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            s[j] = 0.f;
+#pragma unroll
+            for (int l = 0; l < 8; ++l) s[j] += part[l][cg * 8 + j];
+        }
+        load8(gpos + (long)t * E + col, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] += s[j];
+        store8(gpos + (long)t * E + col, g);
+        if (t == 0) {
+            load8(gcls + col, g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] += s[j];
+            store8(gcls + col, g);
+        }
+    }
+}
+
 // deterministic variant: d64 = persistent zeroed V×E 64-bit scratch
 void rn_emb_bwd_acc_det(const int64_t* ids, const void* dx, void* d64, unsigned* owner, void* gwte, void* gwpe, int B,
                         int T, int E, int V, hipStream_t st) {
@@ -365,6 +429,16 @@ void rn_emb_bwd_acc_det(const int64_t* ids, const void* dx, void* d64, unsigned*
                                                         E, V);
     emb_finish_fx_k<<<(rows + 3) / 4, 256, 0, st>>>(ids, (unsigned long long*)d64, owner, (bf16*)gwte, rows, E);
     if (gwpe) emb_pos_acc_k<<<rn_cdiv((long)T * E, 256), 256, 0, st>>>((const bf16*)dx, (bf16*)gwpe, B, T, E);
+}
+
+void rn_vit_join_fwd(const void* patch, const void* cls, const void* pos, void* out, int B, int P, int E, hipStream_t st) {
+    const long n = (long)B * (P + 1) * (E / 8);
+    vit_join_fwd_k<<<rn_cdiv(n, 256), 256, 0, st>>>((const bf16*)patch, (const bf16*)cls, (const bf16*)pos, (bf16*)out, B,
+                                                    P, E);
+}
+void rn_vit_join_bwd(const void* dx, void* dpatch, void* gcls, void* gpos, int B, int P, int E, hipStream_t st) {
+    dim3 grid(P + 1, (E + 255) / 256);
+    vit_join_bwd_k<<<grid, 256, 0, st>>>((const bf16*)dx, (bf16*)dpatch, (bf16*)gcls, (bf16*)gpos, B, P, E);
 }
 
 int rn_norm_ws_floats() { return NORM_BLOCKS; }

@@ -66,8 +66,7 @@ class ViT(nn.Module):
         c = self.config
         B = images.shape[0]
         x = ops.conv2d_nhwc(images, self.patch_weight, self.patch_bias, stride=c.patch)
-        x = x.reshape(B, -1, c.n_embd)
-        x = torch.cat([self.cls_token.expand(B, -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype)
+        x = ops.vit_join(x.reshape(B, -1, c.n_embd), self.cls_token, self.pos_embed)  # [cls; patches] + pos
         prev = None
         for blk in self.blocks:
             x = blk(x, prev)

@@ -55,3 +55,37 @@ def embedding(ids, wte, wpe=None):
     if wpe is not None:
         x = x + wpe[: ids.shape[-1]]
     return x
+
+
+class _VitJoinFn(torch.autograd.Function):
+    """x = concat(cls, patches) + pos in one kernel; the backward returns the patch gradient and
+    accumulates the cls / pos gradients straight into their flat-buffer views (or fresh zeros)."""
+
+    @staticmethod
+    def forward(ctx, patches, cls, pos):
+        ctx.cls_ref, ctx.pos_ref = cls, pos
+        return _ext.ops().vit_join_fwd(patches.contiguous(), cls, pos)
+
+    @staticmethod
+    def backward(ctx, gx):
+        from .linear import _direct_grad, _notify
+        cls, pos = ctx.cls_ref, ctx.pos_ref
+        gc, gp = _direct_grad(cls), _direct_grad(pos)
+        direct = gc is not None and gp is not None
+        if not direct:
+            gc, gp = torch.zeros_like(cls), torch.zeros_like(pos)
+        dpatch = _ext.ops().vit_join_bwd(gx.contiguous(), gc, gp)
+        if direct:
+            _notify(cls)
+            _notify(pos)
+            return dpatch, None, None
+        return dpatch, gc, gp
+
+
+def vit_join(patches, cls, pos):
+    """ViT token sequence: (B, P, E) patch embeddings → (B, 1 + P, E) = [cls; patches] + pos, with
+    ``cls`` (1, 1, E) and ``pos`` (1, 1 + P, E) parameters.  GPU: one fused kernel each way."""
+    if _ext.use_native(patches) and patches.dtype == torch.bfloat16 and cls.dtype == torch.bfloat16:
+        return _VitJoinFn.apply(patches, cls, pos)
+    B = patches.shape[0]
+    return torch.cat([cls.expand(B, -1, -1).to(patches.dtype), patches], dim=1) + pos.to(patches.dtype)

@@ -508,6 +508,31 @@ def test_softmax_act_dropout(cuda):
     assert abs(keep - 0.75) < 0.01 and abs(d.float().mean().item() - 1.0) < 0.02
 
 
+@pytest.mark.parametrize("flat", [False, True])
+def test_vit_join(cuda, flat):
+    """ViT token join ([cls; patches] + pos, fused kernel both ways) against the fp32 reference, with
+    the cls / pos gradients returned (autograd) or accumulated into the flat-buffer views."""
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(21)
+    B, P, E = 5, 196, 768
+    mod = torch.nn.Module()
+    mod.cls = torch.nn.Parameter(bf(1, 1, E))
+    mod.pos = torch.nn.Parameter(bf(1, P + 1, E))
+    if flat:
+        fp = FlatParams(mod)
+        fp.zero_grad()
+    patches = bf(B, P, E).requires_grad_()
+    x = ops.vit_join(patches, mod.cls, mod.pos)
+    g = bf(B, P + 1, E)
+    x.backward(g)
+    pf, cf, qf = [t.detach().float().requires_grad_() for t in (patches, mod.cls, mod.pos)]
+    xr = torch.cat([cf.expand(B, -1, -1), pf], dim=1) + qf
+    xr.backward(g.float())
+    assert rel_err(x, xr) < 1e-2
+    assert torch.equal(patches.grad, g[:, 1:])  # a copy: exact
+    assert rel_err(mod.cls.grad, cf.grad) < 1e-2 and rel_err(mod.pos.grad, qf.grad) < 1e-2
+
+
 def test_embedding(cuda):
     torch.manual_seed(13)
     V, E, B, T = 500, 128, 3, 40
