@@ -684,14 +684,18 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd64v2_k(AttnArgs p) {
         }
     };
     // (not unrolled by buffer like the backward kernels: at occupancy 3 the unrolled loop spills)
+    // A wave whose queries all lie past Tq (the padded rows of a T = 197 sequence's last block) skips
+    // every tile's work; it still joins every tile's barrier and DMA issue.
+    const int nf = q0 < p.Tq ? nfull : 0;  // wave-uniform trip count
     int t = 0;
-    for (; t < nfull; ++t) {
+    for (; t < nf; ++t) {
         sync_prefetch(t);
         tile(t, std::false_type{});
     }
     for (; t < nkv; ++t) {
         sync_prefetch(t);
         if (CAUSAL && t * 64 > q0 + QW - 1 + off) continue;  // wave-uniform: every query of this wave precedes the tile
+        if (q0 >= p.Tq) continue;                            // wave-uniform: no live query in this wave
         tile(t, std::true_type{});
     }
 #undef Kt
