@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 fault() { grep -q "illegal memory access\|hipErrorIllegalAddress\|HSA_STATUS_ERROR\|Memory access fault" "$1"; }
 # first: the fused ViT token join (new kernels) against fp32, and the ViT models on the GPU
-timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_ops_gpu.py tests/test_convergence_gpu.py tests/test_models.py -k "vit or embedding" > gpurun_out/n_tests.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_ops_gpu.py tests/test_convergence_gpu.py tests/test_models.py -k "vit or embedding or attention" > gpurun_out/n_tests.log 2>&1; rc=$?
 echo "=== n_tests rc=$rc $(grep -E 'passed|failed' gpurun_out/n_tests.log | tail -1)"; grep -E "FAILED" gpurun_out/n_tests.log | head
 fault gpurun_out/n_tests.log && exit 2; [ $rc -ne 0 ] && exit 1
 timeout -k 10 1000 bash scripts/pmc_step.sh "--steps 2 --warmup 1" gpt2s > gpurun_out/n_pmc.log 2>&1 || { echo "pmc failed"; tail -5 gpurun_out/n_pmc.log; exit 1; }
