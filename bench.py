@@ -66,6 +66,8 @@ def parse_args(argv=None):
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="capture the whole training step as one hipGraph (auto: on for 1 process)")
     ap.add_argument("--device", default=None, help="cpu: run the same harness on the CPU/gloo path (tests)")
+    ap.add_argument("--ce-chunk", type=int, default=0,
+                    help="GPT-2: LM head + loss over token chunks of this size (0: whole batch)")
     return ap.parse_args(argv)
 
 
@@ -134,7 +136,8 @@ def main(argv=None):
                       weight_decay=0.1 if not args.model.startswith("resnet") else 5e-5,
                       warmup_steps=10, lr=3e-4 if args.model.startswith("gpt2-medium") else 6e-4, bucket_mb=args.bucket_mb,
                       reduce_dtype=args.reduce_dtype, ddp_schedule=args.ddp_schedule, log_every=10**9,
-                      graph=args.graph, ddp=args.ddp, comm=args.comm, device=args.device)
+                      graph=args.graph, ddp=args.ddp, comm=args.comm, device=args.device,
+                      model_kwargs={"ce_chunk": args.ce_chunk} if (is_lm and args.ce_chunk) else {})
     tr = Trainer(cfg)
     world = tr.world
     dev = tr.device
@@ -220,6 +223,8 @@ def main(argv=None):
             "gemm_cu_reserve": (int(torch.ops.replicann.gemm_get_reserve())
                                 if dev.type == "cuda" and hasattr(torch.ops.replicann, "gemm_get_reserve") else None),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
+            **({"ce_chunk_rows": args.ce_chunk} if (is_lm and args.ce_chunk) else {}),
+            "peak_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if dev.type == "cuda" else None),
         },
     }
     if tr.rank == 0:

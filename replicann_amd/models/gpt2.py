@@ -41,6 +41,9 @@ class GPT2Config:
     # (profiles/fp8_gemm_ab_r2r.txt).  c_attn / c_fc take e4m3 straight from the LayerNorm kernel,
     # the MLP c_proj from c_fc's GEMM epilogue
     fp8_proj: bool = False
+    # LM head + loss over row chunks of this many tokens (0: the whole batch at once).  Bounds the
+    # logits buffer (rows x vocab_pad bf16: 6.6 GB at b64 x 1024) for long sequences / big batches
+    ce_chunk: int = 0
 
     @staticmethod
     def small(**kw):
@@ -103,7 +106,8 @@ class GPT2(nn.Module):
         h = self.hidden(idx)
         if targets is None:
             return ops.linear(h, self.wte)[..., : self.config.vocab_size]
-        return ops.linear_cross_entropy(h, self.wte, targets, n_valid_cols=self.config.vocab_size)
+        return ops.linear_cross_entropy(h, self.wte, targets, n_valid_cols=self.config.vocab_size,
+                                        chunk_rows=self.config.ce_chunk)
 
     def flops_per_token(self, T=None):
         """Training FLOPs per token (fwd+bwd): 6·N_matmul + attention (causal)."""

@@ -92,10 +92,81 @@ class _LinearXentFn(torch.autograd.Function):
         return gh, gw, None, None, None
 
 
-def linear_cross_entropy(h, weight, target, *, n_valid_cols=None, ignore_index=-100):
-    """mean CE(h·weightᵀ, target) without materialising a separate logits gradient."""
+class _ChunkedLinearXentFn(torch.autograd.Function):
+    """LM head + cross-entropy over row chunks: peak logits memory rows·V → chunk·V.
+
+    The loss's gradients are formed DURING the forward, one chunk at a time, while that
+    chunk's logits are live: logits_c = h_c·Wᵀ → CE writes (softmax − onehot) in place →
+    dh_c = that·W / n (straight into dh's rows) and dW += thatᵀ·h_c / n (fp32, accumulated
+    by the GEMM epilogue).  One logits buffer of ``chunk`` rows is reused by every chunk.
+    The backward only scales the two stored gradients by the incoming g.
+
+    Cost (GPT-2-small b64, 65,536 rows, V = 50,304): the unchunked path holds a 6.6 GB bf16
+    logits tensor; chunks of 16,384 rows hold 1.65 GB plus dh (bf16, 100 MB) and dW (fp32,
+    154 MB).  The GEMM FLOPs are the same; the smaller-M dgrad shapes need split-K to fill
+    256 CUs (the runtime autotuner picks it).  Measured cost in ``profiles/lmhead_chunk_*``.
+    Default off (``GPT2Config.ce_chunk = 0``): on a 288 GB device the whole-batch logits fit,
+    and the chunked form pays the split-K reduction and the backward scaling passes."""
+
+    @staticmethod
+    def forward(ctx, h, weight, target, n_valid_cols, ignore_index, chunk):
+        ops = _ext.ops()
+        shp = h.shape
+        h2 = h.reshape(-1, shp[-1]).contiguous()
+        tg = target.reshape(-1).long().contiguous()
+        M, V = h2.shape[0], weight.shape[0]
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        want = need_h or need_w
+        n = (tg != ignore_index).sum().clamp_min(1).float()
+        inv_n = (1.0 / n).reshape(1)
+        gh = torch.empty_like(h2) if need_h else None
+        gw = torch.zeros(weight.shape, dtype=torch.float32, device=h2.device) if need_w else None
+        buf = torch.empty(min(chunk, M), V, dtype=h2.dtype, device=h2.device)
+        loss = torch.zeros((), dtype=torch.float32, device=h2.device)
+        for r0 in range(0, M, chunk):
+            r1 = min(M, r0 + chunk)
+            hc, lg = h2[r0:r1], buf[: r1 - r0]
+            ops.gemm(hc, weight, False, True, None, None, 0, None, lg, False, 0, False, None, -1)
+            rows, _ = ops.xent_fwd(lg, tg[r0:r1], n_valid_cols, ignore_index, want)
+            loss += rows.sum()
+            if need_h:
+                ops.gemm(lg, weight, False, False, None, None, 0, None, gh[r0:r1], False, -1, False, inv_n, -1)
+            if need_w:
+                ops.gemm(lg, hc, True, False, None, None, 0, None, gw, True, -1, False, inv_n, -1)
+        del buf
+        ctx.save_for_backward(weight, gh, gw)
+        ctx.shp = shp
+        return loss / n
+
+    @staticmethod
+    def backward(ctx, g):
+        from .linear import _direct_grad, _notify
+        weight, gh, gw = ctx.saved_tensors
+        g = g.float()
+        out_h = out_w = None
+        if ctx.needs_input_grad[0]:
+            out_h = (gh * g).reshape(ctx.shp)  # bf16 result, fp32 arithmetic
+        if ctx.needs_input_grad[1]:
+            gw = gw * g
+            acc = _direct_grad(weight)
+            if acc is not None:
+                acc.add_(gw)
+                _notify(weight)
+            else:
+                out_w = gw.to(weight.dtype)
+        return out_h, out_w, None, None, None, None
+
+
+def linear_cross_entropy(h, weight, target, *, n_valid_cols=None, ignore_index=-100, chunk_rows=0):
+    """mean CE(h·weightᵀ, target) without materialising a separate logits gradient.
+
+    ``chunk_rows`` > 0 (GPU): the LM head and the loss run over row chunks of that size, so
+    the logits never exist for more than ``chunk_rows`` rows at once (``_ChunkedLinearXentFn``)."""
     nv = weight.shape[0] if n_valid_cols is None else n_valid_cols
     if _ext.use_native(h):
+        rows = h.numel() // h.shape[-1]
+        if chunk_rows and chunk_rows < rows:
+            return _ChunkedLinearXentFn.apply(h, weight, target, nv, ignore_index, int(chunk_rows))
         return _LinearXentFn.apply(h, weight, target, nv, ignore_index)
     logits = F.linear(h, weight)
     return F.cross_entropy(logits.reshape(-1, logits.shape[-1])[:, :nv].float(), target.reshape(-1),

@@ -315,11 +315,39 @@ def test_cross_entropy_padded(cuda):
     assert lg.grad[:, nv:].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("kern", ["2", "1"])
-def test_fused_lm_xent_rows_gpt2_vocab(cuda, monkeypatch, kern):
-    """The in-place gradient row kernels at GPT-2's padded vocab (50304 columns, 50257 valid):
-    v2 (one block reduction, one exp per element; default) and the round-1 kernel (=1)."""
-    monkeypatch.setenv("REPLICANN_XENT", kern)
+@pytest.mark.parametrize("chunk", [256, 384])
+def test_linear_cross_entropy_chunked(cuda, chunk):
+    """LM head + CE over row chunks (gradients formed in the forward, scaled by g in the
+    backward) vs the whole-batch fused path and fp32 math; a partial last chunk (1000 rows,
+    384-row chunks), ignore_index rows and a non-unit upstream gradient."""
+    torch.manual_seed(11)
+    R, E, V, nv = 1000, 128, 2048, 2000
+    h = bf(R, E)
+    w = bf(V, E, scale=0.5)
+    w[nv:] = 0
+    t = torch.randint(0, nv, (R,), device="cuda")
+    t[::37] = -100
+    outs = []
+    for c in (0, chunk):
+        hh = h.clone().requires_grad_()
+        ww = w.clone().requires_grad_()
+        loss = ops.linear_cross_entropy(hh, ww, t, n_valid_cols=nv, chunk_rows=c)
+        (loss * 0.75).backward()
+        outs.append((loss.detach(), hh.grad.float(), ww.grad.float()))
+    hf = h.float().requires_grad_()
+    wf = w.float().requires_grad_()
+    lref = F.cross_entropy((hf @ wf.t())[:, :nv], t, ignore_index=-100)
+    (lref * 0.75).backward()
+    (l0, gh0, gw0), (l1, gh1, gw1) = outs
+    assert abs(l1.item() - lref.item()) < 1e-2 and abs(l1.item() - l0.item()) < 2e-3
+    assert rel_err(gh1, hf.grad) < 2e-2 and rel_err(gw1, wf.grad) < 2e-2
+    assert rel_err(gh1, gh0) < 1e-2 and rel_err(gw1, gw0) < 1e-2
+    assert gw1[nv:].abs().max().item() == 0
+
+
+def test_fused_lm_xent_rows_gpt2_vocab(cuda):
+    """The in-place gradient row kernel at GPT-2's padded vocab (50304 columns, 50257 valid):
+    one block reduction, one exp per element."""
     torch.manual_seed(8)
     N, V, nv = 96, 50304, 50257
     logits = bf(N, V, scale=4.0)
