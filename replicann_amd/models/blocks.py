@@ -90,9 +90,17 @@ class Attention(nn.Module):
         """Bias whose gradient equals Σ_rows of the block output's gradient (None if dropout intervenes)."""
         return self.c_proj.bias if not (self.resid_dropout > 0 and self.training) else None
 
-    def forward(self, h, residual):
+    def forward(self, h, residual, cache=None, layer=0):
+        """``cache``: a :class:`KVCache` (inference) — this call's keys / values are appended at the
+        cache position and the queries attend to everything cached so far (causal, bottom-right
+        aligned: query i of T new tokens sees keys ≤ pos + i)."""
         B, T, E = h.shape
         qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
+        if cache is not None:
+            q, k, v = qkv.unbind(2)
+            k_all, v_all = cache.update(layer, k, v)
+            a = ops.attention(q, k_all, v_all, causal=self.causal).reshape(B, T, E)
+            return self.c_proj(a, residual=residual)
         a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
                                  training=self.training,
                                  producer_bias=self.c_attn.bias)
@@ -123,6 +131,30 @@ class MLP(nn.Module):
                        residual=residual, fp8=fp8)
 
 
+class KVCache:
+    """Per-layer key / value buffers for incremental decoding, (B, max_len, H, D) each, allocated on
+    first use in the dtype / device of the keys (one HBM allocation per layer for the whole
+    generation; appends are row copies, the attention reads a strided prefix view)."""
+
+    def __init__(self, n_layer, max_len):
+        self.max_len, self.pos = max_len, 0
+        self.kv = [None] * n_layer
+
+    def update(self, layer, k, v):
+        B, T, H, D = k.shape
+        if self.pos + T > self.max_len:
+            raise ValueError(f"KV cache full: {self.pos} + {T} > {self.max_len}")
+        if self.kv[layer] is None:
+            self.kv[layer] = (k.new_empty(B, self.max_len, H, D), v.new_empty(B, self.max_len, H, D))
+        kb, vb = self.kv[layer]
+        kb[:, self.pos: self.pos + T].copy_(k)
+        vb[:, self.pos: self.pos + T].copy_(v)
+        return kb[:, : self.pos + T], vb[:, : self.pos + T]
+
+    def advance(self, T):
+        self.pos += T
+
+
 class PreLNBlock(nn.Module):
     def __init__(self, n_embd, n_head, causal, mlp_ratio=4, dropout=0.0, n_layer=12, eps=1e-5, fp8=False,
                  fp8_proj=True):
@@ -135,12 +167,13 @@ class PreLNBlock(nn.Module):
     def out_bias(self):
         return self.mlp.out_bias()
 
-    def forward(self, x, prev_bias=None):
+    def forward(self, x, prev_bias=None, cache=None, layer=0):
         """``prev_bias``: out_bias() of the block that produced x (its gradient is
-        then reduced inside ln_1's backward kernel)."""
+        then reduced inside ln_1's backward kernel).  ``cache`` / ``layer``: incremental
+        decoding (see :class:`KVCache`)."""
         # fp8 blocks: the LayerNorms also emit the e4m3 input of c_attn / c_fc
         h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias, fp8=self.attn.c_attn.fp8_state)
-        x = self.attn(h, residual=x)
+        x = self.attn(h, residual=x, cache=cache, layer=layer)
         h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias(), fp8=self.mlp.c_fc.fp8_state)
         x = self.mlp(h, residual=x)
         return x

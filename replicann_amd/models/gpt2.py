@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .blocks import LayerNorm, PreLNBlock
+from .blocks import KVCache, LayerNorm, PreLNBlock
 
 
 @dataclass(frozen=True)
@@ -109,6 +109,45 @@ class GPT2(nn.Module):
         return ops.linear_cross_entropy(h, self.wte, targets, n_valid_cols=self.config.vocab_size,
                                         chunk_rows=self.config.ce_chunk)
 
+    @torch.no_grad()
+    def decode_step(self, idx, cache):
+        """Logits (B, vocab) of the LAST position of ``idx`` (B, T) appended at ``cache.pos``:
+        prefill (T = prompt length) and one-token decode steps share this path."""
+        c = self.config
+        T = idx.shape[1]
+        x = ops.embedding(idx, self.wte, self.wpe[cache.pos: cache.pos + T])
+        prev = None
+        for i, blk in enumerate(self.h):
+            x = blk(x, prev, cache=cache, layer=i)
+            prev = blk.out_bias()
+        h = self.ln_f(x, producer_bias=prev)
+        cache.advance(T)
+        return ops.linear(h[:, -1:].contiguous(), self.wte)[:, 0, : c.vocab_size]
+
+    @torch.no_grad()
+    def generate(self, idx, max_new_tokens, *, temperature=1.0, top_k=None, generator=None):
+        """Autoregressive sampling with a KV cache: ``idx`` (B, T0) prompt → (B, T0 + max_new_tokens).
+        ``temperature`` 0 = greedy.  One prefill pass over the prompt, then one-token steps whose
+        attention reads the cached keys / values (no recomputation of the prefix)."""
+        c = self.config
+        B, T0 = idx.shape
+        if T0 + max_new_tokens > c.block_size:
+            raise ValueError(f"prompt {T0} + {max_new_tokens} new tokens exceeds block_size {c.block_size}")
+        was_training = self.training
+        self.eval()
+        try:
+            cache = KVCache(c.n_layer, T0 + max_new_tokens)
+            logits = self.decode_step(idx, cache)
+            out = [idx]
+            for i in range(max_new_tokens):
+                nxt = _sample(logits.float(), temperature, top_k, generator)
+                out.append(nxt)
+                if i + 1 < max_new_tokens:
+                    logits = self.decode_step(nxt, cache)
+            return torch.cat(out, 1)
+        finally:
+            self.train(was_training)
+
     def flops_per_token(self, T=None):
         """Training FLOPs per token (fwd+bwd): 6·N_matmul + attention (causal)."""
         c = self.config
@@ -116,3 +155,15 @@ class GPT2(nn.Module):
         n_mm = c.n_layer * 12 * c.n_embd**2 + c.vocab_size * c.n_embd
         attn = c.n_layer * 2 * 2 * T * c.n_embd * 0.5  # fwd, causal ≈ half
         return 6 * n_mm + 3 * attn
+
+
+def _sample(logits, temperature, top_k, generator):
+    """(B, V) fp32 logits → (B, 1) next-token ids."""
+    if temperature == 0:
+        return logits.argmax(-1, keepdim=True)
+    logits = logits / temperature
+    if top_k is not None and top_k < logits.shape[-1]:
+        kth = torch.topk(logits, top_k, dim=-1).values[:, -1:]
+        logits = logits.masked_fill(logits < kth, float("-inf"))
+    probs = torch.softmax(logits, -1)
+    return torch.multinomial(probs, 1, generator=generator)
