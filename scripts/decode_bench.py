@@ -9,9 +9,13 @@ per batch size: prefill ms, ms per decode step, generated tokens/s over the batc
 
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
