@@ -292,8 +292,12 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
             Tensor scratch_pre = act_fwd_pre ? at::empty({M, N}, a.options()) : Tensor();
             const bool plain = !(bias && bias->defined()) && !(residual && residual->defined()) && act == 0 &&
                                !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
-            const int ncfg = (plain && lib_candidate()) ? 7 : 6;
-            const int cfgs[7] = {9, 1, 6, 0, 2, 8, kLibCfg};
+            // decode-size GEMMs (M <= 64 rows, x·Wᵀ): the skinny config 10 joins the candidates
+            const bool skinny = M <= 64 && !ta && tb && !act_bwd && !accumulate && !want_bg;
+            int cfgs[8] = {9, 1, 6, 0, 2, 8, 0, 0};
+            int ncfg = 6;
+            if (plain && lib_candidate()) cfgs[ncfg++] = kLibCfg;
+            if (skinny) cfgs[ncfg++] = 10;
             // non-powers of two too: the split that makes tiles × split just fill the 256 CUs
             // (e.g. 48 tiles × 5 = 240) beats the next power of two by up to 25 %
             // up to 128 slabs for tiny outputs over a huge K (e.g. a conv-stem weight gradient: 64×147

@@ -197,6 +197,7 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 //   cfg: -1 auto, 0 = 128x128, 1 = 256x256 pipelined, 2 = 256x128 pipelined, 3 = 128x256,
 //        4 = 256x256 simple, 5 = 128x128 pipelined, 6 = 256x192 pipelined, 8 = 256x128 3-stage ring,
 //        9 = persistent 256x256 half-tile stream (gemm_pk.h; needs N % 8 == 0, ldc % 8 == 0)
+//        10 = skinny-M forward GEMM for decoding (gemm_skinny.hip; M <= 64, x·Wᵀ layout, split = K ranges),
 //        (7 is the vendor-library candidate handled in the bindings, off by default);
 //        split: -1 auto, 0/1 none
 // Returns 0, or -1 if the shape violates the kernel's alignment rules.
@@ -209,10 +210,17 @@ long rn_gemm_colpart_rows(int cfg, int M) {
     return cfg == 9 ? 2L * ((M + 255) / 256) : (long)((M + rn_gemm_cfg_bm(cfg) - 1) / rn_gemm_cfg_bm(cfg));
 }
 
+int rn_gemm_skinny(const void* A, const void* W, void* C, const void* bias, const void* res, void* pre, float* ws,
+                   const float* alpha, int M, int N, int K, long lda, long ldw, long ldc, int trans_a, int trans_b,
+                   int act, int split, int out_f32, int accumulate, const float* colpart, hipStream_t st);
+
 int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void* res, void* pre, float* ws,
             const float* alpha, int M, int N, int K, long lda, long ldb, long ldc, int trans_a, int trans_b, int act,
             int split, int out_f32, int accumulate, int cfg, hipStream_t st, float* colpart) {
     if (K % 8 != 0) return -1;
+    if (cfg == 10)  // skinny-M decode GEMM (gemm_skinny.hip): its own N x K decomposition
+        return rn_gemm_skinny(A, B, C, bias, res, pre, ws, alpha, M, N, K, lda, ldb, ldc, trans_a, trans_b, act,
+                              split, out_f32, accumulate, colpart, st);
     if (act_bwd(act) && (trans_a || trans_b || !pre)) return -1;  // fused act-backward: dgrad layout only
     if (trans_a && (M % 8 != 0 || lda % 8 != 0)) return -1;
     if (!trans_a && lda % 8 != 0) return -1;

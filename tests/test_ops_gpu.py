@@ -128,6 +128,36 @@ def test_gemm_epilogue(cuda, act, cfg):
         assert rel_err(pre, h) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
+@pytest.mark.parametrize("N,K,split", [(24, 8, 0), (768, 768, 0), (1000, 1000, 3), (2304, 96, 2), (200, 3072, 12)])
+def test_gemm_skinny_decode(cuda, M, N, K, split):
+    """Config 10 (decode-size x·Wᵀ, gemm_skinny.hip) against fp32 math: bias + residual, the GELU
+    saved-derivative epilogue, split-K partials; bitwise repeatable."""
+    torch.manual_seed(M * 7 + N)
+    a, w = bf(M, K), bf(N, K, scale=0.1)
+    bias, res = bf(N), bf(M, N)
+    out = ops.gemm(a, w, tb=True, bias=bias, residual=res, split_k=split, cfg=10)
+    h = a.float() @ w.float().t() + bias.float()
+    assert rel_err(out, h + res.float()) < 1e-2
+    assert torch.equal(out, ops.gemm(a, w, tb=True, bias=bias, residual=res, split_k=split, cfg=10))
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y = ops.gemm(a, w, tb=True, bias=bias, act=5, preact=pre, split_k=split, cfg=10)
+    assert rel_err(y, F.gelu(h, approximate="tanh")) < 1e-2
+    assert rel_err(pre, _gelu_grad(h.bfloat16())) < 1e-2
+    r = ops.gemm(a, w, tb=True, act=1, split_k=split, cfg=10)
+    assert rel_err(r, F.relu(a.float() @ w.float().t())) < 1e-2
+    o32 = ops.gemm(a, w, tb=True, split_k=split, cfg=10, out_dtype=torch.float32)
+    assert o32.dtype == torch.float32 and rel_err(o32, a.float() @ w.float().t()) < 5e-3
+
+
+def test_gemm_skinny_rejects_other_layouts(cuda):
+    a, w = bf(16, 64), bf(64, 32)
+    with pytest.raises(RuntimeError):
+        ops.gemm(a, w, cfg=10)  # B not K-contiguous: config 10 takes the Linear forward layout only
+    with pytest.raises(RuntimeError):
+        ops.gemm(bf(128, 64), bf(32, 64), tb=True, cfg=10)  # M > 64
+
+
 def _gelu_grad(h):
     hf = h.float().requires_grad_()
     (g,) = torch.autograd.grad(F.gelu(hf, approximate="tanh"), hf, torch.ones_like(hf))
