@@ -149,7 +149,7 @@ void sk_launch(const SkArgs& a, int mb, hipStream_t st) {
 // Returns -1 for what this config does not take (the caller's autotuner then skips it): a
 // transposed operand, M > 64, accumulate, activation backward, column partials, split without a
 // workspace.  ``split``: K ranges (>= 1); each is a multiple of 32 deep.
-int rn_gemm_skinny(const void* A, const void* W, void* C, const void* bias, const void* res, void* pre, float* ws,
+extern "C" int rn_gemm_skinny(const void* A, const void* W, void* C, const void* bias, const void* res, void* pre, float* ws,
                    const float* alpha, int M, int N, int K, long lda, long ldw, long ldc, int trans_a, int trans_b,
                    int act, int split, int out_f32, int accumulate, const float* colpart, hipStream_t st) {
     if (trans_a || !trans_b || M < 1 || M > 64 || accumulate || act_bwd(act) || colpart) return -1;
