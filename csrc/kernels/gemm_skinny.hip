@@ -5,7 +5,7 @@
 // At decode sizes (M = batch rows, one new token each) the 256²/128² tile kernels leave almost the
 // whole chip idle (GPT-2-small c_proj: 768 output columns = 6 tiles of 128) and walk K serially
 // through LDS, so each launch is a chain of K/64 DMA round trips (≈ 25 µs measured per decode GEMM,
-// profiles/decode_r4r.txt).  Here the work is cut along N AND K:
+// profiles/decode_r4s.txt).  Here the work is cut along N AND K:
 //   * one workgroup = 16 output columns × one K range; its 4 waves take interleaved 32-deep k-steps
 //     of that range, so a launch has N/16 × S workgroups (S = K splits, picked by the autotuner);
 //   * no LDS staging: for v_mfma_f32_16x16x32_bf16 lane l holds row (l & 15), k-run 8·(l >> 4) of

@@ -99,7 +99,10 @@ class Attention(nn.Module):
         if cache is not None:
             q, k, v = qkv.unbind(2)
             k_all, v_all = cache.update(layer, k, v)
-            a = ops.attention(q, k_all, v_all, causal=self.causal).reshape(B, T, E)
+            if cache.mask is not None:  # device-position mode: the key mask carries causality
+                a = ops.attention(q, k_all, v_all, bias=cache.mask).reshape(B, T, E)
+            else:
+                a = ops.attention(q, k_all, v_all, causal=self.causal).reshape(B, T, E)
             return self.c_proj(a, residual=residual)
         a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
                                  training=self.training,
@@ -139,8 +142,24 @@ class KVCache:
     def __init__(self, n_layer, max_len):
         self.max_len, self.pos = max_len, 0
         self.kv = [None] * n_layer
+        # device-position mode (a captured decode step, GPT2.generate(graph=True)): the write row is
+        # the 1-element device tensor pos_t and the attention reads the whole buffer under the additive
+        # key mask (1, 1, max_len): 0 for written rows, -inf past them — no host value per step
+        self.pos_t = None
+        self.mask = None
+
+    def to_device_position(self):
+        dev = self.kv[0][0].device
+        self.pos_t = torch.full((1,), self.pos, dtype=torch.long, device=dev)
+        self.mask = torch.full((1, 1, self.max_len), float("-inf"), device=dev)
+        self.mask[..., : self.pos] = 0.0
 
     def update(self, layer, k, v):
+        if self.pos_t is not None:
+            kb, vb = self.kv[layer]
+            kb.index_copy_(1, self.pos_t, k)
+            vb.index_copy_(1, self.pos_t, v)
+            return kb, vb
         B, T, H, D = k.shape
         if self.pos + T > self.max_len:
             raise ValueError(f"KV cache full: {self.pos} + {T} > {self.max_len}")

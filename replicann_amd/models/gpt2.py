@@ -125,24 +125,77 @@ class GPT2(nn.Module):
         return ops.linear(h[:, -1:].contiguous(), self.wte)[:, 0, : c.vocab_size]
 
     @torch.no_grad()
-    def generate(self, idx, max_new_tokens, *, temperature=1.0, top_k=None, generator=None):
+    def _device_position_step(self, tok, cache):
+        """One-token decode step with every per-step value on the device (``KVCache`` device-position
+        mode): capturable as a hipGraph.  Reads ``tok`` (B, 1), returns (B, vocab) logits, advances
+        ``cache.pos_t``."""
+        c = self.config
+        cache.mask.index_fill_(2, cache.pos_t, 0.0)
+        x = ops.embedding(tok, self.wte, self.wpe.index_select(0, cache.pos_t))
+        prev = None
+        for i, blk in enumerate(self.h):
+            x = blk(x, prev, cache=cache, layer=i)
+            prev = blk.out_bias()
+        h = self.ln_f(x, producer_bias=prev)
+        logits = ops.linear(h, self.wte)[:, 0, : c.vocab_size]
+        cache.pos_t.add_(1)
+        return logits
+
+    def _capture_decode(self, cache, B):
+        """Record the one-token decode step as a hipGraph (after one eager warm-up that tunes the
+        decode GEMM shapes); the caller writes the next token into ``tok`` and replays."""
+        dev = self.wte.device
+        cache.to_device_position()
+        tok = torch.zeros(B, 1, dtype=torch.long, device=dev)
+        pos0 = cache.pos
+
+        def reset():  # the warm-up wrote row pos0 and advanced the position: undo
+            cache.pos_t.fill_(pos0)
+            cache.mask[..., pos0:] = float("-inf")
+
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            self._device_position_step(tok, cache)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        reset()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self._device_position_step(tok, cache)
+        reset()
+        return graph, tok, out
+
+    @torch.no_grad()
+    def generate(self, idx, max_new_tokens, *, temperature=1.0, top_k=None, generator=None, graph=None):
         """Autoregressive sampling with a KV cache: ``idx`` (B, T0) prompt → (B, T0 + max_new_tokens).
         ``temperature`` 0 = greedy.  One prefill pass over the prompt, then one-token steps whose
-        attention reads the cached keys / values (no recomputation of the prefix)."""
+        attention reads the cached keys / values (no recomputation of the prefix).  ``graph``
+        (default: on for GPU models): the one-token step is captured once as a hipGraph and replayed
+        (per-step values live on the device), so a step costs its kernels, not ~130 host launches."""
         c = self.config
         B, T0 = idx.shape
         if T0 + max_new_tokens > c.block_size:
             raise ValueError(f"prompt {T0} + {max_new_tokens} new tokens exceeds block_size {c.block_size}")
+        use_graph = (self.wte.is_cuda if graph is None else graph) and max_new_tokens > 2
         was_training = self.training
         self.eval()
         try:
             cache = KVCache(c.n_layer, T0 + max_new_tokens)
             logits = self.decode_step(idx, cache)
             out = [idx]
+            g = None
             for i in range(max_new_tokens):
                 nxt = _sample(logits.float(), temperature, top_k, generator)
                 out.append(nxt)
-                if i + 1 < max_new_tokens:
+                if i + 1 == max_new_tokens:
+                    break
+                if use_graph:
+                    if g is None:
+                        g, tok, g_out = self._capture_decode(cache, B)
+                    tok.copy_(nxt)
+                    g.replay()
+                    logits = g_out
+                else:
                     logits = self.decode_step(nxt, cache)
             return torch.cat(out, 1)
         finally:

@@ -1,8 +1,9 @@
 """GPT-2 KV-cache decoding throughput on one MI355X (random-init weights, bf16, greedy).
 
-For each batch size: one untimed generate (GEMM autotuning of the decode shapes, allocations),
-then a timed prefill of the prompt and a timed generate of ``--new`` tokens.  Prints one JSON line
-per batch size: prefill ms, ms per decode step, generated tokens/s over the batch.
+For each batch size: a timed prefill of the prompt, then for the eager and the hipGraph-replayed
+one-token step: one untimed generate (GEMM autotuning of the decode shapes, graph capture) and a
+timed generate of ``--new`` tokens.  One JSON line per (batch, step form): prefill ms, ms per
+decode step (generate time minus the prefill, over the steps), generated tokens/s over the batch.
 
     python scripts/decode_bench.py --model gpt2-small --batches 1,16,64 --prompt 128 --new 128
 """
@@ -40,23 +41,25 @@ def main():
     m.eval()
     for B in [int(b) for b in a.batches.split(",")]:
         idx = torch.randint(0, m.config.vocab_size, (B, a.prompt), device=dev)
-        m.generate(idx, a.new, temperature=0)  # warm-up: tunes the decode GEMM shapes
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         cache = KVCache(m.config.n_layer, a.prompt + a.new)
         m.decode_step(idx, cache)
         torch.cuda.synchronize()
         prefill = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        out = m.generate(idx, a.new, temperature=0)
-        torch.cuda.synchronize()
-        total = time.perf_counter() - t0
-        step_ms = (total - prefill) / max(1, a.new - 1) * 1e3
-        print(json.dumps({"model": a.model, "batch": B, "prompt": a.prompt, "new_tokens": a.new,
-                          "prefill_ms": round(prefill * 1e3, 3), "decode_ms_per_step": round(step_ms, 3),
-                          "generated_tokens_per_s": round(B * a.new / total, 1),
-                          "out_shape": list(out.shape), "dtype": "bf16", "weights": "random init"}), flush=True)
-
+        for graph in (False, True):
+            m.generate(idx, a.new, temperature=0, graph=graph)  # warm-up: tunes the decode GEMM shapes
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = m.generate(idx, a.new, temperature=0, graph=graph)
+            torch.cuda.synchronize()
+            total = time.perf_counter() - t0
+            step_ms = (total - prefill) / max(1, a.new - 1) * 1e3
+            print(json.dumps({"model": a.model, "batch": B, "prompt": a.prompt, "new_tokens": a.new,
+                              "decode_step": "hipGraph replay" if graph else "eager",
+                              "prefill_ms": round(prefill * 1e3, 3), "decode_ms_per_step": round(step_ms, 3),
+                              "generated_tokens_per_s": round(B * a.new / total, 1),
+                              "out_shape": list(out.shape), "dtype": "bf16", "weights": "random init"}), flush=True)
 
 if __name__ == "__main__":
     main()

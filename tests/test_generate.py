@@ -62,3 +62,20 @@ def test_cache_limits():
     m.train()
     m.generate(torch.zeros(1, 2, dtype=torch.long), 2)
     assert m.training is True  # generate restores the mode
+
+
+def test_device_position_steps_match_host_position():
+    """The capturable step (device-side position, cache rows written by index, the key mask carrying
+    causality) against the host-position decode, teacher-forced, run eagerly here."""
+    m = _model()
+    seq = torch.randint(0, 1000, (2, 20))
+    host = KVCache(m.config.n_layer, 20)
+    dev = KVCache(m.config.n_layer, 20)
+    m.decode_step(seq[:, :12], host)
+    m.decode_step(seq[:, :12], dev)
+    dev.to_device_position()
+    for t in range(12, 20):
+        a = m.decode_step(seq[:, t:t + 1], host)
+        b = m._device_position_step(seq[:, t:t + 1], dev)
+        assert (a - b).abs().max().item() < 1e-4
+    assert int(dev.pos_t) == 20 and bool((dev.mask == 0).all())

@@ -47,3 +47,27 @@ def test_generate_gpu(cuda):
     assert torch.equal(out[:, 16], first)
     s = m.generate(idx, 8, temperature=1.0, top_k=20, generator=torch.Generator(device=cuda).manual_seed(1))
     assert s.shape == (4, 24) and int(s.max()) < m.config.vocab_size
+
+
+def test_generate_graph_matches_eager(cuda):
+    """The hipGraph-replayed one-token step (device-side position, masked full-cache attention)
+    against the eager host-position steps: same first token, logits of each replay close."""
+    from replicann_amd.models.blocks import KVCache
+    m = _model(cuda, 2)
+    idx = torch.randint(0, 1000, (3, 20), device=cuda)
+    seq = torch.cat([idx, torch.randint(0, 1000, (3, 12), device=cuda)], 1)
+    host = KVCache(m.config.n_layer, 32)
+    dev = KVCache(m.config.n_layer, 32)
+    m.decode_step(idx, host)
+    m.decode_step(idx, dev)
+    g, tok, out = m._capture_decode(dev, 3)
+    for t in range(20, 32):
+        a = m.decode_step(seq[:, t:t + 1], host)
+        tok.copy_(seq[:, t:t + 1])
+        g.replay()
+        assert rel_err(out, a) < 3e-2, t
+    torch.cuda.synchronize()
+    assert int(dev.pos_t) == 32
+    e = m.generate(idx, 12, temperature=0, graph=False)
+    r = m.generate(idx, 12, temperature=0, graph=True)
+    assert torch.equal(e[:, :21], r[:, :21])
