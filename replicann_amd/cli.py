@@ -3,6 +3,7 @@
 
     replicann train --model gpt2-small --batch-size 64 --steps 100 [--checkpoint ck.pt]
     replicann eval  --model gpt2-small --checkpoint ck.pt
+    replicann generate --model gpt2-small --checkpoint ck.pt --prompt 464,2068 --new 32 --top-k 50
     replicann build            # compile the gfx950 extension in-tree (hipcc --offload-arch=gfx950)
     replicann <train args...>  # no command: train (kept for ``python -m replicann --model ...``)
 
@@ -16,7 +17,7 @@ from __future__ import annotations
 
 import sys
 
-COMMANDS = ("train", "eval", "build")
+COMMANDS = ("train", "eval", "generate", "build")
 
 
 def main(argv=None):
@@ -28,8 +29,8 @@ def main(argv=None):
         from . import _build
         _build.build(verbose=True)
         return 0
-    from .training import eval_main, main as train_main
-    (eval_main if cmd == "eval" else train_main)(argv)
+    from .training import eval_main, generate_main, main as train_main
+    {"eval": eval_main, "generate": generate_main}.get(cmd, train_main)(argv)
     return 0
 
 

@@ -469,6 +469,52 @@ def eval_main(argv=None):
     return out
 
 
+def generate_main(argv=None):
+    """``python -m replicann generate``: sample continuations from a GPT-2 model — random init, or a
+    checkpoint written by ``train(checkpoint=...)`` — with the KV cache and the hipGraph-replayed
+    decode step (``GPT2.generate``).  Prints one JSON line: the token ids, decode timing."""
+    ap = argparse.ArgumentParser(description="replicann generation entrypoint (GPT-2 models)")
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--prompt", default=None, help="comma-separated token ids (default: random ids)")
+    ap.add_argument("--prompt-len", type=int, default=16)
+    ap.add_argument("--batch-size", type=int, default=1)
+    ap.add_argument("--new", type=int, default=32)
+    ap.add_argument("--temperature", type=float, default=1.0)
+    ap.add_argument("--top-k", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--model-kwargs", type=json.loads, default={})
+    a = ap.parse_args(argv)
+    if not a.model.startswith("gpt2"):
+        raise SystemExit(f"generate: {a.model} is not an autoregressive GPT-2 model")
+    from .utils.checkpoint import load_checkpoint
+    dev = torch.device(a.device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    torch.manual_seed(a.seed)
+    model = build_model(a.model, **a.model_kwargs)
+    if a.checkpoint:
+        load_checkpoint(a.checkpoint, model, restore_rng=False, allow_world_change=True)
+    model = model.to(dev)
+    if dev.type == "cuda":
+        from .tuning import load_committed
+        load_committed(a.model)
+        model = model.to(torch.bfloat16)
+    if a.prompt:
+        ids = torch.tensor([[int(t) for t in a.prompt.split(",")]] * a.batch_size, dtype=torch.long)
+    else:
+        ids = torch.randint(0, model.config.vocab_size, (a.batch_size, a.prompt_len))
+    gen = torch.Generator(device=dev).manual_seed(a.seed)
+    t0 = time.perf_counter()
+    out = model.generate(ids.to(dev), a.new, temperature=a.temperature, top_k=a.top_k, generator=gen)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    res = {"model": a.model, "tokens": out[:, ids.shape[1]:].tolist(), "prompt_len": ids.shape[1],
+           "new_tokens": a.new, "seconds": round(dt, 4), "tokens_per_s": round(out.shape[0] * a.new / dt, 1)}
+    print(json.dumps(res))
+    return res
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="replicann_amd training entrypoint")
     for f, v in asdict(TrainConfig()).items():

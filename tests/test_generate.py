@@ -79,3 +79,21 @@ def test_device_position_steps_match_host_position():
         b = m._device_position_step(seq[:, t:t + 1], dev)
         assert (a - b).abs().max().item() < 1e-4
     assert int(dev.pos_t) == 20 and bool((dev.mask == 0).all())
+
+
+def test_generate_cli_from_checkpoint(tmp_path, capsys):
+    """``python -m replicann generate`` loads a training checkpoint (weights_only) and reproduces the
+    model's own greedy continuation."""
+    import json
+
+    from replicann_amd import cli
+    from replicann_amd.utils.checkpoint import save_checkpoint
+    m = _model()
+    ck = tmp_path / "ck.pt"
+    save_checkpoint(str(ck), m, step=3)
+    prompt = [5, 17, 256, 999]
+    cli.main(["generate", "--model", "gpt2-tiny", "--checkpoint", str(ck), "--prompt", ",".join(map(str, prompt)),
+              "--new", "6", "--temperature", "0", "--device", "cpu"])
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    want = m.generate(torch.tensor([prompt]), 6, temperature=0)[0, 4:].tolist()
+    assert res["tokens"] == [want] and res["new_tokens"] == 6
