@@ -99,7 +99,7 @@ class Attention(nn.Module):
         if cache is not None:
             q, k, v = qkv.unbind(2)
             k_all, v_all = cache.update(layer, k, v)
-            if cache.mask is not None:  # device-position mode: the key mask carries causality
+            if cache.device_pos:  # device-position mode: the key mask carries causality
                 a = ops.attention(q, k_all, v_all, bias=cache.mask).reshape(B, T, E)
             else:
                 a = ops.attention(q, k_all, v_all, causal=self.causal).reshape(B, T, E)
@@ -147,15 +147,26 @@ class KVCache:
         # key mask (1, 1, max_len): 0 for written rows, -inf past them — no host value per step
         self.pos_t = None
         self.mask = None
+        self.device_pos = False
 
     def to_device_position(self):
-        dev = self.kv[0][0].device
-        self.pos_t = torch.full((1,), self.pos, dtype=torch.long, device=dev)
-        self.mask = torch.full((1, 1, self.max_len), float("-inf"), device=dev)
+        """Switch to device-position mode at the current host position (the same pos_t / mask
+        tensors are refilled on later calls, so a graph captured on them stays valid)."""
+        if self.pos_t is None:
+            dev = self.kv[0][0].device
+            self.pos_t = torch.empty(1, dtype=torch.long, device=dev)
+            self.mask = torch.empty(1, 1, self.max_len, device=dev)
+        self.pos_t.fill_(self.pos)
+        self.mask.fill_(float("-inf"))
         self.mask[..., : self.pos] = 0.0
+        self.device_pos = True
+
+    def reset(self):
+        """Start a new sequence in the same buffers (host-position mode, position 0)."""
+        self.pos, self.device_pos = 0, False
 
     def update(self, layer, k, v):
-        if self.pos_t is not None:
+        if self.device_pos:
             kb, vb = self.kv[layer]
             kb.index_copy_(1, self.pos_t, k)
             vb.index_copy_(1, self.pos_t, v)

@@ -180,18 +180,34 @@ class GPT2(nn.Module):
         was_training = self.training
         self.eval()
         try:
-            cache = KVCache(c.n_layer, T0 + max_new_tokens)
+            L = T0 + max_new_tokens
+            # the parameters' storage is part of the key: a graph reads them by address, so one captured
+            # before a parameter was re-assigned (p.data = ...) must never be replayed
+            sig = tuple(p.data_ptr() for p in self.parameters())
+            key = (B, L, self.wte.dtype, self.wte.device, sig)
+            graphs = self._decode_graphs()
+            for k in [k for k in graphs if k[4] != sig]:
+                del graphs[k]
+            entry = graphs.get(key) if use_graph else None
+            if entry is not None:  # same batch / length as an earlier call: reuse its cache and graph
+                cache = entry[0]
+                cache.reset()
+            else:
+                cache = KVCache(c.n_layer, L)
             logits = self.decode_step(idx, cache)
             out = [idx]
-            g = None
             for i in range(max_new_tokens):
                 nxt = _sample(logits.float(), temperature, top_k, generator)
                 out.append(nxt)
                 if i + 1 == max_new_tokens:
                     break
                 if use_graph:
-                    if g is None:
-                        g, tok, g_out = self._capture_decode(cache, B)
+                    if entry is None:
+                        entry = (cache, *self._capture_decode(cache, B))
+                        graphs[key] = entry
+                    elif not cache.device_pos:
+                        cache.to_device_position()
+                    _, g, tok, g_out = entry
                     tok.copy_(nxt)
                     g.replay()
                     logits = g_out
@@ -200,6 +216,18 @@ class GPT2(nn.Module):
             return torch.cat(out, 1)
         finally:
             self.train(was_training)
+
+    def _decode_graphs(self):
+        """Captured decode steps kept across ``generate`` calls, keyed by (batch, total length, dtype,
+        device, parameter storage): a serving loop with fixed shapes captures once.  Each holds its KV cache (2 ·
+        n_layer · B · length · n_embd elements); ``clear_decode_graphs`` frees them."""
+        d = self.__dict__.get("_rn_decode_graphs")
+        if d is None:
+            d = self.__dict__["_rn_decode_graphs"] = {}
+        return d
+
+    def clear_decode_graphs(self):
+        self.__dict__.pop("_rn_decode_graphs", None)
 
     def flops_per_token(self, T=None):
         """Training FLOPs per token (fwd+bwd): 6·N_matmul + attention (causal)."""

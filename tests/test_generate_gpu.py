@@ -71,3 +71,24 @@ def test_generate_graph_matches_eager(cuda):
     e = m.generate(idx, 12, temperature=0, graph=False)
     r = m.generate(idx, 12, temperature=0, graph=True)
     assert torch.equal(e[:, :21], r[:, :21])
+
+
+def test_generate_graph_reuse(cuda):
+    """A second generate with the same batch / length replays the stored graph (no new capture) and
+    gives the same greedy tokens; another batch size captures its own; re-assigned parameters
+    invalidate the stored graphs."""
+    m = _model(cuda, 2)
+    idx = torch.randint(0, 1000, (2, 10), device=cuda)
+    a = m.generate(idx, 9, temperature=0)
+    assert len(m._decode_graphs()) == 1
+    b = m.generate(idx, 9, temperature=0)
+    assert torch.equal(a, b) and len(m._decode_graphs()) == 1
+    m.generate(idx[:1], 9, temperature=0)
+    assert len(m._decode_graphs()) == 2
+    with torch.no_grad():
+        for p in m.parameters():
+            p.data = p.data.clone()
+    c = m.generate(idx, 9, temperature=0)
+    assert torch.equal(a, c) and len(m._decode_graphs()) == 1
+    m.clear_decode_graphs()
+    assert len(m._decode_graphs()) == 0
