@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 fault() { grep -q "illegal memory access\|hipErrorIllegalAddress\|HSA_STATUS_ERROR\|Memory access fault" "$1"; }
 PT="python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 300 $PT -x tests/tesv_generate_gpu.py tests/tesv_generate.py > gpurun_out/v_gen.log 2>&1; rc=$?
+timeout -k 10 300 $PT -x tests/test_generate_gpu.py tests/test_generate.py > gpurun_out/v_gen.log 2>&1; rc=$?
 echo "=== v_gen rc=$rc $(grep -E 'passed|failed' gpurun_out/v_gen.log | tail -1)"; grep -E "FAILED|Error" gpurun_out/v_gen.log | head
 fault gpurun_out/v_gen.log && exit 2; [ $rc -ne 0 ] && exit 1
 timeout -k 10 400 python scripts/decode_bench.py --batches 1,16,64 > gpurun_out/v_decode.log 2>&1; rc=$?
