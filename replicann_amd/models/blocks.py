@@ -175,7 +175,10 @@ class KVCache:
         if self.pos + T > self.max_len:
             raise ValueError(f"KV cache full: {self.pos} + {T} > {self.max_len}")
         if self.kv[layer] is None:
-            self.kv[layer] = (k.new_empty(B, self.max_len, H, D), v.new_empty(B, self.max_len, H, D))
+            # zeroed, not empty: the device-position step reads the WHOLE buffer under the key mask, and
+            # a masked row still enters P·V as 0 · v — a NaN bit pattern in an unwritten row would
+            # turn that into NaN
+            self.kv[layer] = (k.new_zeros(B, self.max_len, H, D), v.new_zeros(B, self.max_len, H, D))
         kb, vb = self.kv[layer]
         kb[:, self.pos: self.pos + T].copy_(k)
         vb[:, self.pos: self.pos + T].copy_(v)
