@@ -97,8 +97,8 @@ class Attention(nn.Module):
         B, T, E = h.shape
         qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
         if cache is not None:
-            q, k, v = qkv.unbind(2)
-            k_all, v_all = cache.update(layer, k, v)
+            q = qkv[:, :, 0]
+            k_all, v_all = cache.update(layer, qkv[:, :, 1:3])
             if cache.device_pos:  # device-position mode: the key mask carries causality
                 a = ops.attention(q, k_all, v_all, bias=cache.mask).reshape(B, T, E)
             else:
@@ -135,9 +135,9 @@ class MLP(nn.Module):
 
 
 class KVCache:
-    """Per-layer key / value buffers for incremental decoding, (B, max_len, H, D) each, allocated on
+    """Per-layer key / value buffer for incremental decoding, (B, max_len, 2, H, D), allocated on
     first use in the dtype / device of the keys (one HBM allocation per layer for the whole
-    generation; appends are row copies, the attention reads a strided prefix view)."""
+    generation; an append is one row copy, the attention reads strided key / value views)."""
 
     def __init__(self, n_layer, max_len):
         self.max_len, self.pos = max_len, 0
@@ -153,7 +153,7 @@ class KVCache:
         """Switch to device-position mode at the current host position (the same pos_t / mask
         tensors are refilled on later calls, so a graph captured on them stays valid)."""
         if self.pos_t is None:
-            dev = self.kv[0][0].device
+            dev = self.kv[0].device
             self.pos_t = torch.empty(1, dtype=torch.long, device=dev)
             self.mask = torch.empty(1, 1, self.max_len, device=dev)
         self.pos_t.fill_(self.pos)
@@ -165,24 +165,26 @@ class KVCache:
         """Start a new sequence in the same buffers (host-position mode, position 0)."""
         self.pos, self.device_pos = 0, False
 
-    def update(self, layer, k, v):
+    def update(self, layer, kv):
+        """Append ``kv`` (B, T, 2, H, D) — the key / value slice of the packed QKV projection — at
+        the cache position; returns the (key, value) views the attention reads.  K and V share one
+        (B, max_len, 2, H, D) buffer per layer, so an append is ONE copy (one index_copy_ in
+        device-position mode)."""
         if self.device_pos:
-            kb, vb = self.kv[layer]
-            kb.index_copy_(1, self.pos_t, k)
-            vb.index_copy_(1, self.pos_t, v)
-            return kb, vb
-        B, T, H, D = k.shape
+            buf = self.kv[layer]
+            buf.index_copy_(1, self.pos_t, kv)
+            return buf[:, :, 0], buf[:, :, 1]
+        B, T, _, H, D = kv.shape
         if self.pos + T > self.max_len:
             raise ValueError(f"KV cache full: {self.pos} + {T} > {self.max_len}")
         if self.kv[layer] is None:
             # zeroed, not empty: the device-position step reads the WHOLE buffer under the key mask, and
             # a masked row still enters P·V as 0 · v — a NaN bit pattern in an unwritten row would
             # turn that into NaN
-            self.kv[layer] = (k.new_zeros(B, self.max_len, H, D), v.new_zeros(B, self.max_len, H, D))
-        kb, vb = self.kv[layer]
-        kb[:, self.pos: self.pos + T].copy_(k)
-        vb[:, self.pos: self.pos + T].copy_(v)
-        return kb[:, : self.pos + T], vb[:, : self.pos + T]
+            self.kv[layer] = kv.new_zeros(B, self.max_len, 2, H, D)
+        buf = self.kv[layer]
+        buf[:, self.pos: self.pos + T].copy_(kv)
+        return buf[:, : self.pos + T, 0], buf[:, : self.pos + T, 1]
 
     def advance(self, T):
         self.pos += T
