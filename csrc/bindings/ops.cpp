@@ -67,8 +67,6 @@ int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, fl
             long, long, long, int, int, int, int, int, int, int, hipStream_t, float*);
 int rn_gemm_cfg_bm(int);
 long rn_gemm_colpart_rows(int, int);
-int rn_ln_gemm_skinny(const void*, const void*, const void*, float, const void*, const void*, void*, int, int, int,
-                      long, long, long, int, hipStream_t);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
                 int, int, float, int, float, uint64_t, const uint64_t*, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
@@ -386,25 +384,6 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
         rn_colsum_f32(colpart.data_ptr<float>(), (int)rn_gemm_colpart_rows((int)cfg, (int)M), (int)N, tmp.data_ptr<float>(),
                       bias_grad->data_ptr(), 1, cur_stream());
     }
-    return c;
-}
-
-// decode-size LayerNorm → projection in one launch: act(LN(x)·Wᵀ + bias), x [M][K] with M <= 64
-// (gemm_skinny.hip); the LayerNorm output is never written
-Tensor ln_linear(const Tensor& x, const Tensor& ln_w, const optional<Tensor>& ln_b, double eps, const Tensor& w,
-                 const optional<Tensor>& bias, int64_t act) {
-    CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(ln_w); CHECK_BF16(w); GUARD(x);
-    TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.stride(1) == 1, "ln_linear: 2-D row-major operands");
-    const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-    TORCH_CHECK(w.size(1) == K && ln_w.numel() == K && ln_w.is_contiguous(), "ln_linear: shape mismatch");
-    if (ln_b && ln_b->defined()) { CHECK_BF16(*ln_b); TORCH_CHECK(ln_b->numel() == K && ln_b->is_contiguous()); }
-    if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
-    Tensor c = at::empty({M, N}, x.options());
-    if (M == 0 || N == 0) return c;
-    const int rc = rn_ln_gemm_skinny(x.data_ptr(), ln_w.data_ptr(), optr(ln_b), (float)eps, w.data_ptr(), optr(bias),
-                                     c.data_ptr(), (int)M, (int)N, (int)K, x.stride(0), w.stride(0), c.stride(0),
-                                     (int)act, cur_stream());
-    TORCH_CHECK(rc == 0, "ln_linear: unsupported shape M=", M, " K=", K, " act=", act, " (M <= 64, K % 8 == 0)");
     return c;
 }
 
@@ -1117,7 +1096,6 @@ TORCH_LIBRARY(replicann, m) {
     m.def("gemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, Tensor? residual, int act, Tensor? preact, "
           "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1, "
           "Tensor(a!)? bias_grad=None) -> Tensor");
-    m.def("ln_linear(Tensor x, Tensor ln_w, Tensor? ln_b, float eps, Tensor w, Tensor? bias, int act) -> Tensor");
     m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias, Tensor(a!)? db_accum=None) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
@@ -1191,7 +1169,6 @@ TORCH_LIBRARY(replicann, m) {
 
 TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("gemm", &gemm);
-    m.impl("ln_linear", &ln_linear);
     m.impl("bias_act_grad", &bias_act_grad);
     m.impl("act_fwd", &act_fwd);
     m.impl("act_bwd", &act_bwd);

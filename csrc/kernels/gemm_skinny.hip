@@ -16,11 +16,6 @@
 //     and applies it: deterministic, no atomics.
 // Epilogue order as the tile kernels': ·alpha, +bias, activation (with the optional
 // pre-activation / gelu' store of the bf16-rounded h), +residual.
-//
-// LN variant (rn_ln_gemm_skinny, the decode step's LayerNorm → projection pairs): A = LN(x) is never
-// written — each workgroup first reduces its rows' mean / rstd (two passes over the row, as the
-// LayerNorm kernel), then normalises every A fragment as it is loaded ((x − μ)·rstd·γ + β, rounded
-// to bf16 like the stored LayerNorm output).  Saves one launch per LayerNorm of a decode step.
 #include "common.h"
 
 namespace {
@@ -37,9 +32,6 @@ struct SkArgs {
     int M, N, K, S, kc;  // kc: K range per split (multiple of 32)
     long lda, ldw, ldc;
     int out_f32;
-    const bf16* ln_w;  // LN variant: γ, β (β optional), eps
-    const bf16* ln_b;
-    float eps;
 };
 
 template <int ACT>
@@ -65,48 +57,10 @@ RN_DEV s16x8 sk_load(const bf16* base, long row_off, int k, int K, bool row_ok) 
     return (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
 }
 
-// LN(x) fragment: 8 consecutive k of one row, normalised with the row's (μ, rstd), rounded to bf16
-RN_DEV s16x8 sk_load_ln(const SkArgs& p, long row_off, int k, int K, bool row_ok, float mu, float rs) {
-    if (!(row_ok && k < K)) return (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
-    float x[8], g[8], b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    load8(p.A + row_off + k, x);
-    load8(p.ln_w + k, g);
-    if (p.ln_b) load8(p.ln_b + k, b);
-    s16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = __builtin_bit_cast(short, (bf16)((x[j] - mu) * rs * g[j] + b[j]));
-    return o;
-}
-
-template <int MB, int ACT, bool LN = false>
+template <int MB, int ACT>
 __global__ void __launch_bounds__(256) skinny_k(SkArgs p) {
     __shared__ f32x4 red[4][MB][64];
-    [[maybe_unused]] __shared__ float st_mu[64], st_rs[64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if constexpr (LN) {  // row statistics over the full K: 4 lanes per row, two passes (mean, then Σ(x−μ)²)
-        const int row = threadIdx.x >> 2, part = threadIdx.x & 3, nch = p.K / 8;
-        const bool ok = row < p.M;
-        const bf16* xr = p.A + (long)(ok ? row : 0) * p.lda;
-        float s = 0.f, f[8];
-        for (int c = part; ok && c < nch; c += 4) {
-            load8(xr + c * 8, f);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s += f[j];
-        }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        const float mu = s / p.K;
-        float q = 0.f;
-        for (int c = part; ok && c < nch; c += 4) {
-            load8(xr + c * 8, f);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { const float d = f[j] - mu; q += d * d; }
-        }
-        q += __shfl_xor(q, 1, 64);
-        q += __shfl_xor(q, 2, 64);
-        if (part == 0) { st_mu[row] = mu; st_rs[row] = rsqrtf(q / p.K + p.eps); }
-        __syncthreads();
-    }
     const int n0 = blockIdx.x * 16, split = blockIdx.y;
     const int r = lane & 15, kg = 8 * (lane >> 4);
     const int k_lo = split * p.kc, k_hi = min(p.K, k_lo + p.kc);
@@ -114,18 +68,12 @@ __global__ void __launch_bounds__(256) skinny_k(SkArgs p) {
     const long w_off = (long)min(n, p.N - 1) * p.ldw;
     long a_off[MB];
     bool a_ok[MB];
-    [[maybe_unused]] float a_mu[MB], a_rs[MB];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
         const int m = mb * 16 + r;
         a_ok[mb] = m < p.M;
         a_off[mb] = (long)min(m, p.M - 1) * p.lda;
-        if constexpr (LN) { a_mu[mb] = st_mu[min(m, 63)]; a_rs[mb] = st_rs[min(m, 63)]; }
     }
-    auto load_a = [&](int mb, int kk) -> s16x8 {
-        if constexpr (LN) return sk_load_ln(p, a_off[mb], kk, k_hi, a_ok[mb], a_mu[mb], a_rs[mb]);
-        else return sk_load(p.A, a_off[mb], kk, k_hi, a_ok[mb]);
-    };
     f32x4 acc[MB];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) acc[mb] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -137,8 +85,8 @@ __global__ void __launch_bounds__(256) skinny_k(SkArgs p) {
         s16x8 a0[MB], a1[MB];
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) {
-            a0[mb] = load_a(mb, k + kg);
-            a1[mb] = load_a(mb, k + 128 + kg);
+            a0[mb] = sk_load(p.A, a_off[mb], k + kg, k_hi, a_ok[mb]);
+            a1[mb] = sk_load(p.A, a_off[mb], k + 128 + kg, k_hi, a_ok[mb]);
         }
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[mb], w0, acc[mb], 0, 0, 0);
@@ -149,7 +97,8 @@ __global__ void __launch_bounds__(256) skinny_k(SkArgs p) {
         const s16x8 w0 = sk_load(p.W, w_off, k + kg, k_hi, n < p.N);
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
-            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_a(mb, k + kg), w0, acc[mb], 0, 0, 0);
+            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sk_load(p.A, a_off[mb], k + kg, k_hi, a_ok[mb]), w0,
+                                                              acc[mb], 0, 0, 0);
     }
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) red[wave][mb][lane] = acc[mb];
@@ -183,14 +132,14 @@ __global__ void __launch_bounds__(256) skinny_fin_k(SkArgs p) {
     sk_store<ACT>(p, m, n, v);
 }
 
-template <int ACT, bool LN = false>
+template <int ACT>
 void sk_launch(const SkArgs& a, int mb, hipStream_t st) {
     const dim3 grid((a.N + 15) / 16, a.S);
     switch (mb) {
-        case 1: skinny_k<1, ACT, LN><<<grid, 256, 0, st>>>(a); break;
-        case 2: skinny_k<2, ACT, LN><<<grid, 256, 0, st>>>(a); break;
-        case 3: skinny_k<3, ACT, LN><<<grid, 256, 0, st>>>(a); break;
-        default: skinny_k<4, ACT, LN><<<grid, 256, 0, st>>>(a); break;
+        case 1: skinny_k<1, ACT><<<grid, 256, 0, st>>>(a); break;
+        case 2: skinny_k<2, ACT><<<grid, 256, 0, st>>>(a); break;
+        case 3: skinny_k<3, ACT><<<grid, 256, 0, st>>>(a); break;
+        default: skinny_k<4, ACT><<<grid, 256, 0, st>>>(a); break;
     }
     if (a.S > 1) skinny_fin_k<ACT><<<rn_cdiv((long)a.M * a.N, 256), 256, 0, st>>>(a);
 }
@@ -222,28 +171,6 @@ extern "C" int rn_gemm_skinny(const void* A, const void* W, void* C, const void*
         case ACT_GELU: sk_launch<ACT_GELU>(a, mb, st); break;
         case ACT_GELU_D: sk_launch<ACT_GELU_D>(a, mb, st); break;
         default: sk_launch<ACT_NONE>(a, mb, st); break;
-    }
-    return 0;
-}
-
-// out[M][N] = act(LN(x)·Wᵀ + bias), LN over K with γ (ln_w), β (ln_b, optional), eps; M <= 64, one K
-// range per workgroup (the row statistics need the whole row anyway).  Returns -1 if not taken.
-extern "C" int rn_ln_gemm_skinny(const void* x, const void* ln_w, const void* ln_b, float eps, const void* W,
-                                 const void* bias, void* C, int M, int N, int K, long ldx, long ldw, long ldc, int act,
-                                 hipStream_t st) {
-    if (M < 1 || M > 64 || K % 8 != 0 || ldx % 8 != 0 || ldw % 8 != 0) return -1;
-    if (act != ACT_NONE && act != ACT_RELU && act != ACT_GELU) return -1;
-    SkArgs a = {};
-    a.A = (const bf16*)x; a.W = (const bf16*)W; a.C = C; a.bias = (const bf16*)bias;
-    a.M = M; a.N = N; a.K = K; a.lda = ldx; a.ldw = ldw; a.ldc = ldc;
-    a.ln_w = (const bf16*)ln_w; a.ln_b = (const bf16*)ln_b; a.eps = eps;
-    a.S = 1;
-    a.kc = (K + 31) / 32 * 32;
-    const int mb = (M + 15) / 16;
-    switch (act) {
-        case ACT_RELU: sk_launch<ACT_RELU, true>(a, mb, st); break;
-        case ACT_GELU: sk_launch<ACT_GELU, true>(a, mb, st); break;
-        default: sk_launch<ACT_NONE, true>(a, mb, st); break;
     }
     return 0;
 }

@@ -90,18 +90,6 @@ class Attention(nn.Module):
         """Bias whose gradient equals Σ_rows of the block output's gradient (None if dropout intervenes)."""
         return self.c_proj.bias if not (self.resid_dropout > 0 and self.training) else None
 
-    def attend_cached(self, qkv, residual, cache, layer):
-        """Attention of the new tokens' packed (B, T, 3, H, D) projections against the KV cache,
-        then the output projection + residual."""
-        B, T = qkv.shape[:2]
-        q = qkv[:, :, 0]
-        k_all, v_all = cache.update(layer, qkv[:, :, 1:3])
-        if cache.device_pos:  # device-position mode: the key mask carries causality
-            a = ops.attention(q, k_all, v_all, bias=cache.mask)
-        else:
-            a = ops.attention(q, k_all, v_all, causal=self.causal)
-        return self.c_proj(a.reshape(B, T, -1), residual=residual)
-
     def forward(self, h, residual, cache=None, layer=0):
         """``cache``: a :class:`KVCache` (inference) — this call's keys / values are appended at the
         cache position and the queries attend to everything cached so far (causal, bottom-right
@@ -109,7 +97,13 @@ class Attention(nn.Module):
         B, T, E = h.shape
         qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
         if cache is not None:
-            return self.attend_cached(qkv, residual, cache, layer)
+            q = qkv[:, :, 0]
+            k_all, v_all = cache.update(layer, qkv[:, :, 1:3])
+            if cache.device_pos:  # device-position mode: the key mask carries causality
+                a = ops.attention(q, k_all, v_all, bias=cache.mask).reshape(B, T, E)
+            else:
+                a = ops.attention(q, k_all, v_all, causal=self.causal).reshape(B, T, E)
+            return self.c_proj(a, residual=residual)
         a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
                                  training=self.training,
                                  producer_bias=self.c_attn.bias)
@@ -138,10 +132,6 @@ class MLP(nn.Module):
         fp8 = (self.c_fc.fp8_state, self.c_proj.fp8_state) if self.c_fc.fp8 else None
         return ops.mlp(h, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias, "gelu",
                        residual=residual, fp8=fp8)
-
-
-def _ln_proj(ln, lin, x, act=None):
-    return ops.ln_linear(x, ln.weight, ln.bias, ln.eps, lin.weight, lin.bias, act=act)
 
 
 class KVCache:
@@ -216,21 +206,9 @@ class PreLNBlock(nn.Module):
         """``prev_bias``: out_bias() of the block that produced x (its gradient is
         then reduced inside ln_1's backward kernel).  ``cache`` / ``layer``: incremental
         decoding (see :class:`KVCache`)."""
-        if cache is not None and self.attn.c_attn.fp8_state is None and not torch.is_grad_enabled():
-            return self._decode(x, cache, layer)
         # fp8 blocks: the LayerNorms also emit the e4m3 input of c_attn / c_fc
         h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias, fp8=self.attn.c_attn.fp8_state)
         x = self.attn(h, residual=x, cache=cache, layer=layer)
         h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias(), fp8=self.mlp.c_fc.fp8_state)
         x = self.mlp(h, residual=x)
         return x
-
-    def _decode(self, x, cache, layer):
-        """Inference step against a KV cache: each LayerNorm runs inside the projection it feeds
-        (``ops.ln_linear``: one launch at decode sizes), the MLP's GELU without the saved derivative."""
-        B, T, E = x.shape
-        at = self.attn
-        qkv = _ln_proj(self.ln_1, at.c_attn, x).view(B, T, 3, at.n_head, E // at.n_head)
-        x = at.attend_cached(qkv, x, cache, layer)
-        u = _ln_proj(self.ln_2, self.mlp.c_fc, x, act="gelu")
-        return self.mlp.c_proj(u, residual=x)

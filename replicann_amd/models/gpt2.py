@@ -120,8 +120,9 @@ class GPT2(nn.Module):
         for i, blk in enumerate(self.h):
             x = blk(x, prev, cache=cache, layer=i)
             prev = blk.out_bias()
+        h = self.ln_f(x, producer_bias=prev)
         cache.advance(T)
-        return ops.ln_linear(x[:, -1:], self.ln_f.weight, self.ln_f.bias, self.ln_f.eps, self.wte)[:, 0, : c.vocab_size]
+        return ops.linear(h[:, -1:].contiguous(), self.wte)[:, 0, : c.vocab_size]
 
     @torch.no_grad()
     def _device_position_step(self, tok, cache):
@@ -135,7 +136,8 @@ class GPT2(nn.Module):
         for i, blk in enumerate(self.h):
             x = blk(x, prev, cache=cache, layer=i)
             prev = blk.out_bias()
-        logits = ops.ln_linear(x, self.ln_f.weight, self.ln_f.bias, self.ln_f.eps, self.wte)[:, 0, : c.vocab_size]
+        h = self.ln_f(x, producer_bias=prev)
+        logits = ops.linear(h, self.wte)[:, 0, : c.vocab_size]
         cache.pos_t.add_(1)
         return logits
 

@@ -180,19 +180,3 @@ def batch_norm_nhwc(x, weight, bias, running_mean, running_var, training, moment
     if relu:
         y = F.relu(y)
     return y
-
-
-def ln_linear(x, ln_weight, ln_bias, eps, weight, bias=None, act=None):
-    """act(LayerNorm(x)·weightᵀ + bias) — inference (no autograd).  On the GPU at decode sizes
-    (≤ 64 rows) ONE kernel: the skinny GEMM normalises its operand as it loads it
-    (``torch.ops.replicann.ln_linear``), the LayerNorm output is never written; otherwise
-    LayerNorm then linear."""
-    from .linear import _ACTS, linear
-    a = _ACTS[act] if not isinstance(act, int) else act
-    rows = x.numel() // x.shape[-1]
-    if (_ext.use_native(x) and rows <= 64 and not torch.is_grad_enabled() and x.dtype == torch.bfloat16
-            and weight.dtype == torch.bfloat16 and ln_weight.dtype == torch.bfloat16):
-        y = _ext.ops().ln_linear(x.reshape(rows, x.shape[-1]).contiguous(), ln_weight, ln_bias, float(eps),
-                                 weight, bias, a)
-        return y.reshape(*x.shape[:-1], weight.shape[0])
-    return linear(layer_norm(x, ln_weight, ln_bias, eps), weight, bias, act=a)
