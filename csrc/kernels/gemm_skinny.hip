@@ -77,28 +77,25 @@ __global__ void __launch_bounds__(256) skinny_k(SkArgs p) {
     f32x4 acc[MB];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) acc[mb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // k-steps k_lo + 32·(wave + 4·i): two steps' loads in flight before their MFMAs
+    // k-steps k_lo + 32·(wave + 4·i): FOUR steps' loads in flight before their MFMAs (a decode GEMM's
+    // wave has only a handful of k-steps, so the launch costs about one memory round trip per
+    // iteration); a step past the range loads zeros (its MFMAs add nothing)
     int k = k_lo + 32 * wave;
 #pragma unroll 1
-    for (; k + 128 < k_hi; k += 256) {
-        s16x8 w0 = sk_load(p.W, w_off, k + kg, k_hi, n < p.N), w1 = sk_load(p.W, w_off, k + 128 + kg, k_hi, n < p.N);
-        s16x8 a0[MB], a1[MB];
+    for (; k < k_hi; k += 512) {
+        s16x8 wf[4], af[4][MB];
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-            a0[mb] = sk_load(p.A, a_off[mb], k + kg, k_hi, a_ok[mb]);
-            a1[mb] = sk_load(p.A, a_off[mb], k + 128 + kg, k_hi, a_ok[mb]);
+        for (int u = 0; u < 4; ++u) {
+            const int kk = k + 128 * u + kg;
+            wf[u] = sk_load(p.W, w_off, kk, k_hi, n < p.N);
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) af[u][mb] = sk_load(p.A, a_off[mb], kk, k_hi, a_ok[mb]);
         }
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[mb], w0, acc[mb], 0, 0, 0);
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[mb], w1, acc[mb], 0, 0, 0);
-    }
-    if (k < k_hi) {
-        const s16x8 w0 = sk_load(p.W, w_off, k + kg, k_hi, n < p.N);
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sk_load(p.A, a_off[mb], k + kg, k_hi, a_ok[mb]), w0,
-                                                              acc[mb], 0, 0, 0);
+            for (int mb = 0; mb < MB; ++mb)
+                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u][mb], wf[u], acc[mb], 0, 0, 0);
     }
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) red[wave][mb][lane] = acc[mb];
