@@ -67,6 +67,8 @@ int rn_gemm(const void*, const void*, void*, const void*, const void*, void*, fl
             long, long, long, int, int, int, int, int, int, int, hipStream_t, float*);
 int rn_gemm_cfg_bm(int);
 long rn_gemm_colpart_rows(int, int);
+int rn_attn_decode(const void*, const void*, const void*, const float*, void*, int, int, int, int, const long*, float,
+                   hipStream_t);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
                 int, int, float, int, float, uint64_t, const uint64_t*, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
@@ -679,6 +681,30 @@ void strides_bth(const Tensor& t, std::vector<long>& s) {
     TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "attention tensors must be (B, T, H, D) with unit D stride");
     s.push_back(t.stride(0)); s.push_back(t.stride(1)); s.push_back(t.stride(2));
 }
+// one-query attention over a KV cache (decode step, attention_decode.hip): q (B, 1, H, 64), k / v
+// (B, Tk, H, 64) strided views, mask: Tk fp32 additive shared by the batch (or none)
+Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& mask, double scale) {
+    CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); GUARD(q);
+    TORCH_CHECK(q.dim() == 4 && q.size(1) == 1, "attn_decode: one query per (batch, head)");
+    const int B = q.size(0), H = q.size(2), D = q.size(3), Tk = k.size(1);
+    TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(2) == H && v.size(1) == Tk, "attn_decode: shape mismatch");
+    if (mask && mask->defined())
+        TORCH_CHECK(mask->scalar_type() == at::kFloat && mask->is_contiguous() && mask->numel() == Tk,
+                    "attn_decode: mask must be Tk contiguous fp32 values");
+    Tensor o = at::empty({B, 1, H, D}, q.options());
+    std::vector<long> s;
+    std::vector<long> t;
+    strides_bth(q, t); s.push_back(t[0]); s.push_back(t[2]); t.clear();
+    strides_bth(k, t); s.insert(s.end(), t.begin(), t.end()); t.clear();
+    strides_bth(v, t); s.insert(s.end(), t.begin(), t.end()); t.clear();
+    strides_bth(o, t); s.push_back(t[0]); s.push_back(t[2]);
+    const int rc = rn_attn_decode(q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                  mask && mask->defined() ? mask->data_ptr<float>() : nullptr, o.data_ptr(), B, H, Tk, D,
+                                  s.data(), (float)scale, cur_stream());
+    TORCH_CHECK(rc == 0, "attn_decode: unsupported shape D=", D, " Tk=", Tk, " (D == 64, Tk <= 1024)");
+    return o;
+}
+
 std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& bias,
                                     double scale, bool causal, double p, int64_t seed,
                                     const optional<Tensor>& seed_buf) {
@@ -1096,6 +1122,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("gemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, Tensor? residual, int act, Tensor? preact, "
           "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1, "
           "Tensor(a!)? bias_grad=None) -> Tensor");
+    m.def("attn_decode(Tensor q, Tensor k, Tensor v, Tensor? mask, float scale) -> Tensor");
     m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias, Tensor(a!)? db_accum=None) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
@@ -1169,6 +1196,7 @@ TORCH_LIBRARY(replicann, m) {
 
 TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("gemm", &gemm);
+    m.impl("attn_decode", &attn_decode);
     m.impl("bias_act_grad", &bias_act_grad);
     m.impl("act_fwd", &act_fwd);
     m.impl("act_bwd", &act_bwd);

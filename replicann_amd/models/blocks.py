@@ -100,7 +100,8 @@ class Attention(nn.Module):
             q = qkv[:, :, 0]
             k_all, v_all = cache.update(layer, qkv[:, :, 1:3])
             if cache.device_pos:  # device-position mode: the key mask carries causality
-                a = ops.attention(q, k_all, v_all, bias=cache.mask).reshape(B, T, E)
+                a = (ops.attention_decode(q, k_all, v_all, cache.mask) if T == 1 else
+                     ops.attention(q, k_all, v_all, bias=cache.mask)).reshape(B, T, E)
             else:
                 a = ops.attention(q, k_all, v_all, causal=self.causal).reshape(B, T, E)
             return self.c_proj(a, residual=residual)

@@ -174,3 +174,19 @@ def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dro
         return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed, producer_bias)
     q, k, v = qkv.unbind(2)
     return attention_reference(q, k, v, scale, causal, bias, p, training)
+
+
+def attention_decode(q, k, v, mask=None, scale=None):
+    """One new query per (batch, head) against a KV cache — q (B, 1, H, D), k / v (B, Tk, H, D) —
+    with an additive key mask (Tk values shared by the batch, or None).  Inference only.  On the GPU
+    at head size 64 one launch of the one-query kernel (csrc/kernels/attention_decode.hip: a workgroup
+    per (batch, head), no query tiling); otherwise the general attention."""
+    B, Tq, H, D = q.shape
+    if scale is None:
+        scale = D ** -0.5
+    Tk = k.shape[1]
+    if _ext.use_native(q) and Tq == 1 and D == 64 and Tk <= 1024 and not torch.is_grad_enabled():
+        m = mask.reshape(-1) if mask is not None else None
+        if m is None or (m.numel() == Tk and m.dtype == torch.float32 and m.is_contiguous()):
+            return _ext.ops().attn_decode(q, k, v, m, float(scale))
+    return attention(q, k, v, scale=scale, bias=mask)

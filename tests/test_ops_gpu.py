@@ -150,6 +150,25 @@ def test_gemm_skinny_decode(cuda, M, N, K, split):
     assert o32.dtype == torch.float32 and rel_err(o32, a.float() @ w.float().t()) < 5e-3
 
 
+@pytest.mark.parametrize("B,H,Tk", [(1, 12, 256), (3, 2, 19), (64, 12, 129), (2, 4, 1024)])
+def test_attention_decode_one_query(cuda, B, H, Tk):
+    """One-query attention over a strided K|V cache view with an additive key mask (the captured
+    decode step's form) against fp32 math."""
+    torch.manual_seed(B * H + Tk)
+    qkv = bf(B, 1, 3, H, 64)
+    kv = bf(B, Tk + 5, 2, H, 64)  # a longer buffer: the kernel reads the first Tk rows of strided views
+    q, k, v = qkv[:, :, 0], kv[:, :Tk, 0], kv[:, :Tk, 1]
+    mask = torch.zeros(1, 1, Tk, device="cuda")
+    mask[..., Tk * 2 // 3:] = float("-inf")
+    with torch.no_grad():
+        o = ops.attention_decode(q, k, v, mask)
+    ref = ops.attention_reference(q, k, v, 64 ** -0.5, bias=mask)
+    assert o.shape == (B, 1, H, 64) and rel_err(o, ref) < 1e-2
+    with torch.no_grad():
+        o2 = ops.attention_decode(q, k, v, None)
+    assert rel_err(o2, ops.attention_reference(q, k, v, 64 ** -0.5)) < 1e-2
+
+
 def test_gemm_skinny_rejects_other_layouts(cuda):
     a, w = bf(16, 64), bf(64, 32)
     with pytest.raises(RuntimeError):
