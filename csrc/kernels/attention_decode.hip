@@ -6,9 +6,10 @@
 // The tiled flash kernels spend a 256-thread block with one live query row per (b, h) here and walk
 // the keys 64 at a time through LDS (≈ 9 µs per layer, profiles/decode_steady_r4w.txt).  This kernel
 // is shaped for one query: one workgroup per (b, h); scores with one key per thread (the q vector in
-// registers, 8 × 16-byte loads of the key row), a block max / sum, then P·V with thread (d, group) =
-// (t % 64, t / 64): 64 lanes read one 128-byte value row per key, 4 key groups merged in LDS in a
-// fixed order.  Deterministic, no atomics.  Tk <= 4 · 256 = 1024 keys (GPT-2's context).
+// registers, 8 × 16-byte loads of the key row), a block max / sum, then P·V with thread (8-column
+// chunk, key group) = (t % 8, t / 8): 16-byte value loads, ≤ Tk / 32 independent iterations per
+// thread, the 32 key groups merged in LDS in a fixed order.  Deterministic, no atomics.
+// Tk <= 4 · 256 = 1024 keys (GPT-2's context).
 #include "common.h"
 
 namespace {
@@ -22,7 +23,7 @@ __global__ void __launch_bounds__(DEC_T) attn_decode64_k(const bf16* __restrict_
                                                          long v_sh, long o_sb, long o_sh, float scale) {
     __shared__ float p_s[DEC_T * DEC_KPT];
     __shared__ float red[DEC_T / 64];
-    __shared__ float part[4][64];
+    __shared__ float part[32][64];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int b = blockIdx.x / H, h = blockIdx.x % H;
     const float sl2 = scale * 1.4426950408889634f;
@@ -67,16 +68,26 @@ __global__ void __launch_bounds__(DEC_T) attn_decode64_k(const bf16* __restrict_
     if (lane == 0) red[wave] = l;
     __syncthreads();
     l = red[0] + red[1] + red[2] + red[3];
-    // P·V: thread (d = lane, key group = wave) over keys wave, wave + 4, ...
-    const bf16* vb = v + b * v_sb + h * v_sh + lane;
-    float acc = 0.f;
-#pragma unroll 8
-    for (int j = wave; j < Tk; j += 4) acc = fmaf(p_s[j], (float)vb[(long)j * v_st], acc);
-    part[wave][lane] = acc;
+    // P·V: thread (8-column chunk t % 8, key group t / 8) over keys t/8, t/8 + 32, ...: 16-byte value
+    // loads, at most Tk / 32 independent iterations per thread; the 32 groups are summed in order
+    const int dc = t & 7, kgp = t >> 3;
+    const bf16* vb = v + b * v_sb + h * v_sh + dc * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int j = kgp; j < Tk; j += 32) {
+        float vf[8];
+        load8(vb + (long)j * v_st, vf);
+        const float pj = p_s[j];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(pj, vf[e], acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[kgp][dc * 8 + e] = acc[e];
     __syncthreads();
-    if (wave == 0) {
-        const float tot = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-        o[b * o_sb + h * o_sh + lane] = (bf16)(l > 0.f ? tot / l : 0.f);
+    if (t < 64) {
+        float tot = 0.f;
+        for (int g = 0; g < 32; ++g) tot += part[g][t];
+        o[b * o_sb + h * o_sh + t] = (bf16)(l > 0.f ? tot / l : 0.f);
     }
 }
 
