@@ -166,9 +166,9 @@ class GPT2(nn.Module):
         return graph, tok, out
 
     @torch.no_grad()
-    def generate(self, idx, max_new_tokens, *, temperature=1.0, top_k=None, generator=None, graph=None):
+    def generate(self, idx, max_new_tokens, *, temperature=1.0, top_k=None, top_p=None, generator=None, graph=None):
         """Autoregressive sampling with a KV cache: ``idx`` (B, T0) prompt → (B, T0 + max_new_tokens).
-        ``temperature`` 0 = greedy.  One prefill pass over the prompt, then one-token steps whose
+        ``temperature`` 0 = greedy; ``top_k`` / ``top_p`` restrict sampling.  One prefill pass over the prompt, then one-token steps whose
         attention reads the cached keys / values (no recomputation of the prefix).  ``graph``
         (default: on for GPU models): the one-token step is captured once as a hipGraph and replayed
         (per-step values live on the device), so a step costs its kernels, not ~130 host launches."""
@@ -197,7 +197,7 @@ class GPT2(nn.Module):
             logits = self.decode_step(idx, cache)
             out = [idx]
             for i in range(max_new_tokens):
-                nxt = _sample(logits.float(), temperature, top_k, generator)
+                nxt = _sample(logits.float(), temperature, top_k, generator, top_p)
                 out.append(nxt)
                 if i + 1 == max_new_tokens:
                     break
@@ -238,13 +238,21 @@ class GPT2(nn.Module):
         return 6 * n_mm + 3 * attn
 
 
-def _sample(logits, temperature, top_k, generator):
-    """(B, V) fp32 logits → (B, 1) next-token ids."""
+def _sample(logits, temperature, top_k, generator, top_p=None):
+    """(B, V) fp32 logits → (B, 1) next-token ids: greedy (temperature 0), else sampling from the
+    temperature-scaled softmax restricted to the top-k logits and / or the smallest set of tokens
+    whose probability mass reaches top_p (nucleus)."""
     if temperature == 0:
         return logits.argmax(-1, keepdim=True)
     logits = logits / temperature
     if top_k is not None and top_k < logits.shape[-1]:
         kth = torch.topk(logits, top_k, dim=-1).values[:, -1:]
         logits = logits.masked_fill(logits < kth, float("-inf"))
+    if top_p is not None and top_p < 1.0:
+        srt, idx = torch.sort(logits, dim=-1, descending=True)
+        cum = torch.softmax(srt, -1).cumsum(-1)
+        drop = cum - torch.softmax(srt, -1) >= top_p  # mass BEFORE a token already reaches top_p
+        srt = srt.masked_fill(drop, float("-inf"))
+        logits = torch.full_like(logits, float("-inf")).scatter(-1, idx, srt)
     probs = torch.softmax(logits, -1)
     return torch.multinomial(probs, 1, generator=generator)

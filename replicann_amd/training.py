@@ -482,6 +482,7 @@ def generate_main(argv=None):
     ap.add_argument("--new", type=int, default=32)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--top-k", type=int, default=None)
+    ap.add_argument("--top-p", type=float, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default=None)
     ap.add_argument("--model-kwargs", type=json.loads, default={})
@@ -505,7 +506,7 @@ def generate_main(argv=None):
         ids = torch.randint(0, model.config.vocab_size, (a.batch_size, a.prompt_len))
     gen = torch.Generator(device=dev).manual_seed(a.seed)
     t0 = time.perf_counter()
-    out = model.generate(ids.to(dev), a.new, temperature=a.temperature, top_k=a.top_k, generator=gen)
+    out = model.generate(ids.to(dev), a.new, temperature=a.temperature, top_k=a.top_k, top_p=a.top_p, generator=gen)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0

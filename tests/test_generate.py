@@ -97,3 +97,19 @@ def test_generate_cli_from_checkpoint(tmp_path, capsys):
     res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     want = m.generate(torch.tensor([prompt]), 6, temperature=0)[0, 4:].tolist()
     assert res["tokens"] == [want] and res["new_tokens"] == 6
+
+
+def test_top_p_nucleus():
+    """top_p keeps the smallest set of most probable tokens reaching the mass (always the top one)."""
+    from replicann_amd.models.gpt2 import _sample
+    lg = torch.log(torch.tensor([[0.5, 0.3, 0.15, 0.05], [0.9, 0.05, 0.03, 0.02]]))
+    g = torch.Generator().manual_seed(0)
+    seen = {0: set(), 1: set()}
+    for _ in range(300):
+        t = _sample(lg.clone(), 1.0, None, g, top_p=0.75)
+        seen[0].add(int(t[0])), seen[1].add(int(t[1]))
+    assert seen[0] == {0, 1} and seen[1] == {0}
+    m = _model()
+    out = m.generate(torch.zeros(2, 3, dtype=torch.long), 5, temperature=1.0, top_p=0.9,
+                     generator=torch.Generator().manual_seed(1))
+    assert out.shape == (2, 8)
