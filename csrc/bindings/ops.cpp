@@ -69,6 +69,8 @@ int rn_gemm_cfg_bm(int);
 long rn_gemm_colpart_rows(int, int);
 int rn_attn_decode(const void*, const void*, const void*, const float*, void*, int, int, int, int, const long*, float,
                    hipStream_t);
+int rn_gemm_skinny_kv(const void*, const void*, const void*, void*, int, int, int, long, long, long, void*,
+                      const int64_t*, long, long, int, hipStream_t);
 int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const float*, int, const long*, int, int, int,
                 int, int, float, int, float, uint64_t, const uint64_t*, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
@@ -681,6 +683,26 @@ void strides_bth(const Tensor& t, std::vector<long>& s) {
     TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "attention tensors must be (B, T, H, D) with unit D stride");
     s.push_back(t.stride(0)); s.push_back(t.stride(1)); s.push_back(t.stride(2));
 }
+// decode-step QKV projection with the K|V cache append fused into the epilogue (gemm_skinny.hip):
+// x (M, K), w (N, K), kv (M, L, 2, H, D) contiguous cache, pos: 1 int64 device row index
+Tensor linear_kv(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const Tensor& kv, const Tensor& pos) {
+    CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(kv); GUARD(x);
+    TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.stride(1) == 1, "linear_kv: 2-D row-major operands");
+    const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+    TORCH_CHECK(w.size(1) == K, "linear_kv: inner dims differ");
+    TORCH_CHECK(kv.dim() == 5 && kv.is_contiguous() && kv.size(0) == M && kv.size(2) == 2, "linear_kv: kv must be (M, L, 2, H, D)");
+    const int64_t kvw = kv.size(2) * kv.size(3) * kv.size(4);
+    TORCH_CHECK(kvw <= N, "linear_kv: cache row wider than the projection");
+    TORCH_CHECK(pos.scalar_type() == at::kLong && pos.numel() == 1 && pos.is_cuda(), "linear_kv: pos must be 1 int64 on the device");
+    if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
+    Tensor c = at::empty({M, N}, x.options());
+    const int rc = rn_gemm_skinny_kv(x.data_ptr(), w.data_ptr(), optr(bias), c.data_ptr(), (int)M, (int)N, (int)K,
+                                     x.stride(0), w.stride(0), c.stride(0), kv.data_ptr(), pos.data_ptr<int64_t>(),
+                                     kv.stride(0), kv.stride(1), (int)(N - kvw), cur_stream());
+    TORCH_CHECK(rc == 0, "linear_kv: unsupported shape M=", M, " K=", K, " (M <= 64, K % 8 == 0)");
+    return c;
+}
+
 // one-query attention over a KV cache (decode step, attention_decode.hip): q (B, 1, H, 64), k / v
 // (B, Tk, H, 64) strided views, mask: Tk fp32 additive shared by the batch (or none)
 Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& mask, double scale) {
@@ -1123,6 +1145,7 @@ TORCH_LIBRARY(replicann, m) {
           "Tensor? out, bool accumulate, int split_k, bool out_fp32, Tensor? alpha=None, int cfg=-1, "
           "Tensor(a!)? bias_grad=None) -> Tensor");
     m.def("attn_decode(Tensor q, Tensor k, Tensor v, Tensor? mask, float scale) -> Tensor");
+    m.def("linear_kv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) kv, Tensor pos) -> Tensor");
     m.def("bias_act_grad(Tensor dy, Tensor? h, int act, bool want_bias, Tensor(a!)? db_accum=None) -> (Tensor, Tensor)");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
@@ -1197,6 +1220,7 @@ TORCH_LIBRARY(replicann, m) {
 TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("gemm", &gemm);
     m.impl("attn_decode", &attn_decode);
+    m.impl("linear_kv", &linear_kv);
     m.impl("bias_act_grad", &bias_act_grad);
     m.impl("act_fwd", &act_fwd);
     m.impl("act_bwd", &act_bwd);

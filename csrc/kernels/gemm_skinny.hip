@@ -32,6 +32,12 @@ struct SkArgs {
     int M, N, K, S, kc;  // kc: K range per split (multiple of 32)
     long lda, ldw, ldc;
     int out_f32;
+    // K|V append (rn_gemm_skinny_kv, the decode step's QKV projection): output columns >= kv_c0 are
+    // also stored into the KV cache row *kv_pos of batch row m: kvd[m·kv_sb + pos·kv_row + n − kv_c0]
+    bf16* kvd;
+    const int64_t* kv_pos;
+    long kv_sb, kv_row;
+    int kv_c0;
 };
 
 template <int ACT>
@@ -50,6 +56,7 @@ RN_DEV void sk_store(const SkArgs& p, int m, int n, float v) {
     if (p.res) v += (float)p.res[(long)m * p.ldc + n];
     if (p.out_f32) reinterpret_cast<float*>(p.C)[(long)m * p.ldc + n] = v;
     else reinterpret_cast<bf16*>(p.C)[(long)m * p.ldc + n] = (bf16)v;
+    if (p.kvd && n >= p.kv_c0) p.kvd[(long)m * p.kv_sb + (long)*p.kv_pos * p.kv_row + (n - p.kv_c0)] = (bf16)v;
 }
 
 RN_DEV s16x8 sk_load(const bf16* base, long row_off, int k, int K, bool row_ok) {
@@ -169,5 +176,22 @@ extern "C" int rn_gemm_skinny(const void* A, const void* W, void* C, const void*
         case ACT_GELU_D: sk_launch<ACT_GELU_D>(a, mb, st); break;
         default: sk_launch<ACT_NONE>(a, mb, st); break;
     }
+    return 0;
+}
+
+// Decode step QKV projection with the K|V append fused: out = x·Wᵀ + bias (M <= 64 rows = batch
+// rows, one new token each) and its columns >= kv_c0 (keys, values) also written into the KV cache
+// at the device-side row *kv_pos — the separate index_copy of every layer's keys / values is gone.
+extern "C" int rn_gemm_skinny_kv(const void* x, const void* W, const void* bias, void* C, int M, int N, int K,
+                                 long ldx, long ldw, long ldc, void* kvd, const int64_t* kv_pos, long kv_sb,
+                                 long kv_row, int kv_c0, hipStream_t st) {
+    if (M < 1 || M > 64 || K % 8 != 0 || ldx % 8 != 0 || ldw % 8 != 0 || kv_c0 < 0 || kv_c0 > N) return -1;
+    SkArgs a = {};
+    a.A = (const bf16*)x; a.W = (const bf16*)W; a.C = C; a.bias = (const bf16*)bias;
+    a.M = M; a.N = N; a.K = K; a.lda = ldx; a.ldw = ldw; a.ldc = ldc;
+    a.S = 1;
+    a.kc = (K + 31) / 32 * 32;
+    a.kvd = (bf16*)kvd; a.kv_pos = kv_pos; a.kv_sb = kv_sb; a.kv_row = kv_row; a.kv_c0 = kv_c0;
+    sk_launch<ACT_NONE>(a, (M + 15) / 16, st);
     return 0;
 }

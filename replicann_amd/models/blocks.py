@@ -95,6 +95,13 @@ class Attention(nn.Module):
         cache position and the queries attend to everything cached so far (causal, bottom-right
         aligned: query i of T new tokens sees keys ≤ pos + i)."""
         B, T, E = h.shape
+        if cache is not None and cache.device_pos and T == 1 and self.c_attn.fp8_state is None:
+            # captured decode step: the projection's epilogue appends this token's key / value row
+            buf = cache.kv[layer]
+            qkv = ops.linear_kv_append(h, self.c_attn.weight, self.c_attn.bias, buf, cache.pos_t)
+            q = qkv.view(B, T, 3, self.n_head, E // self.n_head)[:, :, 0]
+            a = ops.attention_decode(q, buf[:, :, 0], buf[:, :, 1], cache.mask).reshape(B, T, E)
+            return self.c_proj(a, residual=residual)
         qkv = self.c_attn(h).view(B, T, 3, self.n_head, E // self.n_head)
         if cache is not None:
             q = qkv[:, :, 0]

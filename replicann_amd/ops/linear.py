@@ -250,6 +250,21 @@ def linear(x, weight, bias=None, act=None, residual=None, fp8=None):
     return _LinearFn.apply(x, weight, bias, a, residual, fp8)
 
 
+def linear_kv_append(x, weight, bias, kv, pos):
+    """Decode-step QKV projection: y = x·weightᵀ + bias for one new token per batch row (x (B, 1, K)),
+    and y's last 2·H·D columns (keys, values) written into the KV cache buffer ``kv`` (B, L, 2, H, D)
+    at the device-side row ``pos`` (1 int64).  Inference only.  On the GPU one launch: the append
+    is part of the skinny GEMM's epilogue (``torch.ops.replicann.linear_kv``)."""
+    B = x.shape[0]
+    if (_ext.use_native(x) and x.dim() == 3 and x.shape[1] == 1 and B <= 64 and not torch.is_grad_enabled()
+            and kv.is_contiguous()):
+        return _ext.ops().linear_kv(x.reshape(B, -1).contiguous(), weight, bias, kv, pos).view(B, 1, -1)
+    y = linear(x, weight, bias)
+    w = kv[0, 0].numel()
+    kv.index_copy_(1, pos, y[..., -w:].reshape(B, y.shape[1], *kv.shape[2:]))
+    return y
+
+
 # --------------------------------------------------------------------------
 # fused two-layer MLP: y = act(x·W1ᵀ + b1)·W2ᵀ + b2 (+ residual)
 # --------------------------------------------------------------------------

@@ -169,6 +169,26 @@ def test_attention_decode_one_query(cuda, B, H, Tk):
     assert rel_err(o2, ops.attention_reference(q, k, v, 64 ** -0.5)) < 1e-2
 
 
+@pytest.mark.parametrize("B,H", [(1, 12), (5, 2), (64, 12)])
+def test_linear_kv_append(cuda, B, H):
+    """Decode QKV projection with the K|V cache append in the epilogue: the output equals the plain
+    GEMM, cache row pos holds its key / value columns, every other row is untouched."""
+    torch.manual_seed(B + H)
+    E, L = 64 * H, 40
+    x, w, bias = bf(B, 1, E), bf(3 * E, E, scale=0.05), bf(3 * E, scale=0.1)
+    kv = bf(B, L, 2, H, 64)
+    before = kv.clone()
+    pos = torch.tensor([17], device="cuda")
+    with torch.no_grad():
+        y = ops.linear_kv_append(x, w, bias, kv, pos)
+    ref = ops.gemm(x.reshape(B, E), w, tb=True, bias=bias)
+    assert y.shape == (B, 1, 3 * E) and rel_err(y.reshape(B, -1), ref) < 1e-2
+    assert torch.equal(kv[:, 17].reshape(B, -1), y.reshape(B, -1)[:, E:])
+    keep = torch.ones(L, dtype=torch.bool)
+    keep[17] = False
+    assert torch.equal(kv[:, keep], before[:, keep])
+
+
 def test_gemm_skinny_rejects_other_layouts(cuda):
     a, w = bf(16, 64), bf(64, 32)
     with pytest.raises(RuntimeError):
