@@ -16,6 +16,7 @@ MI355X-specific choices:
 
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -59,6 +60,9 @@ class GPT2Config:
         d = dict(n_layer=2, n_head=4, n_embd=128, block_size=128, vocab_size=1000, vocab_pad=1024)
         d.update(kw)
         return GPT2Config(**d)
+
+
+_DECODE_GRAPHS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 class GPT2(nn.Module):
@@ -219,15 +223,14 @@ class GPT2(nn.Module):
 
     def _decode_graphs(self):
         """Captured decode steps kept across ``generate`` calls, keyed by (batch, total length, dtype,
-        device, parameter storage): a serving loop with fixed shapes captures once.  Each holds its KV cache (2 ·
-        n_layer · B · length · n_embd elements); ``clear_decode_graphs`` frees them."""
-        d = self.__dict__.get("_rn_decode_graphs")
-        if d is None:
-            d = self.__dict__["_rn_decode_graphs"] = {}
-        return d
+        device, parameter storage): a serving loop with fixed shapes captures once.  Each holds its KV
+        cache (2 · n_layer · B · length · n_embd elements); ``clear_decode_graphs`` frees them.  Kept
+        outside the module's attributes (a weak-keyed registry), so copying / pickling the model
+        never touches graph objects."""
+        return _DECODE_GRAPHS.setdefault(self, {})
 
     def clear_decode_graphs(self):
-        self.__dict__.pop("_rn_decode_graphs", None)
+        _DECODE_GRAPHS.pop(self, None)
 
     def flops_per_token(self, T=None):
         """Training FLOPs per token (fwd+bwd): 6·N_matmul + attention (causal)."""

@@ -113,3 +113,12 @@ def test_top_p_nucleus():
     out = m.generate(torch.zeros(2, 3, dtype=torch.long), 5, temperature=1.0, top_p=0.9,
                      generator=torch.Generator().manual_seed(1))
     assert out.shape == (2, 8)
+
+
+def test_model_copy_after_generate():
+    """Stored decode graphs / caches live outside the module: deepcopy and state_dict are unaffected."""
+    import copy
+    m = _model()
+    m.generate(torch.zeros(1, 3, dtype=torch.long), 4, temperature=0, graph=False)
+    m2 = copy.deepcopy(m)
+    assert set(m2.state_dict()) == set(m.state_dict())
