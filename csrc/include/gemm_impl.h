@@ -71,6 +71,10 @@ struct GemmArgs {
     // split-K reduction only: slab s lives at ws + s·slab_step·M·N (<= 1: contiguous slabs); set when
     // a group pre-reduction (splitk_group_k) left its partial sums in every slab_step-th slab
     int slab_step;
+    // one-wave-per-SIMD kernel (cfg 11, gemm_w1.h), fp8 operands: the two per-tensor scales (powers of
+    // two, ops/fp8.py) ride the scaled MFMA's E8M0 block-scale operands instead of an epilogue multiply
+    const float* sa;
+    const float* sb;
 };
 
 template <int BN, int NT>

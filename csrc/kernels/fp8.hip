@@ -16,6 +16,20 @@ namespace {
 
 constexpr float E4M3_MAX = 448.f;
 
+// Every per-tensor scale is rounded UP to a power of two (never more clipping than the exact scale:
+// q = x / s stays within the format's range), so that a scale is an exact E8M0 exponent: the
+// one-wave-per-SIMD GEMM (gemm_w1.h) feeds the two tensors' exponents to the scaled MFMA's block-
+// scale operands instead of multiplying every output by sa·sb (the same bits as the multiply: a
+// product of powers of two is exact).
+__device__ inline float pow2_ceil(float s) {
+    if (!(s > 0.f)) return 1.f;
+    uint32_t u = __float_as_uint(s);
+    const uint32_t e = u & 0x7F800000u;
+    if (e == 0x7F800000u) return s;  // inf / nan pass through
+    u = (u & 0x007FFFFFu) ? e + 0x00800000u : e;
+    return __uint_as_float(u ? u : 0x00800000u);  // (subnormal: the smallest normal)
+}
+
 __global__ void __launch_bounds__(256) amax_k(const bf16* __restrict__ x, long n, float* __restrict__ state) {
     __shared__ float sm[16];
     float m = 0.f;
@@ -35,7 +49,7 @@ __global__ void __launch_bounds__(256) amax_k(const bf16* __restrict__ x, long n
 __global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
                                                float* __restrict__ state) {
     const float amax = state[1];
-    const float scale = amax > 0.f ? amax / E4M3_MAX : 1.f;
+    const float scale = amax > 0.f ? pow2_ceil(amax / E4M3_MAX) : 1.f;
     const float inv = 1.f / scale;
     if (blockIdx.x == 0 && threadIdx.x == 0) state[0] = scale;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
@@ -62,7 +76,7 @@ __global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long 
 __device__ inline void fp8_roll_k_body(float* __restrict__ state) {
     const float a = state[1];
     state[2] = a;
-    state[0] = a > 0.f ? 2.f * a / E4M3_MAX : 1.f;
+    state[0] = a > 0.f ? pow2_ceil(2.f * a / E4M3_MAX) : 1.f;
     state[1] = 0.f;
 }
 __global__ void fp8_roll_k(float* __restrict__ state) { fp8_roll_k_body(state); }
@@ -105,7 +119,7 @@ constexpr float E5M2_MAX = 57344.f;
 __global__ void fp8_roll_bf8_k(float* __restrict__ state) {
     const float a = state[1];
     state[2] = a;
-    state[0] = a > 0.f ? 2.f * a / E5M2_MAX : 1.f;
+    state[0] = a > 0.f ? pow2_ceil(2.f * a / E5M2_MAX) : 1.f;
     state[1] = 0.f;
 }
 __global__ void __launch_bounds__(256) quant_delayed_bf8_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
@@ -141,7 +155,7 @@ __global__ void __launch_bounds__(256) quant_delayed_bf8_k(const bf16* __restric
 __global__ void __launch_bounds__(256) quant_bf8_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
                                                    float* __restrict__ state) {
     const float amax = state[1];
-    const float scale = amax > 0.f ? amax / E5M2_MAX : 1.f;
+    const float scale = amax > 0.f ? pow2_ceil(amax / E5M2_MAX) : 1.f;
     const float inv = 1.f / scale;
     if (blockIdx.x == 0 && threadIdx.x == 0) state[0] = scale;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
@@ -230,16 +244,19 @@ inline int gridn(long n) {
     return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
-// REPLICANN_FP8_GEMM: unset = by shape, 0 = one-tile-per-block 256x192, 9 = persistent 256x256
+// REPLICANN_FP8_GEMM: unset = by shape, 0 = one-tile-per-block 256x192, 9 = persistent 256x256,
+// 11 = one-wave-per-SIMD persistent 256x256 (gemm_w1.h)
 int fp8_gemm_kernel() {
     const char* e = std::getenv("REPLICANN_FP8_GEMM");
     if (!e || !e[0]) return -1;  // by shape
-    return e[0] == '0' ? 0 : 9;
+    const int v = std::atoi(e);
+    return v == 0 ? 0 : (v == 11 ? 11 : 9);
 }
 
 }  // namespace
 
 void rn_gemm_launch_pk_fp8(rn_gemm_detail::GemmArgs& a, int act, hipStream_t st);
+int rn_gemm_launch_w1(rn_gemm_detail::GemmArgs& a, int fp8, int act, hipStream_t st);
 void rn_gemm_launch_pk_fp8_wgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 void rn_gemm_launch_pk_fp8_dgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 
@@ -316,6 +333,12 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     // at K = 1024 (1.32 vs 1.59 PF/s: 8 K-tiles per output tile, the per-tile epilogue dominates),
     // so by default it takes K >= 2048 only; REPLICANN_FP8_GEMM=9 forces it, =0 never.
     const int kern = fp8_gemm_kernel();
+    if (kern == 11 && !q8 && !res && act == ACT_NONE) {
+        rn_gemm_detail::GemmArgs w = {};
+        w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C; w.bias = (const bf16*)bias;
+        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
+        if (rn_gemm_launch_w1(w, 1, ACT_NONE, st) == 0) return 0;
+    }
     if (!q8 && N % 8 == 0 && ldc % 8 == 0 && (kern == 9 || (kern < 0 && K >= 2048))) {
         a.tiles_m = (M + 255) / 256;
         a.tiles_n = (N + 255) / 256;

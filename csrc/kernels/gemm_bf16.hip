@@ -51,6 +51,7 @@ using rn_gemm_detail::GemmArgs;
 using rn_gemm_detail::BK;
 
 void rn_gemm_launch_cfg0(GemmArgs&, bool, bool, int, hipStream_t);
+int rn_gemm_launch_w1(GemmArgs& a, int fp8, int act, hipStream_t st);  // gemm_w1.hip (cfg 11)
 void rn_gemm_launch_cfg1(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg2(GemmArgs&, bool, bool, int, hipStream_t);
 void rn_gemm_launch_cfg3(GemmArgs&, bool, bool, int, hipStream_t);
@@ -207,7 +208,7 @@ long rn_gemm_ws_floats(int M, int N, int split) { return split > 1 ? (long)split
 int rn_gemm_cfg_bm(int cfg) { return (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 9) ? 128 : 256; }
 // rows of the column-partial matrix a config writes (cfg 9: one row per (256-row tile, wave row))
 long rn_gemm_colpart_rows(int cfg, int M) {
-    return cfg == 9 ? 2L * ((M + 255) / 256) : (long)((M + rn_gemm_cfg_bm(cfg) - 1) / rn_gemm_cfg_bm(cfg));
+    return (cfg == 9) ? 2L * ((M + 255) / 256) : (long)((M + rn_gemm_cfg_bm(cfg) - 1) / rn_gemm_cfg_bm(cfg));
 }
 
 int rn_gemm_skinny(const void* A, const void* W, void* C, const void* bias, const void* res, void* pre, float* ws,
@@ -226,6 +227,15 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     if (!trans_a && lda % 8 != 0) return -1;
     if (!trans_b && (N % 8 != 0 || ldb % 8 != 0)) return -1;
     if (trans_b && ldb % 8 != 0) return -1;
+    if (cfg == 11) {  // one-wave-per-SIMD persistent kernel (gemm_w1.h): x·Wᵀ, plain / bias epilogue
+        if (!trans_a && trans_b && act == ACT_NONE && !res && !accumulate && !out_f32 && split <= 1 && !colpart) {
+            GemmArgs w = {};
+            w.A = (const bf16*)A; w.B = (const bf16*)B; w.C = C; w.bias = (const bf16*)bias; w.alpha = alpha;
+            w.M = M; w.N = N; w.K = K * 2; w.lda = lda * 2; w.ldb = ldb * 2; w.ldc = ldc;
+            if (rn_gemm_launch_w1(w, 0, act, st) == 0) return 0;
+        }
+        cfg = 9;
+    }
     GemmArgs a = {};
     a.A = (const bf16*)A; a.B = (const bf16*)B; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
     a.pre = (bf16*)pre; a.ws = ws; a.alpha = alpha; a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;

@@ -33,12 +33,24 @@ FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "0") == "1"
 FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "0") == "1"
 
 
+def pow2_ceil(s):
+    """The smallest power of two >= s (float32, exact; 1 for s <= 0): every fp8 scale is one, so the
+    one-wave-per-SIMD GEMM can feed the tensors' exponents to the scaled MFMA (csrc/kernels/fp8.hip,
+    pow2_ceil)."""
+    s = torch.as_tensor(s, dtype=torch.float32)
+    if not bool(s > 0):
+        return torch.tensor(1.0)
+    m, e = torch.frexp(s)  # s = m · 2^e, m in [0.5, 1)
+    e = torch.where(m == 0.5, e - 1, e)
+    return torch.ldexp(torch.tensor(1.0), e).float()
+
+
 def quantize_fp8(x):
-    """(q uint8 e4m3 storage, state[0] = scale) with x ≈ q·scale."""
+    """(q uint8 e4m3 storage, state[0] = scale) with x ≈ q·scale (scale a power of two)."""
     if _ext.use_native(x):
         return _ext.ops().fp8_quantize(x.contiguous())
     amax = x.detach().abs().max().float()
-    scale = amax / E4M3_MAX if amax > 0 else torch.tensor(1.0)
+    scale = pow2_ceil(amax / E4M3_MAX) if amax > 0 else torch.tensor(1.0)
     q = (x.float() / scale).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
     return q.view(torch.uint8), torch.stack([scale, amax, scale * 0, scale * 0]).float()
 
@@ -52,9 +64,9 @@ def quantize_bf8(x, state, delayed):
     if delayed:
         prev = state[1].clone()
         state[2] = prev
-        scale = 2 * prev / E5M2_MAX if float(prev) > 0 else torch.tensor(1.0)
+        scale = pow2_ceil(2 * prev / E5M2_MAX) if float(prev) > 0 else torch.tensor(1.0)
     else:
-        scale = amax / E5M2_MAX if amax > 0 else torch.tensor(1.0)
+        scale = pow2_ceil(amax / E5M2_MAX) if amax > 0 else torch.tensor(1.0)
     state[0] = scale
     state[1] = amax
     q = (x.float() / scale).clamp(-E5M2_MAX, E5M2_MAX).to(torch.float8_e5m2)
@@ -144,9 +156,11 @@ class Fp8State:
         self.wgrad = FP8_WGRAD
         self.dgrad = FP8_DGRAD
         self.w_cached = False  # the last weight quant() came from the optimizer-refreshed cache
-        self._offer = None  # (activation tensor, its e4m3 copy) written by the producer kernel
+        self._offer = None  # (activation tensor, its e4m3 copy, scale slot) written by the producer kernel
         self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
         self.wcache = None  # Fp8WeightCache holding this GEMM's e4m3 weight (refreshed by the optimizer)
+        self._ti = None  # inference scratch slots (see roll_slot)
+        self.grad_mode = True  # grad mode at the op's entry (autograd Functions run forward under no_grad)
 
     @property
     def t(self):
@@ -195,10 +209,36 @@ class Fp8State:
         can emit the e4m3 activation itself (first call: current scaling in quant())."""
         return self.t is not None and self.t.device == device and self.ready[0] and _ext.use_native(self.t)
 
-    def offer(self, x, q):
-        """A producer quantised ``x`` into ``q`` with this state's activation slot (rolled +
-        amax recorded by that kernel); the next quant(x, 0) of the same tensor returns it."""
-        self._offer = (x, q)
+    def inference(self) -> bool:
+        """Inference (no_grad, or the owning module in eval mode): quantisation must not touch the
+        training slots — evaluate() / generate() between training steps would otherwise roll the
+        delayed scales and record their own batches' amax, which the next training step quantises
+        with."""
+        return not self.grad_mode or (self._owner is not None and not self._owner.training)
+
+    def enter(self):
+        """Record the caller's grad mode; every op that hands this state to an autograd Function
+        calls it before ``apply`` (inside ``forward`` grad mode is always off)."""
+        self.grad_mode = torch.is_grad_enabled()
+        return self
+
+    def roll_slot(self, i):
+        """The scale slot a kernel may ROLL and record an amax into for operand ``i``: the training
+        slot, or under inference a scratch copy of it (same delayed scale, amax discarded), so the
+        training state is read-only outside training steps."""
+        st = self.t[i]
+        if not self.inference():
+            return st
+        if self._ti is None or self._ti.device != st.device:
+            self._ti = torch.zeros(2, 4, device=st.device, dtype=torch.float32)
+        self._ti[i].copy_(st)
+        return self._ti[i]
+
+    def offer(self, x, q, slot=None):
+        """A producer quantised ``x`` into ``q`` with scale slot ``slot`` (this state's activation
+        slot, or its inference copy; rolled + amax recorded by that kernel); the next quant(x, 0) of
+        the same tensor returns it."""
+        self._offer = (x, q, self.t[0] if slot is None else slot)
 
     @property
     def fp8_bwd(self):
@@ -213,20 +253,25 @@ class Fp8State:
                 self.w_cached = True
                 return q, self.t[1]
         if i == 0 and self._offer is not None:
-            src, q = self._offer
+            src, q, slot = self._offer
             self._offer = None
             if src.data_ptr() == x.data_ptr() and src.shape == x.shape:
                 self.fed += 1
-                return q, self.t[0]
+                return q, slot
         if self.t is None or self.t.device != x.device:
             self.t = torch.zeros(2, 4, device=x.device, dtype=torch.float32)
             self.ready = [False, False]
-        st = self.t[i]
         if not self.ready[i] or not _ext.use_native(x):
             q, s = quantize_fp8(x)
+            if self.inference():  # current scaling into the scratch slot: the training slot stays unseeded
+                st = self.roll_slot(i)
+                st.copy_(s)
+                return q, st
+            st = self.t[i]
             st.copy_(s)
             self.ready[i] = True
             return q, st
+        st = self.roll_slot(i)
         return _ext.ops().fp8_quantize_delayed(x, st), st
 
 
@@ -275,8 +320,9 @@ def _fp8_forward_q(x2, xq, xs, wq, ws, bias, res2, act, preact, state, out8):
     if _ext.use_native(x2):
         if (out8 is not None and res2 is None and preact is not None and x2.shape[0] > 0
                 and out8.producer_ready(x2.device)):
-            y, q = _ext.ops().gemm_fp8_q8(xq, wq, xs, ws, bias, act, preact, out8.t[0])
-            out8.offer(y, q)
+            slot = out8.roll_slot(0)
+            y, q = _ext.ops().gemm_fp8_q8(xq, wq, xs, ws, bias, act, preact, slot)
+            out8.offer(y, q, slot)
             return y
         return _ext.ops().gemm_fp8(xq, wq, xs, ws, bias, res2, act, preact)
     h = dequantize_fp8(xq, xs).float() @ dequantize_fp8(wq, ws).float().t()

@@ -247,6 +247,8 @@ def linear(x, weight, bias=None, act=None, residual=None, fp8=None):
     a = _ACTS[act] if not isinstance(act, int) else act
     if fp8 is None and not x.is_cuda and not torch.is_grad_enabled() and residual is None and a == ACT_NONE:
         return F.linear(x, weight, bias)
+    if fp8 is not None:
+        fp8.enter()
     return _LinearFn.apply(x, weight, bias, a, residual, fp8)
 
 
@@ -419,6 +421,10 @@ def mlp(x, w1, b1, w2, b2, act="gelu", residual=None, fp8=None):
     ``fp8``: (Fp8State, Fp8State) of the two layers → e4m3 forward GEMMs."""
     a = _ACTS[act] if not isinstance(act, int) else act
     if _ext.use_native(x) and a in ACT_BWD:
+        if fp8 is not None:
+            for st in fp8:
+                if st is not None:
+                    st.enter()
         return _MLPFn.apply(x, w1, b1, w2, b2, a, residual, fp8)
     f1, f2 = fp8 if fp8 is not None else (None, None)
     return linear(linear(x, w1, b1, act=a, fp8=f1), w2, b2, residual=residual, fp8=f2)

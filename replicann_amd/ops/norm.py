@@ -42,8 +42,9 @@ class _LayerNormFn(torch.autograd.Function):
         r2 = residual.reshape(-1, E).contiguous() if residual is not None else None
         if fp8 is not None and fp8.producer_ready(x2.device):
             # the consumer's e4m3 activation comes out of this kernel (delayed scaling)
-            y, h, mean, rstd, q8 = _ext.ops().layernorm_fwd_q8(x2, r2, weight, bias, eps, fp8.t[0])
-            fp8.offer(y, q8)
+            slot = fp8.roll_slot(0)  # (inference: a scratch copy — the training slot stays untouched)
+            y, h, mean, rstd, q8 = _ext.ops().layernorm_fwd_q8(x2, r2, weight, bias, eps, slot)
+            fp8.offer(y, q8, slot)
         else:
             y, h, mean, rstd = _ext.ops().layernorm_fwd(x2, r2, weight, bias, eps)
         ctx.save_for_backward(x2 if residual is None else h, weight, mean, rstd)
@@ -99,6 +100,8 @@ def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, 
     own quantisation pass.
     """
     if _ext.use_native(x):
+        if fp8 is not None:
+            fp8.enter()
         out = _LayerNormFn.apply(x, weight, bias, eps, residual, return_sum, producer_bias, fp8)
         if residual is None and not return_sum:
             return out

@@ -1,0 +1,98 @@
+"""A/B of the one-wave-per-SIMD persistent GEMM (cfg 11, csrc/include/gemm_w1.h) against the 8-wave
+persistent kernel (cfg 9) and, for fp8, the one-tile-per-block kernel, on the GPT-2 forward shapes
+(M = 64 × 1024 tokens), bias epilogue, random operands.  Interleaved rounds in one process (guide
+§5.4 rule 24); one JSON line per (shape, kernel) with the best and median round.
+
+    python scripts/w1_ab.py [--rounds 5] [--iters 20] [--only bf16|fp8]
+"""
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from replicann_amd import _ext, ops  # noqa: E402
+
+BF16 = [("s_qkv", 2304, 768), ("s_proj", 768, 768), ("s_fc1_plain", 3072, 768), ("s_fc2", 768, 3072),
+        ("m_qkv", 3072, 1024), ("m_fc2", 1024, 4096)]
+FP8 = [("m_qkv", 3072, 1024), ("m_proj", 1024, 1024), ("m_fc1_plain", 4096, 1024), ("m_fc2", 1024, 4096)]
+
+
+def graph_time(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+
+    def run():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / iters
+
+    return run
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--m", type=int, default=65536)
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    _ext.ops()
+    torch.manual_seed(0)
+    M = a.m
+    if a.only in (None, "bf16"):
+        for name, N, K in BF16:
+            x = torch.randn(M, K, device="cuda").bfloat16()
+            w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+            bias = (torch.randn(N, device="cuda") * 0.1).bfloat16()
+            runs = {cfg: graph_time(lambda cfg=cfg: ops.gemm(x, w, tb=True, bias=bias, cfg=cfg), a.iters) for cfg in (9, 11)}
+            t = {cfg: [] for cfg in runs}
+            for _ in range(a.rounds):
+                for cfg, r in runs.items():
+                    t[cfg].append(r())
+            fl = 2.0 * M * N * K
+            for cfg, v in t.items():
+                print(json.dumps({"dtype": "bf16", "shape": name, "M": M, "N": N, "K": K, "cfg": cfg,
+                                  "ms_min": round(min(v), 4), "ms_med": round(statistics.median(v), 4),
+                                  "tflops": round(fl / min(v) / 1e9, 1)}), flush=True)
+            del runs
+    if a.only in (None, "fp8"):
+        for name, N, K in FP8:
+            x = torch.randn(M, K, device="cuda").bfloat16()
+            w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+            bias = (torch.randn(N, device="cuda") * 0.1).bfloat16()
+            qa, sa = ops.quantize_fp8(x)
+            qb, sb = ops.quantize_fp8(w)
+            runs = {}
+            for kern in ("0", "9", "11"):
+                os.environ["REPLICANN_FP8_GEMM"] = kern
+                runs[kern] = graph_time(lambda: torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, None, 0, None), a.iters)
+            t = {k: [] for k in runs}
+            for _ in range(a.rounds):
+                for k, r in runs.items():
+                    t[k].append(r())
+            fl = 2.0 * M * N * K
+            for k, v in t.items():
+                print(json.dumps({"dtype": "fp8", "shape": name, "M": M, "N": N, "K": K, "kernel": k,
+                                  "ms_min": round(min(v), 4), "ms_med": round(statistics.median(v), 4),
+                                  "tflops": round(fl / min(v) / 1e9, 1)}), flush=True)
+            del runs
+    os.environ.pop("REPLICANN_FP8_GEMM", None)
+
+
+if __name__ == "__main__":
+    main()
