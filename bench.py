@@ -167,11 +167,17 @@ def main(argv=None):
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    rank_ms = [round(elapsed * 1000 / max(args.steps, 1), 3)]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+        rank_ms = [None] * world
+        dist.all_gather_object(rank_ms, round((t1 - t0) * 1000 / max(args.steps, 1), 3))
     last_loss = float(loss)
+    # after the timed loop: one untimed, phase-timed eager step of the data-parallel path, so a first
+    # multi-GPU record says where its time went (exposed comm, collectives / bytes, schedule, spread)
+    diag = ddp_diagnostics(tr, world, rank_ms, sync) if tr.ddp is not None else None
 
     if args.profile_steps and tr.rank == 0:
         from torch.profiler import ProfilerActivity, profile
@@ -224,6 +230,7 @@ def main(argv=None):
                                 if dev.type == "cuda" and hasattr(torch.ops.replicann, "gemm_get_reserve") else None),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
             **({"ce_chunk_rows": args.ce_chunk} if (is_lm and args.ce_chunk) else {}),
+            **({"ddp_diag": diag} if diag is not None else {}),
             "peak_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if dev.type == "cuda" else None),
         },
     }
@@ -237,6 +244,49 @@ def main(argv=None):
         dist.barrier()
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def ddp_diagnostics(tr, world, rank_ms, sync):
+    """The data-parallel step's own record (untimed, after the timed loop): device phase times of
+    one eager step on every rank (``allreduce_wait_ms`` = how long the compute stream waited for the
+    gradient collectives after the backward: the exposed communication), the collectives and bytes
+    that step issued, the schedule the reducer actually ran (auto resolves to window / eager), the
+    per-rank timed-loop ms/step spread, the RCCL version and every NCCL_* / RCCL_* setting in
+    effect."""
+    import torch
+    import torch.distributed as dist
+
+    comm = tr.ddp.comm
+    info0 = comm.info() if hasattr(comm, "info") else None
+    _, ph = tr.timed_eager_step()
+    sync()
+    info1 = comm.info() if hasattr(comm, "info") else None
+    phases = {k: round(float(v), 3) for k, v in ph.items()}
+    per_rank = [phases]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, phases)
+    waits = [r.get("allreduce_wait_ms") for r in per_rank if r.get("allreduce_wait_ms") is not None]
+    try:
+        rccl = ".".join(str(v) for v in torch.cuda.nccl.version()) if torch.cuda.is_available() else None
+    except Exception:  # noqa: BLE001 - build without the nccl module
+        rccl = None
+    sched = tr.ddp.schedule
+    if sched == "auto":
+        sched = "auto->window" if getattr(tr.ddp, "_windowed", False) else "auto->eager"
+    return {
+        "step_phases_ms_rank0": phases,
+        "allreduce_wait_ms_max": max(waits) if waits else None,
+        "allreduce_wait_ms_min": min(waits) if waits else None,
+        "collectives_per_step": (info1["collectives"] - info0["collectives"]) if info0 else None,
+        "comm_gbytes_per_step": round((info1["bytes"] - info0["bytes"]) / 1e9, 4) if info0 else None,
+        "schedule": sched,
+        "reduce": ("rsag" if getattr(tr.ddp, "rsag", False) else ("fp32 all-reduce" if tr.ddp.fp32 else "bf16 all-reduce")),
+        "rank_ms_per_step": rank_ms,
+        "rank_ms_spread": (round(max(rank_ms) - min(rank_ms), 3) if rank_ms and None not in rank_ms else None),
+        "rccl_version": rccl,
+        "nccl_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_", "TORCH_NCCL_"))},
+    }
 
 
 def precision(model) -> str:

@@ -40,18 +40,32 @@ class TorchComm:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self._works = []
+        self._n = 0  # collectives issued and bytes handed to them (this rank's buffer; info())
+        self._bytes = 0
+
+    def _count(self, t):
+        self._n += 1
+        self._bytes += t.numel() * t.element_size()
+
+    def info(self):
+        """Issued collectives and their bytes so far (same keys as the native communicator's)."""
+        return {"rank": self.rank, "world": self.world, "collectives": self._n, "bytes": self._bytes, "failed": False}
 
     def all_reduce(self, t, op="sum"):
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        self._count(t)
         self._works.append(dist.all_reduce(t, op=rop, group=self.group, async_op=True))
 
     def broadcast(self, t, root=0):
+        self._count(t)
         self._works.append(dist.broadcast(t, root, group=self.group, async_op=True))
 
     def all_gather(self, inp, out):
+        self._count(out)
         self._works.append(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
 
     def reduce_scatter(self, inp, out, op="sum"):
+        self._count(inp)
         self._works.append(dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True))
 
     _side = None
@@ -73,11 +87,13 @@ class TorchComm:
                     self._side.wait_stream(cur)
                 shard16.copy_(shard32)
                 # issued from the side stream: the collective is ordered after the narrowing copy
+                self._count(full)
                 self._works.append(dist.all_gather_into_tensor(full, shard16, group=self.group, async_op=True))
         else:
             if rs is not None:
                 rs.wait()
             shard16.copy_(shard32)
+            self._count(full)
             self._works.append(dist.all_gather_into_tensor(full, shard16, group=self.group, async_op=True))
 
     def wait(self):

@@ -360,6 +360,18 @@ class Trainer:
         self.step_idx += 1
         return loss
 
+    def timed_eager_step(self):
+        """One eager step with device phase timing, whatever the step form (a captured step replays
+        without events): the diagnostic step bench.py records after its timed loop.  Returns
+        (loss, {phase}_ms)."""
+        if not self._tuned:
+            self._tune()
+        batches = [next(self.data) for _ in range(self.cfg.grad_accum)]
+        with self.timer.step(active=True):
+            loss = self._step_body(batches)
+        self.step_idx += 1
+        return loss, self.timer.summary()
+
     def save(self, path):
         """Checkpoint (collective under DDP): model, optimizer, step, config, every rank's RNG
         states and data cursor, and (GPU) the GEMM autotuner's per-shape kernel picks."""
