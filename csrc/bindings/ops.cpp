@@ -694,6 +694,9 @@ Tensor linear_kv(const Tensor& x, const Tensor& w, const optional<Tensor>& bias,
     const int64_t kvw = kv.size(2) * kv.size(3) * kv.size(4);
     TORCH_CHECK(kvw <= N, "linear_kv: cache row wider than the projection");
     TORCH_CHECK(pos.scalar_type() == at::kLong && pos.numel() == 1 && pos.is_cuda(), "linear_kv: pos must be 1 int64 on the device");
+    TORCH_CHECK(w.device() == x.device() && kv.device() == x.device() && pos.device() == x.device() &&
+                    (!bias || !bias->defined() || bias->device() == x.device()),
+                "linear_kv: x, w, bias, kv and pos must be on one device");
     if (bias && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
     Tensor c = at::empty({M, N}, x.options());
     const int rc = rn_gemm_skinny_kv(x.data_ptr(), w.data_ptr(), optr(bias), c.data_ptr(), (int)M, (int)N, (int)K,
@@ -709,10 +712,19 @@ Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, const opti
     CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); GUARD(q);
     TORCH_CHECK(q.dim() == 4 && q.size(1) == 1, "attn_decode: one query per (batch, head)");
     const int B = q.size(0), H = q.size(2), D = q.size(3), Tk = k.size(1);
-    TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(2) == H && v.size(1) == Tk, "attn_decode: shape mismatch");
+    TORCH_CHECK(k.dim() == 4 && v.dim() == 4, "attn_decode: k / v must be (B, Tk, H, D)");
+    TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(2) == H && v.size(2) == H && v.size(1) == Tk &&
+                    k.size(3) == D && v.size(3) == D,
+                "attn_decode: shape mismatch (q ", q.sizes(), ", k ", k.sizes(), ", v ", v.sizes(), ")");
+    TORCH_CHECK(k.device() == q.device() && v.device() == q.device(), "attn_decode: q, k, v on different devices");
+    // the kernel reads 16-B vectors: base pointers and every non-unit stride 16-B aligned
+    for (const Tensor* t : {&q, &k, &v})
+        TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0 && t->stride(3) == 1,
+                    "attn_decode: q / k / v need a 16-byte aligned base and a contiguous head dimension");
     if (mask && mask->defined())
-        TORCH_CHECK(mask->scalar_type() == at::kFloat && mask->is_contiguous() && mask->numel() == Tk,
-                    "attn_decode: mask must be Tk contiguous fp32 values");
+        TORCH_CHECK(mask->scalar_type() == at::kFloat && mask->is_contiguous() && mask->numel() == Tk &&
+                        mask->device() == q.device(),
+                    "attn_decode: mask must be Tk contiguous fp32 values on q's device");
     Tensor o = at::empty({B, 1, H, D}, q.options());
     std::vector<long> s;
     std::vector<long> t;

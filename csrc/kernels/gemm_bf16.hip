@@ -41,6 +41,7 @@
 // XCD a contiguous run of tiles, walked in GROUP_M-row groups for L2 reuse.
 #include <atomic>
 #include <cstdlib>
+#include <cstdio>
 #include <mutex>
 
 #include "common.h"
@@ -150,6 +151,7 @@ struct SlotState {
     unsigned next[kEagerStreams] = {};
     int n_streams = 0;
     int next_captured = kSlotsPerStream * kEagerStreams;
+    bool warned = false;
 };
 static SlotState g_slots[64];
 int rn_gemm_sched_init(int dev) {
@@ -179,7 +181,13 @@ int* rn_gemm_sched_slot(int dev, hipStream_t st) {
     SlotState& ss = g_slots[dev];
     int s = -1;
     if (capturing) {
-        if (ss.next_captured < kSchedSlots) s = ss.next_captured++;
+        if (ss.next_captured < kSchedSlots) {
+            s = ss.next_captured++;
+        } else if (!ss.warned) {  // captured slots are never handed back (a replay may run any time)
+            ss.warned = true;
+            std::fprintf(stderr, "[replicann] gemm: the captured dynamic-schedule slots of device %d are used up; "
+                                 "further captured GEMMs take the static tile walk\n", dev);
+        }
     } else {
         int k = 0;
         while (k < ss.n_streams && ss.streams[k] != st) ++k;

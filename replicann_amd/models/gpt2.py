@@ -16,6 +16,7 @@ MI355X-specific choices:
 
 from __future__ import annotations
 
+import os
 import weakref
 from dataclasses import dataclass
 
@@ -63,6 +64,10 @@ class GPT2Config:
 
 
 _DECODE_GRAPHS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+# captured decode steps kept per model (least recently used evicted first): each holds a KV cache of
+# 2 · n_layer · B · length · n_embd elements (≈ 2.4 GB for GPT-2-small at B = 64, length 1024)
+DECODE_GRAPHS_MAX = int(os.environ.get("REPLICANN_DECODE_GRAPHS", "4"))
+DECODE_LEN_BUCKET = 64  # cache lengths are rounded up to this (capped at block_size): one graph per bucket
 
 
 class GPT2(nn.Module):
@@ -180,11 +185,15 @@ class GPT2(nn.Module):
         B, T0 = idx.shape
         if T0 + max_new_tokens > c.block_size:
             raise ValueError(f"prompt {T0} + {max_new_tokens} new tokens exceeds block_size {c.block_size}")
+        if top_p is not None and not 0.0 < top_p <= 1.0:
+            raise ValueError(f"top_p must be in (0, 1], got {top_p}")
         use_graph = (self.wte.is_cuda if graph is None else graph) and max_new_tokens > 2
         was_training = self.training
         self.eval()
         try:
             L = T0 + max_new_tokens
+            if use_graph:  # one captured step (and cache) serves every length of a bucket
+                L = min(c.block_size, -(-L // DECODE_LEN_BUCKET) * DECODE_LEN_BUCKET)
             # the parameters' storage is part of the key: a graph reads them by address, so one captured
             # before a parameter was re-assigned (p.data = ...) must never be replayed
             sig = tuple(p.data_ptr() for p in self.parameters())
@@ -192,7 +201,9 @@ class GPT2(nn.Module):
             graphs = self._decode_graphs()
             for k in [k for k in graphs if k[4] != sig]:
                 del graphs[k]
-            entry = graphs.get(key) if use_graph else None
+            entry = graphs.pop(key, None) if use_graph else None
+            if entry is not None:
+                graphs[key] = entry  # most recently used last
             if entry is not None:  # same batch / length as an earlier call: reuse its cache and graph
                 cache = entry[0]
                 cache.reset()
@@ -207,6 +218,8 @@ class GPT2(nn.Module):
                     break
                 if use_graph:
                     if entry is None:
+                        while len(graphs) >= max(DECODE_GRAPHS_MAX, 1):  # bounded: evict the least recently used
+                            graphs.pop(next(iter(graphs)))
                         entry = (cache, *self._capture_decode(cache, B))
                         graphs[key] = entry
                     elif not cache.device_pos:
@@ -222,9 +235,11 @@ class GPT2(nn.Module):
             self.train(was_training)
 
     def _decode_graphs(self):
-        """Captured decode steps kept across ``generate`` calls, keyed by (batch, total length, dtype,
-        device, parameter storage): a serving loop with fixed shapes captures once.  Each holds its KV
-        cache (2 · n_layer · B · length · n_embd elements); ``clear_decode_graphs`` frees them.  Kept
+        """Captured decode steps kept across ``generate`` calls, keyed by (batch, cache length rounded
+        up to DECODE_LEN_BUCKET, dtype, device, parameter storage): a serving loop captures once per
+        (batch, length bucket).  At most DECODE_GRAPHS_MAX (REPLICANN_DECODE_GRAPHS, default 4) are
+        kept, least recently used evicted first.  Each holds its KV cache (2 · n_layer · B · length ·
+        n_embd elements); ``clear_decode_graphs`` frees them.  Kept
         outside the module's attributes (a weak-keyed registry), so copying / pickling the model
         never touches graph objects."""
         return _DECODE_GRAPHS.setdefault(self, {})
@@ -255,6 +270,7 @@ def _sample(logits, temperature, top_k, generator, top_p=None):
         srt, idx = torch.sort(logits, dim=-1, descending=True)
         cum = torch.softmax(srt, -1).cumsum(-1)
         drop = cum - torch.softmax(srt, -1) >= top_p  # mass BEFORE a token already reaches top_p
+        drop[..., 0] = False  # the most likely token always stays (top_p <= 0 would drop every token)
         srt = srt.masked_fill(drop, float("-inf"))
         logits = torch.full_like(logits, float("-inf")).scatter(-1, idx, srt)
     probs = torch.softmax(logits, -1)

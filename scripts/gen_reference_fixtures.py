@@ -69,6 +69,23 @@ def main():
     out = os.path.join(ROOT, "tests", "fixtures", "ref_gpu_grads.pt")
     torch.save(gx, out)
     print(f"wrote {out} ({os.path.getsize(out) / 2**20:.1f} MiB), cases: {sorted(gx)}")
+    write_io_floors(tr)
+
+
+def write_io_floors(tr):
+    """The bf16 floors of the stacked encoder → cross-decoder case's OUTPUT and INPUT gradients (the
+    reference run in bf16 against itself in fp32), so the GPU test derives those tolerances the way
+    it derives the per-parameter ones (1.25 x the reference's own bf16 error) instead of hand-setting
+    them.  JSON: plain numbers."""
+    import json
+
+    y, gs, gt, _ = _cross(tr, torch.float32)
+    y16, gs16, gt16, _ = _cross(tr, torch.bfloat16)
+    fl = {refgen.GRAD_CROSS[0]: {"y": _rel(y16, y), "g_src": _rel(gs16, gs), "g_tgt": _rel(gt16, gt)}}
+    out = os.path.join(ROOT, "tests", "fixtures", "ref_io_floors.json")
+    with open(out, "w") as f:
+        json.dump(fl, f, indent=1)
+    print(f"wrote {out}: {fl}")
 
 
 def _rel(a, b):
@@ -136,4 +153,7 @@ def grad_fixtures(tr):
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--io-floors"]:  # only the small JSON (the .pt fixtures stay byte for byte)
+        write_io_floors(load_reference())
+    else:
+        main()

@@ -1,4 +1,8 @@
 #!/bin/bash
+# HISTORICAL (kept as the record of round-4 call E): the REPLICANN_ATTN_DQ_QG / REPLICANN_ATTN_DKDV_KG
+# knobs it sets were removed in commit b263165, so on the current library every arm runs the default
+# kernel and the A/B would compare nothing.  It refuses to run.
+echo "gpu_r4e.sh is historical: its attention knobs no longer exist (b263165)" >&2; exit 2
 # round 4 (call E): software-pipelined D=64 attention forward (REPLICANN_ATTN_FWD_PIPE 1 / 2) —
 # fp32-reference tests of every attention arm, forward A/B at GPT-2-small shapes, per-kernel times
 # of the backward arms (kernel trace), attention PMC of the default arm.

@@ -122,3 +122,22 @@ def test_model_copy_after_generate():
     m.generate(torch.zeros(1, 3, dtype=torch.long), 4, temperature=0, graph=False)
     m2 = copy.deepcopy(m)
     assert set(m2.state_dict()) == set(m.state_dict())
+
+
+def test_top_p_degenerate_keeps_top_token():
+    """top_p <= 0 in _sample keeps the most likely token (no all -inf row, no NaN softmax); generate
+    and the CLI refuse top_p outside (0, 1]."""
+    import pytest
+
+    import replicann_amd as R
+    from replicann_amd.models.gpt2 import _sample
+
+    lg = torch.tensor([[0.1, 2.0, -1.0, 0.5], [3.0, 0.0, 0.0, 0.0]])
+    g = torch.Generator().manual_seed(0)
+    for p in (0.0, -1.0, 1e-9):
+        t = _sample(lg.clone(), 1.0, None, g, top_p=p)
+        assert t.squeeze(-1).tolist() == [1, 0]
+    m = R.GPT2(R.GPT2Config.tiny())
+    for bad in (0.0, -0.5, 1.5):
+        with pytest.raises(ValueError):
+            m.generate(torch.zeros(1, 3, dtype=torch.long), 2, top_p=bad)

@@ -1,5 +1,11 @@
 """KV-cache decoding on the HIP kernels: cached one-token steps (attention with Tq < Tk, causal
-bottom-right aligned) against the full bf16 forward, head sizes 64 and 32."""
+bottom-right aligned) and the hipGraph-replayed step against an fp32 ATen forward of the same weights
+(the model's CPU path), head sizes 64 and 32.
+
+Tolerance: 3e-2 relative L2 on the logits, the bf16 budget of this 2-layer model (bf16 weights,
+activations and cache; its full native forward is within 1.2e-2 of the same fp32 reference)."""
+
+import copy
 
 import pytest
 import torch
@@ -17,8 +23,15 @@ def _model(cuda, n_head):
 
 
 def rel_err(a, b):
-    a, b = a.float(), b.float()
+    a, b = a.float().cpu(), b.float().cpu()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _fp32_logits(m, seq):
+    """fp32 ATen forward (the CPU path of GPT2.forward) of the same bf16 weights: (B, T, vocab)."""
+    ref = copy.deepcopy(m).float().cpu().eval()
+    with torch.no_grad():
+        return ref(seq.cpu())
 
 
 @pytest.mark.parametrize("n_head", [2, 4])
@@ -26,8 +39,9 @@ def test_decode_matches_full_forward(cuda, n_head):
     from replicann_amd.models.blocks import KVCache
     m = _model(cuda, n_head)
     seq = torch.randint(0, 1000, (3, 90), device=cuda)
+    full = _fp32_logits(m, seq)
     with torch.no_grad():
-        full = m(seq)
+        assert rel_err(m(seq), full) < 2e-2  # the native full forward itself
     cache = KVCache(m.config.n_layer, 90)
     lg = m.decode_step(seq[:, :70], cache)  # prefill
     assert rel_err(lg, full[:, 69]) < 3e-2
@@ -50,12 +64,13 @@ def test_generate_gpu(cuda):
 
 
 def test_generate_graph_matches_eager(cuda):
-    """The hipGraph-replayed one-token step (device-side position, masked full-cache attention)
-    against the eager host-position steps: same first token, logits of each replay close."""
+    """The hipGraph-replayed one-token step (device-side position, masked full-cache attention) and
+    the eager host-position steps, each against the fp32 forward of the same prefix."""
     from replicann_amd.models.blocks import KVCache
     m = _model(cuda, 2)
     idx = torch.randint(0, 1000, (3, 20), device=cuda)
     seq = torch.cat([idx, torch.randint(0, 1000, (3, 12), device=cuda)], 1)
+    full = _fp32_logits(m, seq)
     host = KVCache(m.config.n_layer, 32)
     dev = KVCache(m.config.n_layer, 32)
     m.decode_step(idx, host)
@@ -65,21 +80,37 @@ def test_generate_graph_matches_eager(cuda):
         a = m.decode_step(seq[:, t:t + 1], host)
         tok.copy_(seq[:, t:t + 1])
         g.replay()
-        assert rel_err(out, a) < 3e-2, t
+        assert rel_err(a, full[:, t]) < 3e-2, t
+        assert rel_err(out, full[:, t]) < 3e-2, t
     torch.cuda.synchronize()
     assert int(dev.pos_t) == 32
+    # generate(): graph replay and eager steps give the same greedy prefix, and every replayed step's
+    # logits (re-derived here by the fp32 forward of the generated prefix) make its token a top choice
     e = m.generate(idx, 12, temperature=0, graph=False)
     r = m.generate(idx, 12, temperature=0, graph=True)
     assert torch.equal(e[:, :21], r[:, :21])
-    # every replayed step's greedy token is the argmax of the eager logits of the same prefix (up to
-    # near-ties between the two attention kernels' roundings)
-    host = KVCache(m.config.n_layer, 32)
-    lg = m.decode_step(r[:, :20], host)
-    agree = 0
+    ref = _fp32_logits(m, r)
     for t in range(20, 31):
-        agree += int((lg.float().argmax(-1) == r[:, t]).sum())
-        lg = m.decode_step(r[:, t:t + 1], host)
-    assert agree >= 0.9 * 3 * 11
+        lg = ref[:, t - 1]
+        chosen = lg.gather(-1, r[:, t:t + 1].cpu()).squeeze(-1)
+        # greedy on bf16 logits within the bf16 budget of the fp32 maximum
+        assert bool((chosen >= lg.max(-1).values - 3e-2 * lg.abs().max(-1).values).all()), t
+
+
+def test_generate_registry_bounded(cuda):
+    """Serving with varying prompt lengths / batch sizes keeps at most DECODE_GRAPHS_MAX captured steps:
+    lengths share a 64-token bucket, the least recently used entry is evicted."""
+    from replicann_amd.models import gpt2 as G
+    m = _model(cuda, 2)
+    for B in (1, 2, 3):
+        for T0 in (5, 9, 30, 61):
+            m.generate(torch.randint(0, 1000, (B, T0), device=cuda), 3, temperature=0)
+            assert len(m._decode_graphs()) <= G.DECODE_GRAPHS_MAX
+    lens = {k[1] for k in m._decode_graphs()}
+    assert lens <= {64, 128}
+    m.generate(torch.randint(0, 1000, (5, 10), device=cuda), 4, temperature=0)
+    assert len(m._decode_graphs()) <= G.DECODE_GRAPHS_MAX
+    m.clear_decode_graphs()
 
 
 def test_generate_graph_reuse(cuda):

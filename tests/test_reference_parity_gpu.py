@@ -144,6 +144,13 @@ def _param_case(gfx, i, dev, dtype, flat, tol):
     _check_param_grads(m.named_parameters(), ref, tol, name)
 
 
+def _io_floors():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "ref_io_floors.json")) as f:
+        return json.load(f)
+
+
 def _param_cross(gfx, dev, dtype, flat, tol):
     name, H, E, Ts, Tt = refgen.GRAD_CROSS
     ref = gfx[name]
@@ -156,12 +163,14 @@ def _param_cross(gfx, dev, dtype, flat, tol):
     y.backward(refgen.det_grad(y.shape, 904).to(dev, dtype))
     t = tol if tol is not None else 3e-2
     assert rel(y, ref["y"]) < t
-    # input gradients of the stacked bf16 blocks (encoder → the decoder's cross-attention K / V):
-    # measured 3.4 % (source) and 3.5 % (target) against fp32 on the MI355X — the same order as the
-    # reference's own bf16 error on the FFN parameters (the fixture's floors, up to 6.5 %)
-    ti = tol if tol is not None else 5e-2
-    assert rel(src.grad, ref["g_src"]) < ti, rel(src.grad, ref["g_src"])
-    assert rel(tgt.grad, ref["g_tgt"]) < ti, rel(tgt.grad, ref["g_tgt"])
+    # input gradients of the stacked bf16 blocks (encoder → the decoder's cross-attention K / V): the
+    # same derived bound as every parameter gradient — 1.25 x the REFERENCE's own bf16 error on that
+    # tensor (tests/fixtures/ref_io_floors.json, scripts/gen_reference_fixtures.py --io-floors: 3.7 %
+    # / 3.6 %), at least 2 % (the native path measured 3.4 % / 3.5 % on the MI355X)
+    fl = _io_floors()[name]
+    for key, g in (("g_src", src.grad), ("g_tgt", tgt.grad)):
+        ti = tol if tol is not None else max(2e-2, 1.25 * fl[key])
+        assert rel(g, ref[key]) < ti, (key, rel(g, ref[key]), ti)
     named = [("enc." + n, p) for n, p in enc.named_parameters()] + [("dec." + n, p) for n, p in dec.named_parameters()]
     _check_param_grads(named, ref, tol, name)
 
