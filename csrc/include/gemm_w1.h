@@ -51,14 +51,13 @@ constexpr int W1_B0 = 2 * W1_STAGE;   // B ring: 3 stages
 constexpr int W1_LDS = 5 * W1_STAGE;  // 160 KiB
 constexpr int W1_WAIT_J = 13;         // block that opens with the end-of-K-tile wait + barrier
 
-enum { W1_FIRST = 0, W1_EPI = 1, W1_STEADY = 2, W1_LAST = 3 };
+enum { W1_EPI = 1, W1_STEADY = 2, W1_LAST = 3 };
 
-// ops a K-tile issues before its wait (block 13) and after its last DMA (block 8)
+// VMEM ops a K-tile issues before its end-of-K-tile wait (block 13): the wait for K-tile t + 1 (whose
+// DMA went out in K-tile t - 1's blocks 1-8) leaves exactly these in flight.  Ops of K-tile t - 1
+// issued after its DMA (an EPI's stores of blocks 9-15) are waited for too: conservative, no branch.
 constexpr int w1_before_wait(int kind) { return (kind == W1_LAST ? 8 : 0) + 16 + (kind == W1_EPI ? 24 : 0); }
-constexpr int w1_after_dma(int kind) { return kind == W1_EPI ? 16 : 0; }
-// the end-of-K-tile wait: K-tile t + 1's DMA went out last in K-tile t - 1's blocks 1-8
-constexpr int w1_wait_count(int kind, bool prev_epi) { return w1_before_wait(kind) + (prev_epi ? w1_after_dma(W1_EPI) : 0); }
-static_assert(w1_wait_count(W1_LAST, true) <= 63 && w1_wait_count(W1_EPI, false) <= 63, "vmcnt range");
+static_assert(w1_before_wait(W1_EPI) <= 63, "vmcnt range");
 
 struct W1Frag {
     s16x8 lo, hi;  // 16-B chunks g and g + 4 of the fragment row (k-steps 0 / 1 of bf16; one 32-B e4m3 operand)
@@ -158,7 +157,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
         n0 = tn * 256;
     };
     int m0 = 0, n0 = 0, m1 = 0, n1 = 0, pm0 = 0, pn0 = 0;
-    bool has1 = false;
+    bool has1 = false, pm_live = false;
     item_mn(0, m0, n0);
     auto set_next = [&](int s) {
         has1 = s < n_items;
@@ -272,53 +271,26 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
         for (int i = 0; i < 4; ++i) pk_st16(o[i], crs, st_off(i, pp, tn0));
     };
 
-    // ---- the K-tile loop: one body for every K-tile of the block (a single loop keeps one phi per
-    // accumulator; separate first / steady / last bodies made the allocator permute AGPRs between
-    // paths and spill).  Uniform flags: k0 = first K-tile of a tile (bias as the C operand), epi = k0
-    // with a previous tile (its epilogue interleaved), last = last K-tile of a tile (issues the next
-    // tile's bias).  Ring slots: A t % 2, B t % 3. ----
-    int aslot = 0, bslot = 0, kt = 0;
-    bool prev_epi = false;
-    const int total = n_items * nk;
-
-    // ---- prologue: bias of tile 0, its K-tiles 0 and 1 in flight, K-tile 0's first fragments ----
-    bias_issue(true, n0);
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        const u32x4 rsA = dma_rs(true, d), rsB = dma_rs(false, d);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dma_one(rsA, true, d, i);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dma_one(rsB, false, d, i);
-    }
-    w1_pin8<16>(braw);  // bias + K-tile 0 (own DMA) landed
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Acur[i] = rd_a(0, i);
-    Bq[0] = rd_b(0, 0);
-    Bq[1] = rd_b(0, 1);
-    Bq[2] = rd_b(0, 2);
-
-#pragma unroll 1
-    for (int t = 0; t < total; ++t) {
-        const bool k0 = kt == 0, epi = k0 && t > 0, last = kt == nk - 1;
-        if (epi) {  // a new tile: the finished one's epilogue runs under this K-tile
-            pm0 = m0;
-            pn0 = n0;
-            m0 = m1;
-            n0 = n1;
-            set_next(t / nk + 1);
-        }
-        u32x4 crs = st_rs(epi ? p.C : nullptr, pm0, pn0);
-        if (last) bias_issue(has1, n1);
-        // the end-of-K-tile wait: K-tile t + 1's DMA went out in K-tile t - 1's blocks 1-8; younger are
-        // this K-tile's bias / DMA / stores issued before block 13 and t - 1's stores after its DMA
-        const int nwait = (last ? 8 : 0) + 16 + (epi ? 24 : 0) + (prev_epi ? 16 : 0);
+    // ---- K-tile bodies.  Three straight-line bodies, no branch inside (a uniform branch per block made
+    // hipcc sink every MFMA below the block's reads and DMA): EPI = a tile's first K-tile (bias as the
+    // MFMAs' C operand) with the previous tile's epilogue interleaved (the block's first tile "stores"
+    // zero-initialised accumulators through a zero-record descriptor: no traffic, same counts), STEADY,
+    // LAST (issues the next tile's bias).  The end-of-K-tile waits are the counts of each body's own
+    // ops plus, where a K-tile follows an EPI, nothing more: the EPI's late stores are simply waited
+    // for a K-tile later (conservative, branch-free).  Ring slots: A t % 2, B t % 3. ----
+    int aslot = 0, bslot = 0;
+    auto ktile = [&](auto kc, int kt) {
+        constexpr int KIND = decltype(kc)::value;
+        constexpr bool K0 = KIND == W1_EPI;
+        [[maybe_unused]] u32x4 crs = {0u, 0u, 0u, 0u};
+        if constexpr (K0) crs = st_rs(pm_live ? p.C : nullptr, pm0, pn0);
+        if constexpr (KIND == W1_LAST) bias_issue(has1, n1);
+        if constexpr (K0) w1_pin8<16>(braw);  // this tile's bias (issued a K-tile ago; 16 DMA younger)
+        constexpr int NW = w1_before_wait(KIND);
         const int an = aslot ^ 1, bn = bslot == 2 ? 0 : bslot + 1;
         const int bd = bslot == 0 ? 2 : bslot - 1;  // B slot of K-tile t + 2 (= t - 1's)
         const u32x4 rsA = dma_rs(true, kt + 2), rsB = dma_rs(false, kt + 2);
-        u32x4 pend[4];
+        [[maybe_unused]] u32x4 pend[4];
         W1Frag Bf[16], An[4];
         Bf[0] = Bq[0];
         Bf[1] = Bq[1];
@@ -329,10 +301,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             if (j == W1_WAIT_J) {
                 // K-tile t + 1 staged (own DMA), every wave done reading B(t): barrier, then its first
                 // fragments under blocks 13-15
-                if (nwait == 16) vm_wait<16>();
-                else if (nwait == 24) vm_wait<24>();
-                else if (nwait == 32) vm_wait<32>();
-                else vm_wait<40>();
+                vm_wait<NW>();
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -348,15 +317,9 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
                 Bq[1] = rd_b(bn, 1);
             }
             if (j == 15) Bq[2] = rd_b(bn, 2);
-            if (j == 0 && epi) w1_pin8<16>(braw);  // this tile's bias: retired at the end of the last K-tile
-            if (epi) {
+            if constexpr (K0) {
                 if ((j & 1) == 0) epi_convert(j >> 1, pend, true);
                 else epi_store(pend, j >> 1, crs, pn0);
-            }
-            if (k0) {
-                const f32x4 c = cinit(j);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[i][j] = c;
             }
             if (j >= 1 && j <= 8) {
                 const bool isA = j <= 4;
@@ -366,25 +329,74 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             }
             if (j + 3 < 16) Bf[j + 3] = rd_b(bslot, j + 3);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i][j] = w1_mma<FP8>(Bf[j], Acur[i], acc[i][j], eb, ea);
+            for (int i = 0; i < 4; ++i) acc[i][j] = w1_mma<FP8>(Bf[j], Acur[i], K0 ? cinit(j) : acc[i][j], eb, ea);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (last) w1_pin8<16>(braw);  // the next tile's bias (issued at block 0, 16 DMA younger)
+        // every accumulator lives in the AGPR file across the loops: without this the allocator gives
+        // some loop-carried accumulators arch VGPRs and copies each MFMA result out (hazard nops)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) asm volatile("" : "+a"(acc[i][j]));
+        if constexpr (KIND == W1_LAST) w1_pin8<16>(braw);  // the next tile's bias (16 DMA younger)
 #pragma unroll
         for (int i = 0; i < 4; ++i) Acur[i] = An[i];
         aslot = an;
         bslot = bn;
-        prev_epi = epi;
-        kt = last ? 0 : kt + 1;
+    };
+    using KEpi = std::integral_constant<int, W1_EPI>;
+    using KSteady = std::integral_constant<int, W1_STEADY>;
+    using KLast = std::integral_constant<int, W1_LAST>;
+
+    // ---- prologue: bias of tile 0, its K-tiles 0 and 1 in flight, K-tile 0's first fragments ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bias_issue(true, n0);
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        const u32x4 rsA = dma_rs(true, d), rsB = dma_rs(false, d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma_one(rsA, true, d, i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma_one(rsB, false, d, i);
     }
-    // ---- the last tile's epilogue (exposed) ----
+    vm_wait<16>();  // K-tile 0 (own DMA) landed
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Acur[i] = rd_a(0, i);
+    Bq[0] = rd_b(0, 0);
+    Bq[1] = rd_b(0, 1);
+    Bq[2] = rd_b(0, 2);
+
+#pragma unroll 1
+    for (int s = 0; s < n_items; ++s) {
+        if (s > 0) {  // a new tile: the finished one's epilogue runs under its first K-tile
+            pm0 = m0;
+            pn0 = n0;
+            m0 = m1;
+            n0 = n1;
+            set_next(s + 1);
+        }
+        pm_live = s > 0;
+        ktile(KEpi{}, 0);
+#pragma unroll 1
+        for (int kt = 1; kt < nk - 1; ++kt) ktile(KSteady{}, kt);
+        ktile(KLast{}, nk - 1);
+    }
+    // ---- the last tile's epilogue (exposed; asm accumulator reads as in the loop, after enough wait
+    // states for the last MFMAs' results: 4 × s_nop 7 > the longest MFMA write latency) ----
     {
         const u32x4 crs = st_rs(p.C, m0, n0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
         for (int pp = 0; pp < 8; ++pp) {
             __builtin_amdgcn_sched_barrier(0);
             u32x4 o[4];
-            epi_convert(pp, o, false);
+            epi_convert(pp, o, true);
             epi_store(o, pp, crs, n0);
         }
     }
