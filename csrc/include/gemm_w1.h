@@ -125,10 +125,11 @@ RN_DEV int w1_e8m0(const float* s) {
     return (int)((u >> 23) & 0xFF);
 }
 
-template <int FP8, int ACT, bool ALPHA>
+template <int FP8, int ACT, bool ALPHA, bool BKC>
 __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
     static_assert(ACT == ACT_NONE, "w1: forward epilogues without activation (activations: cfg 9)");
     static_assert(!(FP8 && ALPHA), "fp8: the scales ride the MFMA");
+    static_assert(BKC || !FP8, "w1: fp8 operands K-contiguous");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -169,15 +170,29 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
     // (A: swz_kc, B: swz_kcp; both depend on i only through i & 1 / i & 3)
     const int dr = 64 * w + (lane >> 3);
     uint32_t a_off[2], b_off[4];
+    [[maybe_unused]] int b_col[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int r = dr + 8 * q;
         a_off[q] = (uint32_t)((long)r * lda + (((lane & 7) ^ swz_kc(r)) << 4));
     }
+    if constexpr (BKC) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = dr + 8 * q;
-        b_off[q] = (uint32_t)((long)r * ldb + (((lane & 7) ^ swz_kcp(r)) << 4));
+        for (int q = 0; q < 4; ++q) {
+            const int r = dr + 8 * q;
+            b_off[q] = (uint32_t)((long)r * ldb + (((lane & 7) ^ swz_kcp(r)) << 4));
+        }
+    } else {
+        // MN-contiguous B ([k][n] rows, the data gradient dY·W): wave w stages sub-image w = columns
+        // 64w..64w+63 of the 64 k rows, k row 8i + (lane>>3), 8-column chunk (lane&7) ^ swz_mnp(k)
+        // (pk_stage<false, true>'s image); the swizzle depends on i only through i & 1
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int r = 8 * q + (lane >> 3);
+            b_col[q] = 64 * w + (((lane & 7) ^ swz_mnp(r)) << 3);
+            b_off[q] = (uint32_t)((long)r * ldb + b_col[q] * 2);
+        }
+        b_off[2] = b_off[3] = 0u;
     }
     // descriptors of K-tile d of the tile (d >= nk: K-tile d - nk of the next tile; past the block's
     // last tile: zero records, every lane out of range — the DMA zero-fills and moves nothing)
@@ -187,13 +202,25 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
         const bool live = !nxt || has1;
         const int r0 = isA ? (nxt ? m1 : m0) : (nxt ? n1 : n0);
         const long ld = isA ? lda : ldb;
+        if (!BKC && !isA) {  // K-tile dd = k rows 64dd..64dd+63 (bf16), columns from r0; N tail per lane
+            const char* base = (const char*)p.B + (long)(64 * dd) * ld + (long)r0 * 2;
+            const long n = live ? (long)((p.K >> 1) - 64 * dd) * ld - (long)r0 * 2 : 0;
+            return w1_rsrc(base, clamp_u(n));
+        }
         const char* base = (const char*)(isA ? p.A : p.B) + (long)r0 * ld + dd * 128;
         const long n = live ? (long)((isA ? p.M : p.N) - r0) * ld - dd * 128 : 0;
         return w1_rsrc(base, clamp_u(n));
     };
-    auto dma_one = [&](const u32x4& rs, bool isA, int slot, int i) {
-        const uint32_t off = isA ? w1_opq(a_off[i & 1]) + (uint32_t)((i & ~1) * 8 * w1_opq_s((int)lda))
-                                 : w1_opq(b_off[i & 3]) + (uint32_t)((i & ~3) * 8 * w1_opq_s((int)ldb));
+    // columns of the tile K-tile d belongs to that exist (MN-contiguous B: the per-lane N-tail check)
+    auto b_ncols = [&](int d) -> int { return p.N - (d >= nk ? n1 : n0); };
+    auto dma_one = [&](const u32x4& rs, bool isA, int slot, int i, int ncols) {
+        uint32_t off;
+        if (isA) off = w1_opq(a_off[i & 1]) + (uint32_t)((i & ~1) * 8 * w1_opq_s((int)lda));
+        else if constexpr (BKC) off = w1_opq(b_off[i & 3]) + (uint32_t)((i & ~3) * 8 * w1_opq_s((int)ldb));
+        else {
+            off = w1_opq(b_off[i & 1]) + (uint32_t)((i & ~1) * 8 * w1_opq_s((int)ldb));
+            off = (int)w1_opq((uint32_t)b_col[i & 1]) < ncols ? off : 0xFFFFFFF0u;
+        }
         const uint32_t dst = lds_addr(smem) + (isA ? W1_A0 : W1_B0) + slot * W1_STAGE + (uint32_t)((8 * w + i) * 1024);
         dma16_at(rs, off, dst);
     };
@@ -209,11 +236,39 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
     const int brow = 8 * (bi >> 2) + (bi & 3);
     const uint32_t b_lo = (uint32_t)(brow * 128 + ((G ^ swz_kcp(brow)) << 4));
     const uint32_t b_hi = (uint32_t)(brow * 128 + (((G + 4) ^ swz_kcp(brow)) << 4));
+    // MN-contiguous B (pk_frag_b<false> on the 4 sub-images of a stage): k row 8G + (bi>>2) (+4, +32 for
+    // k-step 1), chunk (4·(pair & 1) + (bi&3)) ^ swz_mnp, 8-B half (jj & 1) ^ (bi & 1): four lane offsets
+    [[maybe_unused]] uint32_t b_mn[2][2];
+    if constexpr (!BKC) {
+        const int k0 = 8 * G + (bi >> 2), pl = bi & 3;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                b_mn[e][h] = (uint32_t)(k0 * 128 + (((4 * e + pl) ^ swz_mnp(k0)) << 4) + ((h ^ (pl & 1)) << 3));
+    }
     auto rd_a = [&](int slot, int i) -> W1Frag {
         const char* base = smem + W1_A0 + slot * W1_STAGE + i * 2048;
         return {*reinterpret_cast<const s16x8*>(base + a_lo), *reinterpret_cast<const s16x8*>(base + a_hi)};
     };
     auto rd_b = [&](int slot, int jj) -> W1Frag {
+        if constexpr (!BKC) {
+            typedef __attribute__((address_space(3))) s16x4 lds4;
+            const char* base = smem + W1_B0 + slot * W1_STAGE + (jj >> 2) * 8192 + w1_opq(b_mn[(jj >> 1) & 1][jj & 1]);
+            s16x4 v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)  // (k-step t >> 1, rows +4 for t & 1)
+                v[t] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(base + (t >> 1) * 4096 + (t & 1) * 512));
+            W1Frag f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                f.lo[e] = v[0][e];
+                f.lo[4 + e] = v[1][e];
+                f.hi[e] = v[2][e];
+                f.hi[4 + e] = v[3][e];
+            }
+            return f;
+        }
         const char* base = smem + W1_B0 + slot * W1_STAGE + (jj >> 1) * 4096 + (jj & 1) * 512;
         return {*reinterpret_cast<const s16x8*>(base + b_lo), *reinterpret_cast<const s16x8*>(base + b_hi)};
     };
@@ -241,10 +296,13 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
         for (int pp = 0; pp < 8; ++pp) w1_ld16(braw[pp], rs, w1_opq((uint32_t)(16 * G)) + (uint32_t)(64 * pp));
     };
     // C operand of the first K-tile's MFMAs of B fragment jj: the bias of its 4 columns
+    // (MN-contiguous B: odd lane groups hold a pair's fragment 1 columns first — pk_frag_b's a(g))
+    const bool swp = !BKC && (G & 1);
     auto cinit = [&](int jj) -> f32x4 {
         if constexpr (ALPHA) return (f32x4){0.f, 0.f, 0.f, 0.f};  // (host: no bias with alpha)
         const u32x4 u = braw[jj >> 1];
-        const uint32_t lo = (jj & 1) ? u.z : u.x, hi = (jj & 1) ? u.w : u.y;
+        const bool second = (jj & 1) != (int)swp;
+        const uint32_t lo = second ? u.z : u.x, hi = second ? u.w : u.y;
         return (f32x4){__builtin_bit_cast(float, lo << 16), __builtin_bit_cast(float, lo & 0xFFFF0000u),
                        __builtin_bit_cast(float, hi << 16), __builtin_bit_cast(float, hi & 0xFFFF0000u)};
     };
@@ -264,6 +322,10 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
                 if constexpr (ALPHA) v[c] *= alpha;
             }
             o[i] = (u32x4){pk_pack2(v[0], v[1]), pk_pack2(v[2], v[3]), pk_pack2(v[4], v[5]), pk_pack2(v[6], v[7])};
+            if constexpr (!BKC) {
+                const u32x4 t = o[i];
+                o[i] = swp ? (u32x4){t.z, t.w, t.x, t.y} : t;
+            }
         }
     };
     auto epi_store = [&](const u32x4* o, int pp, const u32x4& crs, int tn0) {
@@ -290,6 +352,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
         const int an = aslot ^ 1, bn = bslot == 2 ? 0 : bslot + 1;
         const int bd = bslot == 0 ? 2 : bslot - 1;  // B slot of K-tile t + 2 (= t - 1's)
         const u32x4 rsA = dma_rs(true, kt + 2), rsB = dma_rs(false, kt + 2);
+        const int ncB = BKC ? 0 : b_ncols(kt + 2);
         [[maybe_unused]] u32x4 pend[4];
         W1Frag Bf[16], An[4];
         Bf[0] = Bq[0];
@@ -324,8 +387,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             if (j >= 1 && j <= 8) {
                 const bool isA = j <= 4;
                 const int i0 = ((j - 1) & 3) * 2;
-                dma_one(isA ? rsA : rsB, isA, isA ? aslot : bd, i0);
-                dma_one(isA ? rsA : rsB, isA, isA ? aslot : bd, i0 + 1);
+                dma_one(isA ? rsA : rsB, isA, isA ? aslot : bd, i0, ncB);
+                dma_one(isA ? rsA : rsB, isA, isA ? aslot : bd, i0 + 1, ncB);
             }
             if (j + 3 < 16) Bf[j + 3] = rd_b(bslot, j + 3);
 #pragma unroll
@@ -357,10 +420,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
 #pragma unroll
     for (int d = 0; d < 2; ++d) {
         const u32x4 rsA = dma_rs(true, d), rsB = dma_rs(false, d);
+        const int ncB = BKC ? 0 : b_ncols(d);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dma_one(rsA, true, d, i);
+        for (int i = 0; i < 8; ++i) dma_one(rsA, true, d, i, 0);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dma_one(rsB, false, d, i);
+        for (int i = 0; i < 8; ++i) dma_one(rsB, false, d, i, ncB);
     }
     vm_wait<16>();  // K-tile 0 (own DMA) landed
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -403,9 +467,9 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
 }
 
 // host: persistent grid of min(tiles, CUs) workgroups, 160 KiB LDS each
-template <int FP8, int ACT, bool ALPHA>
+template <int FP8, int ACT, bool ALPHA, bool BKC>
 void launch_w1_t(GemmArgs& a, hipStream_t st) {
-    auto kern = gemm_w1<FP8, ACT, ALPHA>;
+    auto kern = gemm_w1<FP8, ACT, ALPHA, BKC>;
     static int attr_dev = -1;
     int dev = 0;
     (void)hipGetDevice(&dev);

@@ -256,7 +256,7 @@ int fp8_gemm_kernel() {
 }  // namespace
 
 void rn_gemm_launch_pk_fp8(rn_gemm_detail::GemmArgs& a, int act, hipStream_t st);
-int rn_gemm_launch_w1(rn_gemm_detail::GemmArgs& a, int fp8, int act, hipStream_t st);
+int rn_gemm_launch_w1(rn_gemm_detail::GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn);
 void rn_gemm_launch_pk_fp8_wgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 void rn_gemm_launch_pk_fp8_dgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 
@@ -337,7 +337,7 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
         rn_gemm_detail::GemmArgs w = {};
         w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C; w.bias = (const bf16*)bias;
         w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
-        if (rn_gemm_launch_w1(w, 1, ACT_NONE, st) == 0) return 0;
+        if (rn_gemm_launch_w1(w, 1, ACT_NONE, st, false) == 0) return 0;
     }
     if (!q8 && N % 8 == 0 && ldc % 8 == 0 && (kern == 9 || (kern < 0 && K >= 2048))) {
         a.tiles_m = (M + 255) / 256;

@@ -17,8 +17,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from replicann_amd import _ext, ops  # noqa: E402
 
-BF16 = [("s_qkv", 2304, 768), ("s_proj", 768, 768), ("s_fc1_plain", 3072, 768), ("s_fc2", 768, 3072),
-        ("m_qkv", 3072, 1024), ("m_fc2", 1024, 4096)]
+# (name, N, K, B layout): "nt" = x·Wᵀ (W [N, K]), "nn" = the data gradient dY·W (W [K, N])
+BF16 = [("s_qkv", 2304, 768, "nt"), ("s_proj", 768, 768, "nt"), ("s_fc1_plain", 3072, 768, "nt"),
+        ("s_fc2", 768, 3072, "nt"), ("m_qkv", 3072, 1024, "nt"), ("m_fc2", 1024, 4096, "nt"),
+        ("s_dgrad_qkv", 768, 2304, "nn"), ("s_dgrad_fc1", 768, 3072, "nn"), ("s_dgrad_fc2", 3072, 768, "nn"),
+        ("s_dgrad_proj", 768, 768, "nn")]
 FP8 = [("m_qkv", 3072, 1024), ("m_proj", 1024, 1024), ("m_fc1_plain", 4096, 1024), ("m_fc2", 1024, 4096)]
 
 
@@ -55,18 +58,19 @@ def main():
     torch.manual_seed(0)
     M = a.m
     if a.only in (None, "bf16"):
-        for name, N, K in BF16:
+        for name, N, K, lay in BF16:
             x = torch.randn(M, K, device="cuda").bfloat16()
-            w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
-            bias = (torch.randn(N, device="cuda") * 0.1).bfloat16()
-            runs = {cfg: graph_time(lambda cfg=cfg: ops.gemm(x, w, tb=True, bias=bias, cfg=cfg), a.iters) for cfg in (9, 11)}
+            nt = lay == "nt"
+            w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16() if nt else (torch.randn(K, N, device="cuda") * 0.05).bfloat16()
+            bias = (torch.randn(N, device="cuda") * 0.1).bfloat16() if nt else None
+            runs = {cfg: graph_time(lambda cfg=cfg: ops.gemm(x, w, tb=nt, bias=bias, cfg=cfg), a.iters) for cfg in (9, 11)}
             t = {cfg: [] for cfg in runs}
             for _ in range(a.rounds):
                 for cfg, r in runs.items():
                     t[cfg].append(r())
             fl = 2.0 * M * N * K
             for cfg, v in t.items():
-                print(json.dumps({"dtype": "bf16", "shape": name, "M": M, "N": N, "K": K, "cfg": cfg,
+                print(json.dumps({"dtype": "bf16", "shape": name, "layout": lay, "M": M, "N": N, "K": K, "cfg": cfg,
                                   "ms_min": round(min(v), 4), "ms_med": round(statistics.median(v), 4),
                                   "tflops": round(fl / min(v) / 1e9, 1)}), flush=True)
             del runs

@@ -92,3 +92,30 @@ def test_w1_fp8_vs_dequantised(cuda, M, N, K, with_bias, monkeypatch):
     monkeypatch.setenv("REPLICANN_FP8_GEMM", "9")
     out9 = torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, None, 0, None)
     assert rel_err(out, out9) < 5e-3
+
+
+# MN-contiguous B ([K][N], the data gradient dY·W): the transposing LDS reads, the per-lane N-tail
+# check on the DMA
+@pytest.mark.parametrize("M,N,K", [(65536, 768, 3072), (65536, 3072, 768), (8200, 1032, 256), (300, 200, 512),
+                                   (256, 256, 128)])
+def test_w1_bf16_b_mn_vs_fp32(cuda, M, N, K):
+    torch.manual_seed(M + 2 * N + K)
+    a, b = bf(M, K), bf(K, N, scale=0.05)
+    ref = a.float() @ b.float()
+    out = ops.gemm(a, b, tb=False, cfg=11)
+    assert out.shape == (M, N)
+    assert rel_err(out, ref) < 8e-3
+    assert rel_err(out, ops.gemm(a, b, tb=False, cfg=9)) < 8e-3
+
+
+def test_w1_bf16_b_mn_ragged_untouched(cuda):
+    torch.manual_seed(11)
+    M, N, K = 1000, 776, 384
+    a, b = bf(M, K), bf(K, N, scale=0.05)
+    o1 = ops.gemm(a, b, tb=False, cfg=11)
+    big = torch.full((M + 8, 800), 7.0, device="cuda", dtype=torch.bfloat16)
+    view = big[:M, :N]
+    ops.gemm(a, b, tb=False, cfg=11, out=view)
+    assert torch.equal(view, o1)
+    assert rel_err(o1, a.float() @ b.float()) < 8e-3
+    assert bool((big[M:] == 7.0).all()) and bool((big[:, N:] == 7.0).all())
