@@ -298,8 +298,13 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                                !(alpha && alpha->defined()) && !out_fp32 && !accumulate && c.is_contiguous();
             // decode-size GEMMs (M <= 64 rows, x·Wᵀ): the skinny config 10 joins the candidates
             const bool skinny = M <= 64 && !ta && tb && !act_bwd && !accumulate && !want_bg;
-            int cfgs[8] = {9, 1, 6, 0, 2, 8, 0, 0};
+            int cfgs[9] = {9, 1, 6, 0, 2, 8, 0, 0, 0};
             int ncfg = 6;
+            // the one-wave-per-SIMD persistent kernel (gemm_w1.h): A K-contiguous, plain / bias / alpha epilogue
+            const bool w1_ok = !ta && act == 0 && !(residual && residual->defined()) && !accumulate && !out_fp32 &&
+                               !want_bg && Kp % 64 == 0 && Kp >= 128 && N % 8 == 0 && c.stride(0) % 8 == 0 &&
+                               !((bias && bias->defined()) && (alpha && alpha->defined()));
+            if (w1_ok) cfgs[ncfg++] = 11;
             if (plain && lib_candidate()) cfgs[ncfg++] = kLibCfg;
             if (skinny) cfgs[ncfg++] = 10;
             // non-powers of two too: the split that makes tiles × split just fill the 256 CUs
@@ -324,6 +329,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, bool ta, bool tb, const optional<T
                     const int sp = splits[si];
                     if (sp > 1 && Kp / sp < 256) break;
                     if (cfgs[ci] == kLibCfg && sp > 1) break;
+                    if (cfgs[ci] == 11 && sp > 1) break;  // (no split-K form)
                     auto run = [&]() {
                         if (cfgs[ci] == kLibCfg) { lib_gemm(A, B, ta, tb, scratch); return 0; }
                         return rn_gemm(A.data_ptr(), B.data_ptr(), scratch.data_ptr(), optr(bias), optr(residual),

@@ -51,12 +51,18 @@ constexpr int W1_B0 = 2 * W1_STAGE;   // B ring: 3 stages
 constexpr int W1_LDS = 5 * W1_STAGE;  // 160 KiB
 constexpr int W1_WAIT_J = 13;         // block that opens with the end-of-K-tile wait + barrier
 
-enum { W1_EPI = 1, W1_STEADY = 2, W1_LAST = 3 };
+enum { W1_EPI = 1, W1_STEADY = 2, W1_LAST = 3, W1_RES0 = 4 };  // W1_RES0 + q, q = 0..3: residual bodies
 
 // VMEM ops a K-tile issues before its end-of-K-tile wait (block 13): the wait for K-tile t + 1 (whose
 // DMA went out in K-tile t - 1's blocks 1-8) leaves exactly these in flight.  Ops of K-tile t - 1
 // issued after its DMA (an EPI's stores of blocks 9-15) are waited for too: conservative, no branch.
+// (a residual body's 8 loads go out at its start, before its DMA: outside the allowance, so this wait
+// retires them)
 constexpr int w1_before_wait(int kind) { return (kind == W1_LAST ? 8 : 0) + 16 + (kind == W1_EPI ? 24 : 0); }
+// names 8 registers as redefined here, after the wait that retired their loads (no consumer above it)
+RN_DEV void w1_touch8(u32x4* v) {
+    asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+}
 static_assert(w1_before_wait(W1_EPI) <= 63, "vmcnt range");
 
 struct W1Frag {
@@ -125,8 +131,12 @@ RN_DEV int w1_e8m0(const float* s) {
     return (int)((u >> 23) & 0xFF);
 }
 
-template <int FP8, int ACT, bool ALPHA, bool BKC>
+// DBG (timing ablations, REPLICANN_W1_DBG; outputs wrong): bit 0 issues the epilogue stores out of range
+// (same instructions, no traffic), bit 1 the operand DMA (no HBM/L2 traffic; the LDS is still written)
+// RES: + residual (x·Wᵀ + b + r; p.res, row stride p.ldc) added by MFMA — see the residual bodies below
+template <int FP8, int ACT, bool ALPHA, bool BKC, int DBG = 0, bool RES = false>
 __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
+    static_assert(!RES || (BKC && !ALPHA), "w1 residual: x·Wᵀ layout, no alpha");
     static_assert(ACT == ACT_NONE, "w1: forward epilogues without activation (activations: cfg 9)");
     static_assert(!(FP8 && ALPHA), "fp8: the scales ride the MFMA");
     static_assert(BKC || !FP8, "w1: fp8 operands K-contiguous");
@@ -222,6 +232,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             off = (int)w1_opq((uint32_t)b_col[i & 1]) < ncols ? off : 0xFFFFFFF0u;
         }
         const uint32_t dst = lds_addr(smem) + (isA ? W1_A0 : W1_B0) + slot * W1_STAGE + (uint32_t)((8 * w + i) * 1024);
+        if constexpr ((DBG & 2) != 0) off = 0xFFFFFFF0u;
         dma16_at(rs, off, dst);
     };
 
@@ -328,9 +339,46 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             }
         }
     };
+    // ---- residual (RES): the MFMAs add it.  For output pair pp the lane's 16-B residual chunk (row
+    // 16i + (lane&15), columns 32pp + 8G ..; the chunk the lane stores) is the A-side operand of a bf16
+    // 16x16x32 MFMA whose k runs over the pair's 32 columns, and the B side is a one-hot "permutation"
+    // operand Pid[h]: output row n of fragment 2pp + h takes k = 8(n>>2) + 4h + (n&3) — the column the
+    // permuted fragment put there — so acc[i][2pp+h] += r exactly (products r·1, fp32 sums with zeros).
+    // Residual body q (K-tiles 1-4 of a tile) issues pairs 2q, 2q + 1 (8 × 16 B per lane) at its start,
+    // its end-of-K-tile wait retires them (≈ 13 blocks of MFMAs later) and blocks 14-15 run the 16 extra
+    // MFMAs: 4 % more MFMA work per tile, no epilogue VALU, 32 + 8 registers.  Rows past M / columns past
+    // N load zeros. ----
+    [[maybe_unused]] s16x8 pid[2];
+    [[maybe_unused]] u32x4 rres[8];
+    if constexpr (RES) {
+        const int ni = lane & 15;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) pid[h][c] = (G == (ni >> 2) && c == 4 * h + (ni & 3)) ? (short)0x3F80 : (short)0;
+            asm volatile("" : "+v"(pid[h]));
+        }
+    }
+    auto res_issue = [&](int q) {  // pairs 2q, 2q + 1 of the current tile (m0, n0)
+        const u32x4 rs = w1_rsrc(p.res + ((long)m0 * p.ldc + n0), clamp_u(((long)(p.M - m0) * p.ldc - n0) * 2));
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w1_ld16(rres[e * 4 + i], rs, st_off(i, 2 * q + e, n0));
+    };
+    auto res_mma = [&](int q, int e) {  // pair 2q + e (its loads retired)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int jj = 2 * (2 * q + e) + h;
+                acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pid[h], __builtin_bit_cast(s16x8, rres[e * 4 + i]),
+                                                                     acc[i][jj], 0, 0, 0);
+            }
+    };
     auto epi_store = [&](const u32x4* o, int pp, const u32x4& crs, int tn0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pk_st16(o[i], crs, st_off(i, pp, tn0));
+        for (int i = 0; i < 4; ++i) pk_st16(o[i], crs, (DBG & 1) ? 0xFFFFFFF0u : st_off(i, pp, tn0));
     };
 
     // ---- K-tile bodies.  Three straight-line bodies, no branch inside (a uniform branch per block made
@@ -344,9 +392,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
     auto ktile = [&](auto kc, int kt) {
         constexpr int KIND = decltype(kc)::value;
         constexpr bool K0 = KIND == W1_EPI;
+        constexpr int RQ = KIND >= W1_RES0 ? KIND - W1_RES0 : -1;  // residual body q (or -1)
         [[maybe_unused]] u32x4 crs = {0u, 0u, 0u, 0u};
         if constexpr (K0) crs = st_rs(pm_live ? p.C : nullptr, pm0, pn0);
         if constexpr (KIND == W1_LAST) bias_issue(has1, n1);
+        if constexpr (RQ >= 0) res_issue(RQ);
         if constexpr (K0) w1_pin8<16>(braw);  // this tile's bias (issued a K-tile ago; 16 DMA younger)
         constexpr int NW = w1_before_wait(KIND);
         const int an = aslot ^ 1, bn = bslot == 2 ? 0 : bslot + 1;
@@ -366,7 +416,12 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
                 // fragments under blocks 13-15
                 vm_wait<NW>();
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if constexpr (RQ >= 0) w1_touch8(rres);  // this body's residual loads retired
                 __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (RQ >= 0) {
+                if (j == 14) res_mma(RQ, 0);
+                if (j == 15) res_mma(RQ, 1);
             }
             // next K-tile's fragments spread over blocks 13-15 (lgkmcnt counts stay below 16)
             if (j == 13) {
@@ -446,8 +501,16 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
         }
         pm_live = s > 0;
         ktile(KEpi{}, 0);
+        int kt1 = 1;
+        if constexpr (RES) {  // K-tiles 1-4 (host: nk >= 6)
+            ktile(std::integral_constant<int, W1_RES0>{}, 1);
+            ktile(std::integral_constant<int, W1_RES0 + 1>{}, 2);
+            ktile(std::integral_constant<int, W1_RES0 + 2>{}, 3);
+            ktile(std::integral_constant<int, W1_RES0 + 3>{}, 4);
+            kt1 = 5;
+        }
 #pragma unroll 1
-        for (int kt = 1; kt < nk - 1; ++kt) ktile(KSteady{}, kt);
+        for (int kt = kt1; kt < nk - 1; ++kt) ktile(KSteady{}, kt);
         ktile(KLast{}, nk - 1);
     }
     // ---- the last tile's epilogue (exposed; asm accumulator reads as in the loop, after enough wait
@@ -467,9 +530,9 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
 }
 
 // host: persistent grid of min(tiles, CUs) workgroups, 160 KiB LDS each
-template <int FP8, int ACT, bool ALPHA, bool BKC>
+template <int FP8, int ACT, bool ALPHA, bool BKC, int DBG = 0, bool RES = false>
 void launch_w1_t(GemmArgs& a, hipStream_t st) {
-    auto kern = gemm_w1<FP8, ACT, ALPHA, BKC>;
+    auto kern = gemm_w1<FP8, ACT, ALPHA, BKC, DBG, RES>;
     static int attr_dev = -1;
     int dev = 0;
     (void)hipGetDevice(&dev);

@@ -318,6 +318,17 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
                 int act, hipStream_t st, void* q8, float* q8st) {
     if (K % 16 || lda % 16 || ldb % 16) return -1;
     if (q8 && (!pre || (act != ACT_GELU && act != ACT_GELU_D && act != ACT_RELU) || N % 8 || ldc % 8)) return -2;
+    // the one-wave-per-SIMD persistent kernel (gemm_w1.h, default; REPLICANN_FP8_GEMM=11 forces it where it
+    // applies, 0 / 9 select the older kernels): plain / bias / residual epilogues, the power-of-two tensor
+    // scales riding the scaled MFMA (no alpha pass).  profiles/w1_ab_r5a.txt: 1.67-2.30 PF/s on the
+    // GPT-2-medium shapes against 1.39-1.94 for the best older kernel
+    const int kern = fp8_gemm_kernel();
+    if ((kern == 11 || kern < 0) && !q8 && act == ACT_NONE) {
+        rn_gemm_detail::GemmArgs w = {};
+        w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C; w.bias = (const bf16*)bias; w.res = (const bf16*)res;
+        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
+        if (rn_gemm_launch_w1(w, 1, ACT_NONE, st, false) == 0) return 0;
+    }
     scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
     if (q8) fp8_roll_k<<<1, 1, 0, st>>>(q8st);
     rn_gemm_detail::GemmArgs a = {};
@@ -332,13 +343,6 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
     // b64 shapes (profiles/fp8_gemm_ab_r2r.txt): it wins at K = 4096 (1.94 vs 1.85 PF/s) and loses
     // at K = 1024 (1.32 vs 1.59 PF/s: 8 K-tiles per output tile, the per-tile epilogue dominates),
     // so by default it takes K >= 2048 only; REPLICANN_FP8_GEMM=9 forces it, =0 never.
-    const int kern = fp8_gemm_kernel();
-    if (kern == 11 && !q8 && !res && act == ACT_NONE) {
-        rn_gemm_detail::GemmArgs w = {};
-        w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C; w.bias = (const bf16*)bias;
-        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
-        if (rn_gemm_launch_w1(w, 1, ACT_NONE, st, false) == 0) return 0;
-    }
     if (!q8 && N % 8 == 0 && ldc % 8 == 0 && (kern == 9 || (kern < 0 && K >= 2048))) {
         a.tiles_m = (M + 255) / 256;
         a.tiles_n = (N + 255) / 256;

@@ -236,9 +236,10 @@ int rn_gemm(const void* A, const void* B, void* C, const void* bias, const void*
     if (!trans_b && (N % 8 != 0 || ldb % 8 != 0)) return -1;
     if (trans_b && ldb % 8 != 0) return -1;
     if (cfg == 11) {  // one-wave-per-SIMD persistent kernel (gemm_w1.h): x·Wᵀ, plain / bias epilogue
-        if (!trans_a && act == ACT_NONE && !res && !accumulate && !out_f32 && split <= 1 && !colpart) {
+        if (!trans_a && act == ACT_NONE && !accumulate && !out_f32 && split <= 1 && !colpart) {
             GemmArgs w = {};
             w.A = (const bf16*)A; w.B = (const bf16*)B; w.C = C; w.bias = (const bf16*)bias; w.alpha = alpha;
+            w.res = (const bf16*)res;
             w.M = M; w.N = N; w.K = K * 2; w.lda = lda * 2; w.ldb = ldb * 2; w.ldc = ldc;
             if (rn_gemm_launch_w1(w, 0, act, st, !trans_b) == 0) return 0;
         }

@@ -31,12 +31,19 @@ def main():
                     help="epilogue: 0 none, 2 GELU + pre-activation store (fc fwd), 4 GELU backward reading it")
     ap.add_argument("--bias", action="store_true")
     ap.add_argument("--res", action="store_true", help="residual epilogue (full-tile operand read)")
+    ap.add_argument("--fp8", default=None, help="e4m3 x e4m3 forward GEMM (layout nt) on kernel 0 / 9 / 11")
     a = ap.parse_args()
     ta, tb = a.layout[0] == "t", a.layout[1] == "t"
     torch.manual_seed(0)
     A = torch.randn(*((a.K, a.M) if ta else (a.M, a.K)), device="cuda").bfloat16()
     B = torch.randn(*((a.N, a.K) if tb else (a.K, a.N)), device="cuda").bfloat16()
-    if a.torch:
+    if a.fp8 is not None:
+        os.environ["REPLICANN_FP8_GEMM"] = a.fp8
+        qa, sa = ops.quantize_fp8(A)
+        qb, sb = ops.quantize_fp8(B)
+        bias = torch.randn(a.N, device="cuda").bfloat16() if a.bias else None
+        fn = lambda: torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, None, 0, None)  # noqa: E731
+    elif a.torch:
         Am, Bm = (A.t() if ta else A), (B.t() if tb else B)
         fn = lambda: Am @ Bm  # noqa: E731
     else:
@@ -56,7 +63,7 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     print(json.dumps({"M": a.M, "N": a.N, "K": a.K, "layout": a.layout, "cfg": a.cfg, "split": a.split,
-                      "torch": a.torch, "act": a.act, "res": a.res,
+                      "torch": a.torch, "fp8": a.fp8, "act": a.act, "res": a.res,
                       "ms": round(ms, 4),
                       "tflops": round(2 * a.M * a.N * a.K / ms / 1e9, 1)}), flush=True)
 

@@ -119,3 +119,41 @@ def test_w1_bf16_b_mn_ragged_untouched(cuda):
     assert torch.equal(view, o1)
     assert rel_err(o1, a.float() @ b.float()) < 8e-3
     assert bool((big[M:] == 7.0).all()) and bool((big[:, N:] == 7.0).all())
+
+
+# residual epilogue (x·Wᵀ + b + r): the residual rides bf16 MFMAs against a one-hot operand in K-tiles
+# 1-4 of every tile (nk >= 6; shorter K falls back to cfg 9) — ragged rows / columns load zeros
+@pytest.mark.parametrize("M,N,K", [(65536, 768, 768), (4096, 3072, 1024), (1000, 776, 512), (300, 200, 384),
+                                   (8200, 1032, 3072)])
+def test_w1_bf16_residual_vs_fp32(cuda, M, N, K):
+    torch.manual_seed(M + 3 * N + K)
+    a, b, bias, r = bf(M, K), bf(N, K, scale=0.05), bf(N), bf(M, N, scale=2.0)
+    ref = a.float() @ b.float().t() + bias.float() + r.float()
+    out = ops.gemm(a, b, tb=True, bias=bias, residual=r, cfg=11)
+    assert rel_err(out, ref) < 8e-3
+    assert rel_err(out, ops.gemm(a, b, tb=True, bias=bias, residual=r, cfg=9)) < 8e-3
+
+
+def test_w1_bf16_residual_exact_passthrough(cuda):
+    """A zero weight leaves bias + residual: the one-hot MFMA adds the residual exactly (bf16 values
+    through fp32 sums with zeros), so the output equals the bf16 rounding of r + b."""
+    torch.manual_seed(9)
+    M, N, K = 2048, 1024, 768
+    a, b, bias, r = bf(M, K), torch.zeros(N, K, device="cuda", dtype=torch.bfloat16), bf(N), bf(M, N, scale=3.0)
+    out = ops.gemm(a, b, tb=True, bias=bias, residual=r, cfg=11)
+    assert torch.equal(out, (r.float() + bias.float()).bfloat16())
+
+
+@pytest.mark.parametrize("M,N,K", [(65536, 1024, 1024), (1000, 776, 768), (8192, 1024, 4096)])
+def test_w1_fp8_residual_vs_dequantised(cuda, M, N, K, monkeypatch):
+    torch.manual_seed(M + K + 1)
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    bias, r = bf(N, scale=0.1), bf(M, N)
+    qa, sa = ops.quantize_fp8(x)
+    qb, sb = ops.quantize_fp8(w)
+    ref = ops.dequantize_fp8(qa, sa).float() @ ops.dequantize_fp8(qb, sb).float().t() + bias.float() + r.float()
+    monkeypatch.delenv("REPLICANN_FP8_GEMM", raising=False)  # default: the w1 kernel
+    out = torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, r, 0, None)
+    assert rel_err(out, ref) < 5e-3
+    monkeypatch.setenv("REPLICANN_FP8_GEMM", "0")
+    assert rel_err(out, torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, r, 0, None)) < 5e-3
