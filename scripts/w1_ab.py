@@ -21,8 +21,10 @@ from replicann_amd import _ext, ops  # noqa: E402
 BF16 = [("s_qkv", 2304, 768, "nt"), ("s_proj", 768, 768, "nt"), ("s_fc1_plain", 3072, 768, "nt"),
         ("s_fc2", 768, 3072, "nt"), ("m_qkv", 3072, 1024, "nt"), ("m_fc2", 1024, 4096, "nt"),
         ("s_dgrad_qkv", 768, 2304, "nn"), ("s_dgrad_fc1", 768, 3072, "nn"), ("s_dgrad_fc2", 3072, 768, "nn"),
-        ("s_dgrad_proj", 768, 768, "nn")]
-FP8 = [("m_qkv", 3072, 1024), ("m_proj", 1024, 1024), ("m_fc1_plain", 4096, 1024), ("m_fc2", 1024, 4096)]
+        ("s_dgrad_proj", 768, 768, "nn"), ("s_proj_res", 768, 768, "res"), ("s_fc2_res", 768, 3072, "res"),
+        ("m_proj_res", 1024, 1024, "res"), ("m_fc2_res", 1024, 4096, "res")]
+FP8 = [("m_qkv", 3072, 1024, False), ("m_proj", 1024, 1024, False), ("m_fc1_plain", 4096, 1024, False),
+       ("m_fc2", 1024, 4096, False), ("m_proj_res", 1024, 1024, True), ("m_fc2_res", 1024, 4096, True)]
 
 
 def graph_time(fn, iters):
@@ -60,10 +62,12 @@ def main():
     if a.only in (None, "bf16"):
         for name, N, K, lay in BF16:
             x = torch.randn(M, K, device="cuda").bfloat16()
-            nt = lay == "nt"
+            nt = lay != "nn"
             w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16() if nt else (torch.randn(K, N, device="cuda") * 0.05).bfloat16()
             bias = (torch.randn(N, device="cuda") * 0.1).bfloat16() if nt else None
-            runs = {cfg: graph_time(lambda cfg=cfg: ops.gemm(x, w, tb=nt, bias=bias, cfg=cfg), a.iters) for cfg in (9, 11)}
+            res = torch.randn(M, N, device="cuda").bfloat16() if lay == "res" else None
+            runs = {cfg: graph_time(lambda cfg=cfg: ops.gemm(x, w, tb=nt, bias=bias, residual=res, cfg=cfg), a.iters)
+                    for cfg in (9, 11)}
             t = {cfg: [] for cfg in runs}
             for _ in range(a.rounds):
                 for cfg, r in runs.items():
@@ -75,16 +79,17 @@ def main():
                                   "tflops": round(fl / min(v) / 1e9, 1)}), flush=True)
             del runs
     if a.only in (None, "fp8"):
-        for name, N, K in FP8:
+        for name, N, K, with_res in FP8:
             x = torch.randn(M, K, device="cuda").bfloat16()
             w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
             bias = (torch.randn(N, device="cuda") * 0.1).bfloat16()
             qa, sa = ops.quantize_fp8(x)
             qb, sb = ops.quantize_fp8(w)
+            res = torch.randn(M, N, device="cuda").bfloat16() if with_res else None
             runs = {}
             for kern in ("0", "9", "11"):
                 os.environ["REPLICANN_FP8_GEMM"] = kern
-                runs[kern] = graph_time(lambda: torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, None, 0, None), a.iters)
+                runs[kern] = graph_time(lambda: torch.ops.replicann.gemm_fp8(qa, qb, sa, sb, bias, res, 0, None), a.iters)
             t = {k: [] for k in runs}
             for _ in range(a.rounds):
                 for k, r in runs.items():
