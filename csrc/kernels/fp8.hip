@@ -257,6 +257,7 @@ int fp8_gemm_kernel() {
 
 void rn_gemm_launch_pk_fp8(rn_gemm_detail::GemmArgs& a, int act, hipStream_t st);
 int rn_gemm_launch_w1(rn_gemm_detail::GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn);
+int rn_gemm_launch_w1_wgrad(rn_gemm_detail::GemmArgs& a, int fp8, int split, hipStream_t st);
 void rn_gemm_launch_pk_fp8_wgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 void rn_gemm_launch_pk_fp8_dgrad(rn_gemm_detail::GemmArgs& a, int a_bf8, hipStream_t st);
 
@@ -264,7 +265,9 @@ extern "C" {
 
 // state must hold >= 2 floats; it is (re)initialised here (memset node + 2 kernels).
 void rn_fp8_quantize(const void* x, long n, void* q, float* state, hipStream_t st) {
-    (void)hipMemsetAsync(state, 0, 2 * sizeof(float), st);
+    // all 4 slot floats: a first (current-scaling) quantisation is copied whole into a training slot,
+    // whose [2] / [3] must not carry uninitialised bytes (run-to-run bitwise state_dicts)
+    (void)hipMemsetAsync(state, 0, 4 * sizeof(float), st);
     amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
     quant_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
@@ -362,23 +365,40 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
 // `accumulate`.  ws: split · M · N floats (rn_gemm_fp8_wgrad_ws).  Requirements: M, N, lda, ldb
 // multiples of 16, K a multiple of 128.
 long rn_gemm_fp8_wgrad_split(int M, int N, int K) {
-    // ~2 items per CU over 256 CUs (long K: the per-item epilogue is negligible), K slices of whole
-    // 128-deep K-tiles
+    // K slices of whole 128-deep K-tiles, an exact division of the K-tiles (the one-wave-per-SIMD kernel's
+    // split-K walk) with >= 2 per slice: the divisor with the shortest makespan over 256 CUs, each item
+    // costed as its K-tiles + 2 for its epilogue / pipeline fill (ties: fewer slabs)
     const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
-    long s = (512 + tiles - 1) / tiles;
     const long kt = K / 128;
-    if (s > kt) s = kt;
-    if (s < 1) s = 1;
-    const long per = (kt + s - 1) / s;
-    return (kt + per - 1) / per;
+    long best = 1, best_cost = -1;
+    for (long d = 1; d <= kt / 2; ++d) {
+        if (kt % d) continue;
+        const long rounds = (tiles * d + 255) / 256;
+        const long cost = rounds * (kt / d + 2);
+        if (best_cost < 0 || cost < best_cost) {
+            best = d;
+            best_cost = cost;
+        }
+    }
+    return best;
 }
 long rn_gemm_fp8_wgrad_ws(int M, int N, int K) { return rn_gemm_fp8_wgrad_split(M, N, K) * (long)M * N; }
 int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, const float* sb, float* alpha_ws,
                       float* ws, int M, int N, int K, long lda, long ldb, long ldc, int accumulate, int out_f32,
                       int a_bf8, hipStream_t st) {
     if (M % 16 || N % 16 || lda % 16 || ldb % 16 || K % 128 || M <= 0 || N <= 0) return -1;
-    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
     const int split = (int)rn_gemm_fp8_wgrad_split(M, N, K);
+    const int kern = fp8_gemm_kernel();
+    if (kern == 11 || kern < 0) {
+        // the one-wave-per-SIMD kernel: both operands MN-contiguous (tr_b8 reads), split-K fp32 slabs, the
+        // power-of-two scales on the scaled MFMA; then the fixed-order slab sum
+        rn_gemm_detail::GemmArgs w = {};
+        w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C; w.ws = ws;
+        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
+        w.out_f32 = out_f32; w.accumulate = accumulate;
+        if (rn_gemm_launch_w1_wgrad(w, a_bf8 ? 2 : 1, split, st) == 0) return 0;
+    }
+    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
     const int kt = K / 128, per = (kt + split - 1) / split;
     rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.ws = ws; a.alpha = alpha_ws;
@@ -397,6 +417,15 @@ int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, 
 int rn_gemm_fp8_dgrad(const void* A8, const void* B8, void* C, const float* sa, const float* sb, float* alpha_ws,
                       int M, int N, int K, long lda, long ldb, long ldc, int a_bf8, hipStream_t st) {
     if (K % 16 || N % 16 || lda % 16 || ldb % 16 || ldc % 8 || M <= 0) return -1;
+    const int kern = fp8_gemm_kernel();
+    if ((kern == 11 || kern < 0) && K % 128 == 0 && K >= 256) {
+        // the one-wave-per-SIMD kernel with its fp8 MN-contiguous B path (tr_b8 reads of W as stored; the
+        // power-of-two scales ride the scaled MFMA, no alpha pass)
+        rn_gemm_detail::GemmArgs w = {};
+        w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C;
+        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
+        if (rn_gemm_launch_w1(w, a_bf8 ? 2 : 1, ACT_NONE, st, true) == 0) return 0;
+    }
     scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
     rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.alpha = alpha_ws;

@@ -64,6 +64,8 @@ DGRAD_SHAPES = [  # (tokens M, K = out features, N = in features)
     (16384, 1024, 1024),   # attention c_proj dgrad
     (1000, 400, 272),      # ragged M / K (not a K-tile multiple) / N
     (64, 128, 16),         # one K-tile, one narrow column group
+    (1000, 512, 272),      # the one-wave-per-SIMD kernel (K % 128 == 0) with ragged rows and a 16-column tail
+    (300, 256, 48),        # its shortest K (2 K-tiles), one partial column tile
 ]
 
 
@@ -134,3 +136,48 @@ def test_fp8_model_wgrad_tracks_bf16_wgrad(cuda, dgrad):
     for n in names:
         a, b = grads[True][n], grads[False][n]
         assert ((a - b).norm() / b.norm().clamp_min(1e-12)) < (0.12 if dgrad else 0.08), n
+
+
+@pytest.mark.parametrize("shape", [(16384, 3072, 1024), (1000, 512, 272), (300, 256, 48)], ids=lambda s: "x".join(map(str, s)))
+def test_fp8_dgrad_w1_matches_older_kernel(cuda, shape, monkeypatch):
+    """The one-wave-per-SIMD fp8 data gradient (default for K % 128 == 0: tr_b8 reads of W as stored,
+    e5m2 A through the scaled MFMA's format operand) against the older persistent kernel on the same
+    operands: the same exact products, only accumulation order and the bf16 rounding differ."""
+    M, K, N = shape
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dy = (torch.randn(M, K, generator=g) * 0.01).to(cuda, torch.bfloat16)
+    w = (torch.randn(K, N, generator=g) * 0.02).to(cuda, torch.bfloat16)
+    gs = torch.zeros(4, device=cuda)
+    dy8 = torch.ops.replicann.bf8_quantize(dy, gs, False)
+    w8, ws = ops.quantize_fp8(w)
+    monkeypatch.delenv("REPLICANN_FP8_GEMM", raising=False)
+    new = torch.ops.replicann.gemm_fp8_dgrad(dy8, w8, gs, ws, True)
+    monkeypatch.setenv("REPLICANN_FP8_GEMM", "9")
+    old = torch.ops.replicann.gemm_fp8_dgrad(dy8, w8, gs, ws, True)
+    assert ((new.float() - old.float()).norm() / old.float().norm()).item() < 4e-3
+    monkeypatch.delenv("REPLICANN_FP8_GEMM", raising=False)  # bitwise repeatable
+    assert torch.equal(new, torch.ops.replicann.gemm_fp8_dgrad(dy8, w8, gs, ws, True))
+
+
+@pytest.mark.parametrize("shape", [(16384, 3072, 1024), (1024, 400, 272), (65536, 1024, 1024)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_fp8_wgrad_w1_matches_older_kernel(cuda, shape, monkeypatch):
+    """The one-wave-per-SIMD fp8 weight gradient (default: both operands MN-contiguous through tr_b8 reads,
+    split-K over an exact division of the K-tiles, fp32 slabs, the fixed-order slab sum) against the older
+    persistent kernel on the same operands, fp32 output: equal up to fp32 summation order."""
+    K, M, N = shape
+    g = torch.Generator(device="cpu").manual_seed(12)
+    dy = (torch.randn(K, M, generator=g) * 0.01).to(cuda, torch.bfloat16)
+    x = torch.randn(K, N, generator=g).to(cuda, torch.bfloat16)
+    dy8, gs, x8, xs = _q(dy, x)
+    monkeypatch.delenv("REPLICANN_FP8_GEMM", raising=False)
+    new = torch.zeros(M, N, device=cuda, dtype=torch.float32)
+    torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, new, False, True)
+    monkeypatch.setenv("REPLICANN_FP8_GEMM", "9")
+    old = torch.zeros(M, N, device=cuda, dtype=torch.float32)
+    torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, old, False, True)
+    assert ((new - old).norm() / old.norm()).item() < 2e-5
+    monkeypatch.delenv("REPLICANN_FP8_GEMM", raising=False)
+    again = torch.zeros_like(new)
+    torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, again, False, True)
+    assert torch.equal(new, again)
