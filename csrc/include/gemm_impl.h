@@ -75,6 +75,8 @@ struct GemmArgs {
     // two, ops/fp8.py) ride the scaled MFMA's E8M0 block-scale operands instead of an epilogue multiply
     const float* sa;
     const float* sb;
+    // cfg 11 tile walk: tile-rows per group (0: GROUP_M)
+    int group_m;
 };
 
 template <int BN, int NT>
@@ -169,6 +171,17 @@ RN_DEV void group_tile(int id, int tiles_m, int tiles_n, int& tm, int& tn) {
     const int gid = id / per_group;
     const int first_m = gid * GROUP_M;
     const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int in = id % per_group;
+    tm = first_m + in % gsz;
+    tn = in / gsz;
+}
+
+// the same with a run-time group height
+RN_DEV void group_tile_g(int id, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+    const int per_group = gm * tiles_n;
+    const int gid = id / per_group;
+    const int first_m = gid * gm;
+    const int gsz = min(tiles_m - first_m, gm);
     const int in = id % per_group;
     tm = first_m + in % gsz;
     tn = in / gsz;

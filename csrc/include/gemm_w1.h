@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             sd = it / tiles;
             it -= sd * tiles;
         }
-        group_tile(it, p.tiles_m, p.tiles_n, tm, tn);
+        group_tile_g(it, p.tiles_m, p.tiles_n, p.group_m > 0 ? p.group_m : GROUP_M, tm, tn);
         m0 = tm * 256;
         n0 = tn * 256;
         kt0 = sd * nk;

@@ -11,7 +11,18 @@ using namespace rn_gemm_detail;
 // a: A K-contiguous, B K-contiguous ([N][K], bmn false) or MN-contiguous ([K][N], bmn true; fp8: plain
 // epilogue, N % 16 == 0; fp8 == 2: A in e5m2);
 // K, lda, ldb in BYTES (K % 128 == 0, K >= 256); ldc in elements; N % 8 == 0
+// tile-rows per group of the persistent walk: REPLICANN_W1_GROUP (A/B), else 8 (cfg 9's GROUP_M)
+static int w1_group_m(const GemmArgs& a) {
+    static const int env = [] {
+        const char* e = std::getenv("REPLICANN_W1_GROUP");
+        return e ? std::atoi(e) : 0;
+    }();
+    (void)a;
+    return env > 0 ? env : GROUP_M;
+}
+
 int rn_gemm_launch_w1(GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn) {
+    a.group_m = w1_group_m(a);
     if (a.K % 128 || a.K < 256 || a.N % 8 || a.ldc % 8 || a.lda % 16 || a.ldb % 16) return -1;
     if (act != ACT_NONE) return -1;
     if (a.alpha && a.bias) return -1;
@@ -61,6 +72,7 @@ int rn_gemm_launch_w1(GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn) {
 // floats) summed by splitk_reduce_k into C (bf16 or fp32, accumulate or not).  K, lda, ldb in bytes;
 // M, N % 16; K / 128 divisible by split with >= 2 K-tiles per slab.
 int rn_gemm_launch_w1_wgrad(GemmArgs& a, int fp8, int split, hipStream_t st) {
+    a.group_m = w1_group_m(a);
     const int kt = a.K / 128;
     if (a.K % 128 || a.M % 16 || a.N % 16 || a.lda % 16 || a.ldb % 16 || split < 1 || kt % split || kt / split < 2)
         return -1;

@@ -22,15 +22,17 @@ from .linear import _act_ref, _pre_ref
 
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
-# fp8 weight gradients (dW = dYᵀ·X with dY in e5m2, X the forward's e4m3 copy) of the fp8 layers:
-# REPLICANN_FP8_WGRAD=1 (or Fp8State.wgrad).  Opt-in: measured on the MI355X without a step gain
-# (GPT-2-medium 1.03x the bf16 model with or without it; per-shape fp8 wgrad 0.57-0.99x bf16 —
-# profiles/fp8_bwd_r4g.txt), and the loss trajectory moves 2.0 % from bf16 against 1.8 % without
-FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "0") == "1"
-# fp8 data gradients (dX = dY·W with the same e5m2 dY and the forward's e4m3 weight) of the fp8
-# layers whose dgrad has a plain epilogue: REPLICANN_FP8_DGRAD=1 (or Fp8State.dgrad); opt-in for the
-# same reason (per shape 0.79-1.19x bf16, step +1 % with both on)
-FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "0") == "1"
+# fp8 backward of the fp8 layers (the Transformer-Engine hybrid recipe: dY quantised once to e5m2 with its
+# own delayed scale): weight gradients dW = dYᵀ·X against the forward's e4m3 input copy
+# (REPLICANN_FP8_WGRAD, Fp8State.wgrad) and data gradients dX = dY·W against the forward's e4m3 weight,
+# for the layers whose dgrad has a plain epilogue (REPLICANN_FP8_DGRAD, Fp8State.dgrad).  On by default
+# since round 5: on the one-wave-per-SIMD kernels (csrc/include/gemm_w1.h) the fp8 dgrad runs 1.5-2.0
+# PF/s and the fp8 wgrad 1.5-1.7x the bf16 one per shape, GPT-2-medium 146.8 ms/step with both against
+# 157.0 (dgrad only) / 158.5 (forward only) / 165 (bf16) (profiles/w1_fp8_bwd_r5f.txt,
+# profiles/gpt2m_fp8_r5g.txt); 50-step loss trajectory vs bf16: max rel dev 3.2 % in the steep descent
+# (steps 9-19), 0.8 % at step 50.  =0 turns either off.
+FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "1") == "1"
+FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "1") == "1"
 
 
 def pow2_ceil(s):
