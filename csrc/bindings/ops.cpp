@@ -92,6 +92,8 @@ void rn_fp8_quantize(const void*, long, void*, float*, hipStream_t);
 void rn_fp8_dequantize(const void*, long, const float*, void*, hipStream_t);
 void rn_fp8_quantize_delayed(const void*, long, void*, float*, hipStream_t);
 void rn_bf8_quantize(const void*, long, void*, float*, int, hipStream_t);
+int rn_act_mul_bf8_groups(long, int);
+void rn_act_mul_bf8(const void*, const void*, long, int, void*, float*, int, float*, hipStream_t);
 void rn_bf8_dequantize(const void*, long, const float*, void*, hipStream_t);
 long rn_gemm_fp8_wgrad_ws(int, int, int);
 int rn_gemm_fp8_wgrad(const void*, const void*, void*, const float*, const float*, float*, float*, int, int, int, long,
@@ -1054,6 +1056,33 @@ Tensor fp8_quantize_delayed(const Tensor& x, const Tensor& state) {
 }
 // e5m2 ("bf8") quantisation of a gradient operand: delayed scaling (roll + one pass) or, for a slot
 // without a scale yet, current scaling; state: [scale, amax, amax the scale came from, -]
+// dH = dU ⊙ d (the MLP's GELU backward against the saved gelu'(h)) written only as e5m2 with the gradient
+// slot ``state`` (delayed / current scaling as bf8_quantize); with ``bias_grad`` (bf16 [N]) Σ_rows dH is
+// added into it
+Tensor act_mul_bf8(const Tensor& du, const Tensor& d, const Tensor& state, bool delayed, const optional<Tensor>& bias_grad) {
+    CHECK_BF16(du); CHECK_BF16(d); CHECK_CONTIG(du); CHECK_CONTIG(d); GUARD(du);
+    TORCH_CHECK(du.dim() == 2 && du.sizes() == d.sizes() && du.size(1) % 8 == 0, "act_mul_bf8: matching [M][N] inputs, N % 8");
+    TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda() && state.device() == du.device());
+    const long M = du.size(0);
+    const int N = (int)du.size(1);
+    Tensor q = at::empty(du.sizes(), du.options().dtype(at::kByte));
+    if (M == 0) return q;
+    const bool bg = bias_grad && bias_grad->defined();
+    if (bg)
+        TORCH_CHECK(bias_grad->scalar_type() == at::kBFloat16 && bias_grad->numel() == N && bias_grad->is_contiguous() &&
+                        bias_grad->device() == du.device(),
+                    "act_mul_bf8: bias_grad must be a contiguous bf16 [N] tensor on the same device");
+    const int G = rn_act_mul_bf8_groups(M, N);
+    Tensor part = bg ? at::empty({(int64_t)G * N}, du.options().dtype(at::kFloat)) : Tensor();
+    rn_act_mul_bf8(du.data_ptr(), d.data_ptr(), M, N, q.data_ptr(), state.data_ptr<float>(), delayed ? 1 : 0,
+                   bg ? part.data_ptr<float>() : nullptr, cur_stream());
+    if (bg) {
+        Tensor tmp = at::empty({rn_colsum_ws(N)}, du.options().dtype(at::kFloat));
+        rn_colsum_f32(part.data_ptr<float>(), G, N, tmp.data_ptr<float>(), bias_grad->data_ptr(), 1, cur_stream());
+    }
+    return q;
+}
+
 Tensor bf8_quantize(const Tensor& x, const Tensor& state, bool delayed) {
     CHECK_BF16(x); CHECK_CONTIG(x); GUARD(x);
     TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda());
@@ -1219,6 +1248,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");
     m.def("bf8_quantize(Tensor x, Tensor(a!) state, bool delayed) -> Tensor");
+    m.def("act_mul_bf8(Tensor du, Tensor d, Tensor(a!) state, bool delayed, Tensor(b!)? bias_grad=None) -> Tensor");
     m.def("bf8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("gemm_fp8_wgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) out, bool accumulate, bool a_bf8) -> ()");
     m.def("gemm_fp8_dgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, bool a_bf8) -> Tensor");
@@ -1281,6 +1311,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("fp8_dequantize", &fp8_dequantize);
     m.impl("fp8_quantize_delayed", &fp8_quantize_delayed);
     m.impl("bf8_quantize", &bf8_quantize);
+    m.impl("act_mul_bf8", &act_mul_bf8);
     m.impl("bf8_dequantize", &bf8_dequantize);
     m.impl("gemm_fp8_wgrad", &gemm_fp8_wgrad);
     m.impl("gemm_fp8_dgrad", &gemm_fp8_dgrad);

@@ -176,6 +176,66 @@ __global__ void __launch_bounds__(256) quant_bf8_k(const bf16* __restrict__ x, l
     }
 }
 
+// The GELU backward of the fp8 MLP fused with the e5m2 quantisation of its result: dH = dU ⊙ gelu'(h)
+// (dU = the MLP c_proj's fp8 data gradient, gelu'(h) saved by c_fc's forward epilogue), written ONLY as
+// e5m2 for c_fc's fp8 data / weight gradients, plus per-row-group column partial sums of dH (c_fc's
+// bias gradient, reduced by rn_colsum_f32).  Thread t owns 16-B column chunk t % (N/8) of rows
+// t / (N/8), + G, + 2G, ...  MODE 0: amax of dH only (a slot's first, current-scaling pass); 1: quantise
+// with the scale from that amax (as quant_bf8_k); 2: delayed (scale rolled by fp8_roll_bf8_k, this
+// pass records the new amax).
+template <int MODE>
+__global__ void __launch_bounds__(256) act_mul_bf8_k(const bf16* __restrict__ du, const bf16* __restrict__ dd, long M,
+                                                     int N, uint8_t* __restrict__ q, float* __restrict__ state,
+                                                     float* __restrict__ colpart, int G) {
+    __shared__ float sm[16];
+    const int nc = N / 8;
+    const long t = blockIdx.x * 256L + threadIdx.x;
+    const bool live = t < (long)G * nc;
+    const int c = (int)(t % nc), g = (int)(t / nc);
+    float inv = 1.f;
+    if constexpr (MODE == 1) {
+        const float amax = state[1];
+        const float scale = amax > 0.f ? pow2_ceil(amax / E5M2_MAX) : 1.f;
+        inv = 1.f / scale;
+        if (t == 0) state[0] = scale;
+    } else if constexpr (MODE == 2) {
+        inv = 1.f / state[0];
+    }
+    float m = 0.f, cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        for (long r = g; r < M; r += G) {
+            const long off = r * N + c * 8;
+            float a[8], b[8];
+            load8(du + off, a);
+            load8(dd + off, b);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float h = a[j] * b[j];
+                m = fmaxf(m, fabsf(h));
+                cs[j] += h;
+                a[j] = fminf(fmaxf(h * inv, -E5M2_MAX), E5M2_MAX);
+            }
+            if constexpr (MODE != 0) {
+                int w0 = 0, w1 = 0;
+                w0 = __builtin_amdgcn_cvt_pk_bf8_f32(a[0], a[1], w0, false);
+                w0 = __builtin_amdgcn_cvt_pk_bf8_f32(a[2], a[3], w0, true);
+                w1 = __builtin_amdgcn_cvt_pk_bf8_f32(a[4], a[5], w1, false);
+                w1 = __builtin_amdgcn_cvt_pk_bf8_f32(a[6], a[7], w1, true);
+                *reinterpret_cast<int2*>(q + off) = make_int2(w0, w1);
+            }
+        }
+        if (MODE != 0 && colpart) {
+            float4* cp = reinterpret_cast<float4*>(colpart + (long)g * N + c * 8);
+            cp[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+            cp[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+        }
+    }
+    if constexpr (MODE != 1) {
+        m = block_max(m, sm);
+        if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
+    }
+}
+
 __global__ void dequant_bf8_k(const uint8_t* __restrict__ q, long n, const float* __restrict__ state,
                               bf16* __restrict__ y) {
     const float scale = state[0];
@@ -309,6 +369,28 @@ void rn_bf8_quantize(const void* x, long n, void* q, float* state, int delayed, 
     amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
     quant_bf8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
+// dH = dU ⊙ d in e5m2 (+ column partials [G][N] of dH when colpart): see act_mul_bf8_k.  N % 8 == 0.
+int rn_act_mul_bf8_groups(long M, int N) {
+    const long nc = N / 8;
+    long g = (65536 + nc - 1) / nc;  // ~64 k threads
+    if (g > M) g = M;
+    return (int)(g < 1 ? 1 : g);
+}
+void rn_act_mul_bf8(const void* du, const void* d, long M, int N, void* q, float* state, int delayed, float* colpart,
+                    hipStream_t st) {
+    const int G = rn_act_mul_bf8_groups(M, N);
+    const long threads = (long)G * (N / 8);
+    const int blocks = (int)((threads + 255) / 256);
+    if (delayed) {
+        fp8_roll_bf8_k<<<1, 1, 0, st>>>(state);
+        act_mul_bf8_k<2><<<blocks, 256, 0, st>>>((const bf16*)du, (const bf16*)d, M, N, (uint8_t*)q, state, colpart, G);
+        return;
+    }
+    (void)hipMemsetAsync(state, 0, 2 * sizeof(float), st);
+    act_mul_bf8_k<0><<<blocks, 256, 0, st>>>((const bf16*)du, (const bf16*)d, M, N, (uint8_t*)q, state, nullptr, G);
+    act_mul_bf8_k<1><<<blocks, 256, 0, st>>>((const bf16*)du, (const bf16*)d, M, N, (uint8_t*)q, state, colpart, G);
+}
+
 void rn_bf8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
     dequant_bf8_k<<<gridn(n), 256, 0, st>>>((const uint8_t*)q, n, state, (bf16*)y);
 }

@@ -33,6 +33,10 @@ E5M2_MAX = 57344.0
 # (steps 9-19), 0.8 % at step 50.  =0 turns either off.
 FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "1") == "1"
 FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "1") == "1"
+# fp8 MLP backward with both layers' fp8 gradients: the MLP c_proj data gradient on the fp8 GEMM and the
+# GELU backward fused into the e5m2 quantisation of dH (ops.linear._MLPFn._fp8_backward); 0: the bf16
+# c_proj dgrad with the multiply in its epilogue + a separate e5m2 pass (A/B)
+FP8_MLP_FUSE = os.environ.get("REPLICANN_FP8_MLP_FUSE", "1") == "1"
 
 
 def pow2_ceil(s):
@@ -203,6 +207,24 @@ class Fp8State:
             self.g_ready = False
         st = self.gt[0]
         q = quantize_bf8(dy, st, self.g_ready)
+        self.g_ready = True
+        return q, st
+
+    def gquant_mul(self, du, d, bias_grad=None):
+        """dH = dU ⊙ d (the MLP's GELU backward against the saved gelu'(h)) straight to e5m2 with the
+        gradient slot — dH itself is never written in bf16 — and Σ_rows dH added into ``bias_grad`` (bf16
+        [N]) when given.  Scaling as :meth:`gquant`."""
+        if self.gt is None or self.gt.device != du.device:
+            self.gt = torch.zeros(1, 4, device=du.device, dtype=torch.float32)
+            self.g_ready = False
+        st = self.gt[0]
+        if _ext.use_native(du):
+            q = _ext.ops().act_mul_bf8(du, d, st, self.g_ready, bias_grad)
+        else:
+            dh = du.float() * d.float()
+            if bias_grad is not None:
+                bias_grad.add_(dh.sum(0).to(bias_grad.dtype))
+            q = quantize_bf8(dh, st, self.g_ready)
         self.g_ready = True
         return q, st
 

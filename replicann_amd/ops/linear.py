@@ -361,7 +361,8 @@ class _MLPFn(torch.autograd.Function):
                 ctx.x8 = (sv, None)
             else:
                 u = fp8_forward(x2, w1, b1, None, _MLP_FWD_ACT[act], pre, fp8[0], out8=fp8[1])
-            if fp8[1] is not None and ctx.needs_input_grad[3] and fp8[1].wgrad:
+            if fp8[1] is not None and ((ctx.needs_input_grad[3] and fp8[1].wgrad) or fp8[1].dgrad):
+                # (the e4m3 weight also for layer 2's fp8 data gradient: see _MLPFn._fp8_backward)
                 y, sv2 = fp8_forward(u, w2, b2, res2, ACT_NONE, None, fp8[1], keep=True)
                 ctx.x8 = (ctx.x8[0], sv2)
             elif fp8[1] is not None:
@@ -376,6 +377,43 @@ class _MLPFn(torch.autograd.Function):
         return y.reshape(*shp[:-1], w2.shape[0])
 
     @staticmethod
+    def _fp8_backward(ctx, gy, gy2, x2, w1, pre, u, w2, sv1, sv2):
+        """Both layers' gradients in fp8 with the GELU backward fused into the e5m2 quantisation of
+        dH: dY → e5m2 once (layer 2's dgrad + wgrad), dU = dY·W2 on the fp8 dgrad GEMM, then ONE pass
+        dH8 = e5m2(dU ⊙ gelu'(h)) that also reduces layer 1's bias gradient (csrc/kernels/fp8.hip
+        act_mul_bf8_k), and layer 1's fp8 dgrad / wgrad from dH8.  Replaces the bf16 dgrad GEMM with
+        the multiply in its epilogue + the separate e5m2 pass over dH (profiles/gpt2m_fp8_r5g.txt).
+        Returns the gradient tuple, or None when an operand of that plan is missing."""
+        from .fp8 import FP8_MLP_FUSE, fp8_dgrad, fp8_dgrad_ok
+        nig = ctx.needs_input_grad
+        if not (FP8_MLP_FUSE and nig[0] and nig[1] and _MLP_BWD_ACT[ctx.act] == ACT_MUL_BWD and sv1 is not None and sv2 is not None
+                and sv1[0] is not None and sv1[2] is not None and sv2[2] is not None
+                and fp8_dgrad_ok(gy2, w2.shape[1]) and fp8_dgrad_ok(u, w1.shape[1]) and _fp8_wgrad_ok(u, sv1[0])
+                and pre.shape[1] % 8 == 0):
+            return None
+        dyq2 = sv2[4].gquant(gy2)
+        x8_2 = (sv2[0], sv2[1], sv2[4]) if sv2[0] is not None else None
+        gw2 = _wgrad(gy2, u, w2, True, x8_2, dyq2 if x8_2 is not None else None) if nig[3] else None
+        gb2 = _bias_grad(gy2, ctx.b2, True) if nig[4] else None
+        du = fp8_dgrad(dyq2, sv2[2], sv2[3])
+        b1 = ctx.b1
+        b1_acc, gb1 = None, None
+        if nig[2] and b1 is not None:
+            if not getattr(b1, "_rn_bias_done", False):
+                b1_acc = _direct_grad(b1)
+            if b1_acc is None:
+                gb1 = torch.zeros(b1.shape, device=b1.device, dtype=torch.bfloat16)
+        dyq = sv1[4].gquant_mul(du, pre, b1_acc if b1_acc is not None else gb1)
+        if b1_acc is not None:
+            _notify(b1)
+        elif gb1 is not None:
+            gb1 = gb1.to(b1.dtype)
+        x8_1 = (sv1[0], sv1[1], sv1[4])
+        gw1 = _wgrad(du, x2, w1, True, x8_1, dyq)  # (du: the dH shape for the fp8 path's checks)
+        gx = fp8_dgrad(dyq, sv1[2], sv1[3])
+        return gx.reshape(ctx.shp), gw1, gb1, gw2, gb2, None, gy if ctx.has_res else None, None
+
+    @staticmethod
     def backward(ctx, gy):
         x2, w1, pre, u, w2 = ctx.saved_tensors
         ops = _ext.ops()
@@ -383,6 +421,9 @@ class _MLPFn(torch.autograd.Function):
         nig = ctx.needs_input_grad
         sv1, sv2 = ctx.x8
         ctx.x8 = (None, None)
+        out = _MLPFn._fp8_backward(ctx, gy, gy2, x2, w1, pre, u, w2, sv1, sv2)
+        if out is not None:
+            return out
         x8_2 = (sv2[0], sv2[1], sv2[4]) if sv2 is not None else None
         gw2 = _wgrad(gy2, u, w2, True, x8_2) if nig[3] else None
         gb2 = _bias_grad(gy2, ctx.b2, True) if nig[4] else None

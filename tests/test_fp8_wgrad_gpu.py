@@ -181,3 +181,29 @@ def test_fp8_wgrad_w1_matches_older_kernel(cuda, shape, monkeypatch):
     again = torch.zeros_like(new)
     torch.ops.replicann.gemm_fp8_wgrad(dy8, x8, gs, xs, again, False, True)
     assert torch.equal(new, again)
+
+
+@pytest.mark.parametrize("delayed", [False, True])
+def test_act_mul_bf8_vs_torch(cuda, delayed):
+    """dH = dU ⊙ d straight to e5m2 (the fused GELU backward of the fp8 MLP): the dequantised output
+    against the fp32 product at e5m2 precision, the bias-gradient column sums against fp32, and the
+    slot's scale / amax bookkeeping as bf8_quantize's."""
+    g = torch.Generator(device="cpu").manual_seed(13)
+    M, N = 3000, 4096
+    du = (torch.randn(M, N, generator=g) * 0.01).to(cuda, torch.bfloat16)
+    d = torch.rand(M, N, generator=g).to(cuda, torch.bfloat16) * 1.1
+    ref = du.float() * d.float()
+    st = torch.zeros(4, device=cuda)
+    if delayed:  # a previous pass recorded amax = 2 x this one's
+        st[1] = 2 * ref.abs().max()
+    bg = torch.zeros(N, device=cuda, dtype=torch.bfloat16)
+    q = torch.ops.replicann.act_mul_bf8(du, d, st, delayed, bg)
+    from replicann_amd.ops.fp8 import pow2_ceil
+    amax = ref.abs().max()
+    want = pow2_ceil((2 * 2 * amax if delayed else amax).cpu() / 57344.0).item()
+    assert st[0].item() == want
+    assert abs(st[1].item() - amax.item()) <= 1e-6 * amax.item()
+    deq = q.view(torch.float8_e5m2).float() * st[0]
+    assert ((deq - ref).norm() / ref.norm()).item() < 0.1
+    colsum = ref.sum(0)
+    assert ((bg.float() - colsum).norm() / colsum.norm()).item() < 1e-2
