@@ -41,8 +41,8 @@ class GPT2Config:
     # fp8 also for the attention output projection.  Off by default: its input (the attention
     # output) would need a separate quantisation pass that costs what the fp8 GEMM saves
     # (profiles/fp8_gemm_ab_r2r.txt).  c_attn / c_fc take e4m3 straight from the LayerNorm kernel,
-    # the MLP c_proj from c_fc's GEMM epilogue
-    fp8_proj: bool = False
+    # the MLP c_proj from c_fc's GEMM epilogue (REPLICANN_FP8_PROJ=1: on, for A/B)
+    fp8_proj: bool = os.environ.get("REPLICANN_FP8_PROJ", "0") == "1"
     # LM head + loss over row chunks of this many tokens (0: the whole batch at once).  Bounds the
     # logits buffer (rows x vocab_pad bf16: 6.6 GB at b64 x 1024) for long sequences / big batches
     ce_chunk: int = 0
