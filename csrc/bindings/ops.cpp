@@ -93,7 +93,8 @@ void rn_fp8_dequantize(const void*, long, const float*, void*, hipStream_t);
 void rn_fp8_quantize_delayed(const void*, long, void*, float*, hipStream_t);
 void rn_bf8_quantize(const void*, long, void*, float*, int, hipStream_t);
 int rn_act_mul_bf8_groups(long, int);
-void rn_act_mul_bf8(const void*, const void*, long, int, void*, float*, int, float*, hipStream_t);
+void rn_act_mul_bf8(const void*, const void*, long, int, void*, float*, int, float*, int, hipStream_t);
+void rn_gelu_q8(const void*, long, void*, float*, hipStream_t);
 void rn_bf8_dequantize(const void*, long, const float*, void*, hipStream_t);
 long rn_gemm_fp8_wgrad_ws(int, int, int);
 int rn_gemm_fp8_wgrad(const void*, const void*, void*, const float*, const float*, float*, float*, int, int, int, long,
@@ -1059,7 +1060,8 @@ Tensor fp8_quantize_delayed(const Tensor& x, const Tensor& state) {
 // dH = dU ⊙ d (the MLP's GELU backward against the saved gelu'(h)) written only as e5m2 with the gradient
 // slot ``state`` (delayed / current scaling as bf8_quantize); with ``bias_grad`` (bf16 [N]) Σ_rows dH is
 // added into it
-Tensor act_mul_bf8(const Tensor& du, const Tensor& d, const Tensor& state, bool delayed, const optional<Tensor>& bias_grad) {
+Tensor act_mul_bf8(const Tensor& du, const Tensor& d, const Tensor& state, bool delayed, const optional<Tensor>& bias_grad,
+                   bool from_h) {
     CHECK_BF16(du); CHECK_BF16(d); CHECK_CONTIG(du); CHECK_CONTIG(d); GUARD(du);
     TORCH_CHECK(du.dim() == 2 && du.sizes() == d.sizes() && du.size(1) % 8 == 0, "act_mul_bf8: matching [M][N] inputs, N % 8");
     TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda() && state.device() == du.device());
@@ -1075,11 +1077,21 @@ Tensor act_mul_bf8(const Tensor& du, const Tensor& d, const Tensor& state, bool 
     const int G = rn_act_mul_bf8_groups(M, N);
     Tensor part = bg ? at::empty({(int64_t)G * N}, du.options().dtype(at::kFloat)) : Tensor();
     rn_act_mul_bf8(du.data_ptr(), d.data_ptr(), M, N, q.data_ptr(), state.data_ptr<float>(), delayed ? 1 : 0,
-                   bg ? part.data_ptr<float>() : nullptr, cur_stream());
+                   bg ? part.data_ptr<float>() : nullptr, from_h ? 1 : 0, cur_stream());
     if (bg) {
         Tensor tmp = at::empty({rn_colsum_ws(N)}, du.options().dtype(at::kFloat));
         rn_colsum_f32(part.data_ptr<float>(), G, N, tmp.data_ptr<float>(), bias_grad->data_ptr(), 1, cur_stream());
     }
+    return q;
+}
+
+// e4m3(gelu(h)) with the delayed-scaling slot ``state`` (rolled here, amax recorded): see rn_gelu_q8
+Tensor gelu_q8(const Tensor& h, const Tensor& state) {
+    CHECK_BF16(h); CHECK_CONTIG(h); GUARD(h);
+    TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_cuda() && state.device() == h.device());
+    TORCH_CHECK(h.numel() % 8 == 0, "gelu_q8: numel % 8");
+    Tensor q = at::empty(h.sizes(), h.options().dtype(at::kByte));
+    if (h.numel()) rn_gelu_q8(h.data_ptr(), h.numel(), q.data_ptr(), state.data_ptr<float>(), cur_stream());
     return q;
 }
 
@@ -1248,7 +1260,8 @@ TORCH_LIBRARY(replicann, m) {
     m.def("fp8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("fp8_quantize_delayed(Tensor x, Tensor state) -> Tensor");
     m.def("bf8_quantize(Tensor x, Tensor(a!) state, bool delayed) -> Tensor");
-    m.def("act_mul_bf8(Tensor du, Tensor d, Tensor(a!) state, bool delayed, Tensor(b!)? bias_grad=None) -> Tensor");
+    m.def("act_mul_bf8(Tensor du, Tensor d, Tensor(a!) state, bool delayed, Tensor(b!)? bias_grad=None, bool from_h=False) -> Tensor");
+    m.def("gelu_q8(Tensor h, Tensor(a!) state) -> Tensor");
     m.def("bf8_dequantize(Tensor q, Tensor state) -> Tensor");
     m.def("gemm_fp8_wgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) out, bool accumulate, bool a_bf8) -> ()");
     m.def("gemm_fp8_dgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, bool a_bf8) -> Tensor");
@@ -1312,6 +1325,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("fp8_quantize_delayed", &fp8_quantize_delayed);
     m.impl("bf8_quantize", &bf8_quantize);
     m.impl("act_mul_bf8", &act_mul_bf8);
+    m.impl("gelu_q8", &gelu_q8);
     m.impl("bf8_dequantize", &bf8_dequantize);
     m.impl("gemm_fp8_wgrad", &gemm_fp8_wgrad);
     m.impl("gemm_fp8_dgrad", &gemm_fp8_dgrad);

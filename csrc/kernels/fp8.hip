@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(256) quant_bf8_k(const bf16* __restrict__ x, l
 // t / (N/8), + G, + 2G, ...  MODE 0: amax of dH only (a slot's first, current-scaling pass); 1: quantise
 // with the scale from that amax (as quant_bf8_k); 2: delayed (scale rolled by fp8_roll_bf8_k, this
 // pass records the new amax).
-template <int MODE>
+template <int MODE, bool FROM_H>
 __global__ void __launch_bounds__(256) act_mul_bf8_k(const bf16* __restrict__ du, const bf16* __restrict__ dd, long M,
                                                      int N, uint8_t* __restrict__ q, float* __restrict__ state,
                                                      float* __restrict__ colpart, int G) {
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(256) act_mul_bf8_k(const bf16* __restrict__ du
     auto one = [&](long off, float* a, const float* b) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float h = a[j] * b[j];
+            const float h = a[j] * (FROM_H ? gelu_grad_f(b[j]) : b[j]);
             m = fmaxf(m, fabsf(h));
             cs[j] += h;
             a[j] = fminf(fmaxf(h * inv, -E5M2_MAX), E5M2_MAX);
@@ -391,19 +391,62 @@ int rn_act_mul_bf8_groups(long M, int N) {
     if (g > M) g = M;
     return (int)(g < 1 ? 1 : g);
 }
-void rn_act_mul_bf8(const void* du, const void* d, long M, int N, void* q, float* state, int delayed, float* colpart,
-                    hipStream_t st) {
+extern "C++" template <bool FROM_H>
+static void act_mul_bf8_run(const void* du, const void* d, long M, int N, void* q, float* state, int delayed,
+                            float* colpart, hipStream_t st) {
     const int G = rn_act_mul_bf8_groups(M, N);
     const long threads = (long)G * (N / 8);
     const int blocks = (int)((threads + 255) / 256);
+    const bf16 *a = (const bf16*)du, *b = (const bf16*)d;
     if (delayed) {
         fp8_roll_bf8_k<<<1, 1, 0, st>>>(state);
-        act_mul_bf8_k<2><<<blocks, 256, 0, st>>>((const bf16*)du, (const bf16*)d, M, N, (uint8_t*)q, state, colpart, G);
+        act_mul_bf8_k<2, FROM_H><<<blocks, 256, 0, st>>>(a, b, M, N, (uint8_t*)q, state, colpart, G);
         return;
     }
     (void)hipMemsetAsync(state, 0, 2 * sizeof(float), st);
-    act_mul_bf8_k<0><<<blocks, 256, 0, st>>>((const bf16*)du, (const bf16*)d, M, N, (uint8_t*)q, state, nullptr, G);
-    act_mul_bf8_k<1><<<blocks, 256, 0, st>>>((const bf16*)du, (const bf16*)d, M, N, (uint8_t*)q, state, colpart, G);
+    act_mul_bf8_k<0, FROM_H><<<blocks, 256, 0, st>>>(a, b, M, N, (uint8_t*)q, state, nullptr, G);
+    act_mul_bf8_k<1, FROM_H><<<blocks, 256, 0, st>>>(a, b, M, N, (uint8_t*)q, state, colpart, G);
+}
+// from_h: d holds the pre-activation h and the kernel takes gelu'(h) itself (the fp8 MLP whose forward kept
+// h instead of gelu'(h), rn_gelu_q8)
+void rn_act_mul_bf8(const void* du, const void* d, long M, int N, void* q, float* state, int delayed, float* colpart,
+                    int from_h, hipStream_t st) {
+    if (from_h) act_mul_bf8_run<true>(du, d, M, N, q, state, delayed, colpart, st);
+    else act_mul_bf8_run<false>(du, d, M, N, q, state, delayed, colpart, st);
+}
+
+// The fp8 MLP's activation as its own pass: q8 = e4m3(bf16(gelu(h))) with the consumer's delayed scale
+// (rolled here; this pass records amax(|gelu(h)|)), from the bf16 pre-activation h the c_fc GEMM wrote on the
+// one-wave-per-SIMD kernel.  The MLP then keeps h for the backward (gelu'(h) is re-derived inside
+// act_mul_bf8_k) and never writes gelu(h) or gelu'(h) in bf16: 2 B/element less than the fused-epilogue
+// GEMM's three outputs.
+__global__ void __launch_bounds__(256) gelu_q8_k(const bf16* __restrict__ h, long n, uint8_t* __restrict__ q,
+                                                 float* __restrict__ state) {
+    __shared__ float sm[16];
+    const float inv = 1.f / state[0];
+    float m = 0.f;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
+        float f[8];
+        load8(h + i * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float u = (float)(bf16)gelu_f(f[j]);
+            m = fmaxf(m, fabsf(u));
+            f[j] = fminf(fmaxf(u * inv, -E4M3_MAX), E4M3_MAX);
+        }
+        int w0 = 0, w1 = 0;
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+        *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    }
+    m = block_max(m, sm);
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
+}
+void rn_gelu_q8(const void* h, long n, void* q, float* state, hipStream_t st) {
+    fp8_roll_k<<<1, 1, 0, st>>>(state);
+    gelu_q8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)h, n, (uint8_t*)q, state);
 }
 
 void rn_bf8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {

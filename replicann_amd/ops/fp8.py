@@ -210,18 +210,23 @@ class Fp8State:
         self.g_ready = True
         return q, st
 
-    def gquant_mul(self, du, d, bias_grad=None):
+    def gquant_mul(self, du, d, bias_grad=None, from_h=False):
         """dH = dU ⊙ d (the MLP's GELU backward against the saved gelu'(h)) straight to e5m2 with the
         gradient slot — dH itself is never written in bf16 — and Σ_rows dH added into ``bias_grad`` (bf16
-        [N]) when given.  Scaling as :meth:`gquant`."""
+        [N]) when given.  ``from_h``: ``d`` holds the pre-activation h, gelu'(h) is taken here.  Scaling
+        as :meth:`gquant`."""
         if self.gt is None or self.gt.device != du.device:
             self.gt = torch.zeros(1, 4, device=du.device, dtype=torch.float32)
             self.g_ready = False
         st = self.gt[0]
         if _ext.use_native(du):
-            q = _ext.ops().act_mul_bf8(du, d, st, self.g_ready, bias_grad)
+            q = _ext.ops().act_mul_bf8(du, d, st, self.g_ready, bias_grad, from_h)
         else:
-            dh = du.float() * d.float()
+            dd = d.float()
+            if from_h:
+                from .linear import ACT_GELU, _act_grad_ref
+                dd = _act_grad_ref(torch.ones_like(dd), d, ACT_GELU)
+            dh = du.float() * dd
             if bias_grad is not None:
                 bias_grad.add_(dh.sum(0).to(bias_grad.dtype))
             q = quantize_bf8(dh, st, self.g_ready)

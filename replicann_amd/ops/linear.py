@@ -351,6 +351,22 @@ class _MLPFn(torch.autograd.Function):
         ops = _ext.ops()
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
         ctx.x8 = (None, None)
+        ctx.pre_is_h = False
+        if fp8 is not None and _MLPFn._fp8_keep_h(ctx, x2, w1, w2, act, fp8):
+            # the all-fp8 MLP (both layers' fp8 gradients, fused backward): c_fc on the one-wave-per-SIMD
+            # fp8 GEMM writes h = x·W1ᵀ + b1 only, ONE pass makes e4m3(gelu(h)) for the MLP c_proj
+            # (ops gelu_q8, the consumer's delayed scale), and the backward re-derives gelu'(h) inside its
+            # fused e5m2 pass: gelu(h) / gelu'(h) are never written in bf16
+            from .fp8 import fp8_forward
+            h, sv1 = fp8_forward(x2, w1, b1, None, ACT_NONE, None, fp8[0], keep=True)
+            slot = fp8[1].roll_slot(0)
+            fp8[1].offer(h, ops.gelu_q8(h, slot), slot)
+            y, sv2 = fp8_forward(h, w2, b2, res2, ACT_NONE, None, fp8[1], keep=True)
+            ctx.x8 = (sv1, sv2)
+            ctx.pre_is_h = True
+            ctx.save_for_backward(x2, w1, h, h, w2)  # (pre = h; "u" only lends its shape to the backward)
+            ctx.b1, ctx.b2, ctx.act, ctx.shp, ctx.has_res = b1, b2, act, shp, residual is not None
+            return y.reshape(*shp[:-1], w2.shape[0])
         if fp8 is not None:  # (state of layer 1, state of layer 2 or None): e4m3 forward GEMMs
             from .fp8 import fp8_forward
             # layer 2's e4m3 input comes out of layer 1's epilogue (its delayed scale permitting)
@@ -377,6 +393,23 @@ class _MLPFn(torch.autograd.Function):
         return y.reshape(*shp[:-1], w2.shape[0])
 
     @staticmethod
+    def _fp8_keep_h(ctx, x2, w1, w2, act, fp8):
+        """The forward may keep h instead of gelu(h) / gelu'(h) only when the backward is certain to take
+        the fused fp8 path (which reads neither): GELU, both layers fp8 with fp8 data AND weight gradients,
+        training, and the consumer's delayed scale already seeded."""
+        from .fp8 import FP8_MLP_FUSE, fp8_dgrad_ok, fp8_wgrad_ok
+        f1, f2 = fp8
+        nig = ctx.needs_input_grad
+        if not (FP8_MLP_FUSE and f2 is not None and _MLP_FWD_ACT.get(act) == ACT_GELU_D and nig[0] and nig[1] and nig[3]):
+            return False
+        if not (f1.wgrad and f1.dgrad and f2.wgrad and f2.dgrad and f2.producer_ready(x2.device) and not f2.inference()):
+            return False
+        M, N = x2.shape[0], w1.shape[0]
+        probe = x2.new_empty((M, N))  # (shape only)
+        return (N % 8 == 0 and fp8_dgrad_ok(probe, w1.shape[1]) and fp8_dgrad_ok(x2.new_empty((M, w2.shape[0])), N)
+                and x2.shape[1] % 16 == 0 and N % 16 == 0)
+
+    @staticmethod
     def _fp8_backward(ctx, gy, gy2, x2, w1, pre, u, w2, sv1, sv2):
         """Both layers' gradients in fp8 with the GELU backward fused into the e5m2 quantisation of
         dH: dY → e5m2 once (layer 2's dgrad + wgrad), dU = dY·W2 on the fp8 dgrad GEMM, then ONE pass
@@ -386,7 +419,9 @@ class _MLPFn(torch.autograd.Function):
         Returns the gradient tuple, or None when an operand of that plan is missing."""
         from .fp8 import FP8_MLP_FUSE, fp8_dgrad, fp8_dgrad_ok
         nig = ctx.needs_input_grad
-        if not (FP8_MLP_FUSE and nig[0] and nig[1] and _MLP_BWD_ACT[ctx.act] == ACT_MUL_BWD and sv1 is not None and sv2 is not None
+        if ctx.pre_is_h:  # the forward kept h: this path is the only one that can take it (_fp8_keep_h)
+            assert sv1 is not None and sv2 is not None and sv1[0] is not None and sv2[0] is not None
+        elif not (FP8_MLP_FUSE and nig[0] and nig[1] and _MLP_BWD_ACT[ctx.act] == ACT_MUL_BWD and sv1 is not None and sv2 is not None
                 and sv1[0] is not None and sv1[2] is not None and sv2[2] is not None
                 and fp8_dgrad_ok(gy2, w2.shape[1]) and fp8_dgrad_ok(u, w1.shape[1]) and _fp8_wgrad_ok(u, sv1[0])
                 and pre.shape[1] % 8 == 0):
@@ -403,7 +438,7 @@ class _MLPFn(torch.autograd.Function):
                 b1_acc = _direct_grad(b1)
             if b1_acc is None:
                 gb1 = torch.zeros(b1.shape, device=b1.device, dtype=torch.bfloat16)
-        dyq = sv1[4].gquant_mul(du, pre, b1_acc if b1_acc is not None else gb1)
+        dyq = sv1[4].gquant_mul(du, pre, b1_acc if b1_acc is not None else gb1, from_h=ctx.pre_is_h)
         if b1_acc is not None:
             _notify(b1)
         elif gb1 is not None:

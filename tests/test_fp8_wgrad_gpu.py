@@ -207,3 +207,64 @@ def test_act_mul_bf8_vs_torch(cuda, delayed):
     assert ((deq - ref).norm() / ref.norm()).item() < 0.1
     colsum = ref.sum(0)
     assert ((bg.float() - colsum).norm() / colsum.norm()).item() < 1e-2
+
+
+def test_gelu_q8_and_act_mul_from_h(cuda):
+    """The all-fp8 MLP's split activation: e4m3(gelu(h)) with a delayed scale (rolled, amax recorded) and
+    the backward's dH = dU ⊙ gelu'(h) re-derived from h, against torch."""
+    from replicann_amd.ops.linear import ACT_GELU, _act_grad_ref
+    g = torch.Generator(device="cpu").manual_seed(14)
+    M, N = 2000, 1024
+    h = (torch.randn(M, N, generator=g) * 2).to(cuda, torch.bfloat16)
+    u = torch.nn.functional.gelu(h.float(), approximate="tanh").bfloat16().float()
+    st = torch.tensor([0.0, 3.0, 0.0, 0.0], device=cuda)  # previous amax 3
+    q = torch.ops.replicann.gelu_q8(h, st)
+    from replicann_amd.ops.fp8 import pow2_ceil
+    assert st[0].item() == pow2_ceil(torch.tensor(2 * 3.0 / 448)).item() and st[2].item() == 3.0
+    assert abs(st[1].item() - u.abs().max().item()) <= 1e-3 * u.abs().max().item()
+    deq = q.view(torch.float8_e4m3fn).float() * st[0]
+    assert ((deq - u).norm() / u.norm()).item() < 0.05
+    du = (torch.randn(M, N, generator=g) * 0.01).to(cuda, torch.bfloat16)
+    gs = torch.zeros(4, device=cuda)
+    bg = torch.zeros(N, device=cuda, dtype=torch.bfloat16)
+    q2 = torch.ops.replicann.act_mul_bf8(du, h, gs, False, bg, True)
+    ref = _act_grad_ref(du.float(), h, ACT_GELU).float()
+    deq2 = q2.view(torch.float8_e5m2).float() * gs[0]
+    assert ((deq2 - ref).norm() / ref.norm()).item() < 0.1
+    assert ((bg.float() - ref.sum(0)).norm() / ref.sum(0).norm()).item() < 1e-2
+
+
+def test_fp8_mlp_keep_h_tracks_unfused(cuda, monkeypatch):
+    """GPT-2 (tiny, fp8): the all-fp8 MLP path (h kept, gelu(h) quantised in one pass, fused GELU backward)
+    trains like the REPLICANN_FP8_MLP_FUSE=0 path (bf16 c_proj dgrad, gelu'(h) saved by the epilogue) within
+    fp8 noise, with finite gradients everywhere."""
+    import replicann_amd as R
+    import replicann_amd.ops.fp8 as F
+    from replicann_amd.utils.flat import FlatParams
+    from replicann_amd.optim import FusedAdamW
+
+    def run(fuse):
+        monkeypatch.setattr(F, "FP8_MLP_FUSE", fuse)
+        torch.manual_seed(0)
+        m = R.GPT2(R.GPT2Config.tiny(fp8=True)).to(cuda)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        for st in F.fp8_states(m):
+            st.wgrad = st.dgrad = True
+        flat = FlatParams(m)
+        opt = FusedAdamW(flat, lr=1e-3)
+        gen = torch.Generator(device=cuda).manual_seed(7)
+        losses = []
+        for _ in range(4):
+            ids = torch.randint(0, 1000, (4, 129), device=cuda, generator=gen)
+            opt.zero_grad()
+            loss = m(ids[:, :-1], ids[:, 1:])
+            loss.backward()
+            assert torch.isfinite(flat.grad.float()).all()
+            opt.step()
+            losses.append(float(loss))
+        return losses
+
+    a, b = run(True), run(False)
+    for x, y in zip(a, b):
+        assert abs(x - y) <= 0.02 * abs(y), (a, b)
