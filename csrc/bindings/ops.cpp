@@ -75,7 +75,7 @@ int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const floa
                 int, int, float, int, float, uint64_t, const uint64_t*, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
                 void*, void*, void*, float*, float*, float*, const long*, int, int, int, int, int, float, int, float,
-                uint64_t, const uint64_t*, float*, hipStream_t);
+                uint64_t, const uint64_t*, float*, void*, float*, int, hipStream_t);
 void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
 int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
@@ -769,10 +769,12 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
     TORCH_CHECK(rc == 0, "attention: unsupported shape D=", D, " Tk=", Tk);
     return {o, lse};
 }
-void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+// q8 / q8st / q8_only: see AttnArgs (attention.hip); returns false (nothing launched) when the kernels
+// cannot emit e5m2 for this shape
+bool attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                    const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
                    const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad = {},
-                   const optional<Tensor>& seed_buf = {}) {
+                   const optional<Tensor>& seed_buf = {}, void* q8 = nullptr, float* q8st = nullptr, bool q8_only = false) {
     GUARD(q);
     const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3), Tk = k.size(1);
     std::vector<long> s;
@@ -780,7 +782,7 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
     Tensor delta = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
     Tensor dk32, dv32;  // (no scratch: the generic path's dK/dV kernel writes dk / dv directly)
     int bias_b = bias && bias->defined() ? bias->size(0) : 1;
-    if (B * H * Tq == 0) return;
+    if (B * H * Tq == 0) return true;
     // packed-QKV bias gradient: per-64-row-block column partials from the kernels, then one reduction
     Tensor bsum;
     const bool want_bg = qkv_bias_grad && qkv_bias_grad->defined();
@@ -796,7 +798,8 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
                          dv.data_ptr(), delta.data_ptr<float>(), dk32.defined() ? dk32.data_ptr<float>() : nullptr,
                          dv32.defined() ? dv32.data_ptr<float>() : nullptr, s.data(), B, H, Tq, Tk, D, (float)scale,
                          causal, (float)p, (uint64_t)seed, seed_ptr(seed_buf), want_bg ? bsum.data_ptr<float>() : nullptr,
-                         cur_stream());
+                         q8, q8st, q8_only ? 1 : 0, cur_stream());
+    if (rc == -3 && q8) return false;
     TORCH_CHECK(rc == 0, "attention backward: unsupported shape D=", D);
     if (want_bg) {
         const int C = 3 * H * D;
@@ -804,6 +807,7 @@ void attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
         rn_colsum_f32(bsum.data_ptr<float>(), B * nblk, C, tmp.data_ptr<float>(), qkv_bias_grad->data_ptr(), 1,
                       cur_stream());
     }
+    return true;
 }
 std::tuple<Tensor, Tensor, Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
                                             const Tensor& o, const Tensor& lse, const optional<Tensor>& bias,
@@ -820,6 +824,20 @@ void attn_bwd_out(const Tensor& dout, const Tensor& q, const Tensor& k, const Te
                   const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad,
                   const optional<Tensor>& seed_buf) {
     attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, qkv_bias_grad, seed_buf);
+}
+// the same with the packed dQKV also (q8_only: only) written as e5m2 into q8 (uint8, dQKV's shape) with the
+// delayed-scaling slot q8_state (rolled here); false = this shape cannot (nothing launched)
+bool attn_bwd_out_q8(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                     const Tensor& lse, const optional<Tensor>& bias, double scale, bool causal, double p, int64_t seed,
+                     const Tensor& dq, const Tensor& dk, const Tensor& dv, const optional<Tensor>& qkv_bias_grad,
+                     const optional<Tensor>& seed_buf, const Tensor& q8, const Tensor& q8_state, bool q8_only) {
+    TORCH_CHECK(q8.scalar_type() == at::kByte && q8.is_cuda() && q8.device() == q.device(), "attn q8: uint8 on the device");
+    TORCH_CHECK(q8_state.scalar_type() == at::kFloat && q8_state.numel() >= 4 && q8_state.device() == q.device());
+    // the e5m2 image uses element offsets from dq: q8 is the byte twin of the packed dQKV dq / dk / dv view
+    TORCH_CHECK(q8.numel() == 3 * dq.numel() && dq.data_ptr() < dk.data_ptr() && dk.data_ptr() < dv.data_ptr(),
+                "attn q8: the e5m2 twin of a packed (B, T, 3, H, D) dQKV");
+    return attn_bwd_impl(dout, q, k, v, o, lse, bias, scale, causal, p, seed, dq, dk, dv, qkv_bias_grad, seed_buf,
+                         q8.data_ptr(), q8_state.data_ptr<float>(), q8_only);
 }
 
 // ------------------------------------------------------------------ implicit-GEMM conv
@@ -1238,6 +1256,9 @@ TORCH_LIBRARY(replicann, m) {
     m.def("attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
           "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, "
           "Tensor(d!)? qkv_bias_grad=None, Tensor? seed_buf=None) -> ()");
+    m.def("attn_bwd_out_q8(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor? bias, float scale, "
+          "bool causal, float p, int seed, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, "
+          "Tensor(d!)? qkv_bias_grad, Tensor? seed_buf, Tensor(e!) q8, Tensor(f!) q8_state, bool q8_only) -> bool");
     m.def("im2col(Tensor x, int KH, int KW, int S, int P, int Kp) -> Tensor");
     m.def("conv_fwd_implicit(Tensor x, Tensor w, Tensor? bias, int S, int P) -> Tensor");
     m.def("conv_fwd_implicit_stats(Tensor x, Tensor w, Tensor? bias, int S, int P) -> (Tensor, Tensor)");
@@ -1307,6 +1328,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("attn_fwd", &attn_fwd);
     m.impl("attn_bwd", &attn_bwd);
     m.impl("attn_bwd_out", &attn_bwd_out);
+    m.impl("attn_bwd_out_q8", &attn_bwd_out_q8);
     m.impl("im2col", &im2col);
     m.impl("conv_fwd_implicit", &conv_fwd_implicit);
     m.impl("conv_fwd_implicit_stats", &conv_fwd_implicit_stats);

@@ -59,7 +59,30 @@ struct AttnArgs {
     // lse units: the D = 64 forward kernels store log2(Σ exp) in base-2 units (the backward then
     // needs one FMA per score, exp2(s·scale·log2e − lse2)); the generic forward stores natural log.
     int lse_log2;
+    // optional (D = 64 fast path): dQ | dK | dV also — or, q8_only, only — as OCP e5m2 at q8 (same element
+    // offsets as dq / dk / dv: the packed dQKV's byte image) with the fp8 consumer's delayed scale q8st[0]
+    // (rolled before the launch); amax(|dQKV|) recorded into q8st[1].  The c_attn projection's fp8 data /
+    // weight gradients then need no quantisation pass over dQKV.
+    uint8_t* q8;   // dQ's e5m2 base (dK / dV: q8k / q8v, the same element offsets as dk / dv)
+    uint8_t* q8k;
+    uint8_t* q8v;
+    float* q8st;
+    int q8_only;
 };
+
+// 4 values of a gradient row as e5m2 (one 4-B store) with the delayed scale, their amax folded into m
+RN_DEV void attn_q8_store4(uint8_t* dst, float a, float b, float c, float d, float inv, float& m) {
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d))));
+    const float lim = 57344.f;
+    int w = 0;
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(fminf(fmaxf(a * inv, -lim), lim), fminf(fmaxf(b * inv, -lim), lim), w, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(fminf(fmaxf(c * inv, -lim), lim), fminf(fmaxf(d * inv, -lim), lim), w, true);
+    *reinterpret_cast<int*>(dst) = w;
+}
+RN_DEV void attn_q8_amax(const AttnArgs& p, float m) {
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int*>(p.q8st + 1), __float_as_int(m));
+}
 
 // (bh, block) of this workgroup; `reverse`: the head's heaviest (last) causal block first
 RN_DEV void blk_map(const AttnArgs& p, int nblk, bool reverse, int& bh, int& blk) {
@@ -936,22 +959,36 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
             }
         }
     }
+    float q8m = 0.f;
+    const float q8inv = p.q8 ? 1.f / p.q8st[0] : 0.f;
 #pragma unroll
     for (int u = 0; u < KG; ++u) {
         if (kvl[u] < p.Tk) {
-            bf16* dkp = p.dk + b * p.dk_sb + (long)kvl[u] * p.dk_st + h * p.dk_sh;
-            bf16* dvp = p.dv + b * p.dv_sb + (long)kvl[u] * p.dv_st + h * p.dv_sh;
+            const long ko = b * p.dk_sb + (long)kvl[u] * p.dk_st + h * p.dk_sh;
+            const long vo = b * p.dv_sb + (long)kvl[u] * p.dv_st + h * p.dv_sh;
+            bf16* dkp = p.dk + ko;
+            bf16* dvp = p.dv + vo;
 #pragma unroll
             for (int jd = 0; jd < NJ; ++jd) {
-                bf16x4 k4 = {(bf16)(dkacc[u][jd][0] * p.scale), (bf16)(dkacc[u][jd][1] * p.scale),
-                             (bf16)(dkacc[u][jd][2] * p.scale), (bf16)(dkacc[u][jd][3] * p.scale)};
-                bf16x4 v4 = {(bf16)dvacc[u][jd][0], (bf16)dvacc[u][jd][1], (bf16)dvacc[u][jd][2],
-                             (bf16)dvacc[u][jd][3]};
-                *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
-                *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
+                const float k0 = dkacc[u][jd][0] * p.scale, k1 = dkacc[u][jd][1] * p.scale,
+                            k2 = dkacc[u][jd][2] * p.scale, k3 = dkacc[u][jd][3] * p.scale;
+                if (p.q8) {  // (the e5m2 of the bf16-rounded values a separate pass would quantise)
+                    attn_q8_store4(p.q8k + ko + jd * 16 + 4 * g, (float)(bf16)k0, (float)(bf16)k1, (float)(bf16)k2,
+                                   (float)(bf16)k3, q8inv, q8m);
+                    attn_q8_store4(p.q8v + vo + jd * 16 + 4 * g, (float)(bf16)dvacc[u][jd][0], (float)(bf16)dvacc[u][jd][1],
+                                   (float)(bf16)dvacc[u][jd][2], (float)(bf16)dvacc[u][jd][3], q8inv, q8m);
+                }
+                if (!p.q8_only) {
+                    bf16x4 k4 = {(bf16)k0, (bf16)k1, (bf16)k2, (bf16)k3};
+                    bf16x4 v4 = {(bf16)dvacc[u][jd][0], (bf16)dvacc[u][jd][1], (bf16)dvacc[u][jd][2],
+                                 (bf16)dvacc[u][jd][3]};
+                    *reinterpret_cast<bf16x4*>(dkp + jd * 16 + 4 * g) = k4;
+                    *reinterpret_cast<bf16x4*>(dvp + jd * 16 + 4 * g) = v4;
+                }
             }
         }
     }
+    if (p.q8) attn_q8_amax(p, q8m);
 }
 
 // dQ: grid (B*H, ceil(Tq/(64·QG))); query group qg (< QG) of wave w owns queries
@@ -1157,18 +1194,25 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             }
         }
     }
+    float q8m = 0.f;
+    const float q8inv = p.q8 ? 1.f / p.q8st[0] : 0.f;
 #pragma unroll
     for (int u = 0; u < QG; ++u) {
         if (qok[u]) {
-            bf16* dqp = p.dq + b * p.dq_sb + (long)qgl[u] * p.dq_st + h * p.dq_sh;
+            const long qo = b * p.dq_sb + (long)qgl[u] * p.dq_st + h * p.dq_sh;
+            bf16* dqp = p.dq + qo;
 #pragma unroll
             for (int jd = 0; jd < NJ; ++jd) {
                 bf16x4 q4 = {(bf16)(dqacc[u][jd][0] * p.scale), (bf16)(dqacc[u][jd][1] * p.scale),
                              (bf16)(dqacc[u][jd][2] * p.scale), (bf16)(dqacc[u][jd][3] * p.scale)};
-                *reinterpret_cast<bf16x4*>(dqp + jd * 16 + 4 * g) = q4;
+                if (p.q8)
+                    attn_q8_store4(p.q8 + qo + jd * 16 + 4 * g, (float)q4[0], (float)q4[1], (float)q4[2], (float)q4[3],
+                                   q8inv, q8m);
+                if (!p.q8_only) *reinterpret_cast<bf16x4*>(dqp + jd * 16 + 4 * g) = q4;
             }
         }
     }
+    if (p.q8) attn_q8_amax(p, q8m);
 }
 
 // ============================== generic path (any D <= 256) ==============================
@@ -1423,11 +1467,19 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
 
 // strides: q,k,v,o,do,dq,dk,dv (each b,t,h).  delta: B*H*Tq floats workspace.
 // dk32/dv32: generic path scratch (B*Tk*H*D floats each, zeroed by caller) or null.
+void rn_fp8_roll_bf8(float* state, hipStream_t st);  // fp8.hip
+
 int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                 const float* bias, int bias_b, void* dq, void* dk, void* dv, float* delta, float* dk32, float* dv32,
                 const long* s, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
-                uint64_t seed, const uint64_t* seed_ptr, float* bsum, hipStream_t st) {
+                uint64_t seed, const uint64_t* seed_ptr, float* bsum, void* q8, float* q8st, int q8_only, hipStream_t st) {
     AttnArgs a = {};
+    // q8: the e5m2 twin of the buffer dq / dk / dv live in (same element offsets from dq)
+    a.q8 = (uint8_t*)q8; a.q8st = q8st; a.q8_only = q8_only;
+    if (q8) {
+        a.q8k = (uint8_t*)q8 + ((const bf16*)dk - (const bf16*)dq);
+        a.q8v = (uint8_t*)q8 + ((const bf16*)dv - (const bf16*)dq);
+    }
     a.seed_ptr = seed_ptr;
     a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = (float*)lse;
     a.bias = bias; a.dout = (const bf16*)dout; a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.delta = delta;
@@ -1444,6 +1496,8 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     // the forward chose its path with its own stride test: lse is base 2 iff that one was fast
     a.lse_log2 = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast && !a.lse_log2) return -1;  // cannot happen (the backward test is stricter); never mix units
+    if (q8 && !(fast && D == 64)) return -3;  // e5m2 dQKV: the D = 64 kernels only (the caller quantises instead)
+    if (q8) rn_fp8_roll_bf8(q8st, st);        // the consumer's delayed e5m2 scale, before both kernels
     if (fast && D != 64) {
         if (D == 32) attn_bwd_mfma<32>(a, st);
         else attn_bwd_mfma<128>(a, st);

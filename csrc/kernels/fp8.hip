@@ -127,9 +127,7 @@ __global__ void __launch_bounds__(256) quant_delayed_bf8_k(const bf16* __restric
     __shared__ float sm[16];
     const float inv = 1.f / state[0];
     float m = 0.f;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
-        float f[8];
-        load8(x + i * 8, f);
+    auto one = [&](long i, float* f) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             m = fmaxf(m, fabsf(f[j]));
@@ -141,6 +139,21 @@ __global__ void __launch_bounds__(256) quant_delayed_bf8_k(const bf16* __restric
         w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], w1, false);
         w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], w1, true);
         *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    };
+    // 4 chunks in flight per thread (one at a time left a grid-capped launch latency-bound)
+    const long S = (long)gridDim.x * 256, n8 = n / 8;
+    long i = blockIdx.x * 256L + threadIdx.x;
+    for (; i + 3 * S < n8; i += 4 * S) {
+        float f[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load8(x + (i + u * S) * 8, f[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) one(i + u * S, f[u]);
+    }
+    for (; i < n8; i += S) {
+        float f[8];
+        load8(x + i * 8, f);
+        one(i, f);
     }
     for (long i = (n / 8) * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
         const float v = bf2f(x[i]);
@@ -384,6 +397,8 @@ void rn_bf8_quantize(const void* x, long n, void* q, float* state, int delayed, 
     amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
     quant_bf8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
+void rn_fp8_roll_bf8(float* state, hipStream_t st) { fp8_roll_bf8_k<<<1, 1, 0, st>>>(state); }
+
 // dH = dU ⊙ d in e5m2 (+ column partials [G][N] of dH when colpart): see act_mul_bf8_k.  N % 8 == 0.
 int rn_act_mul_bf8_groups(long M, int N) {
     const long nc = N / 8;
@@ -425,9 +440,7 @@ __global__ void __launch_bounds__(256) gelu_q8_k(const bf16* __restrict__ h, lon
     __shared__ float sm[16];
     const float inv = 1.f / state[0];
     float m = 0.f;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
-        float f[8];
-        load8(h + i * 8, f);
+    auto one = [&](long i, float* f) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const float u = (float)(bf16)gelu_f(f[j]);
@@ -440,6 +453,20 @@ __global__ void __launch_bounds__(256) gelu_q8_k(const bf16* __restrict__ h, lon
         w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
         w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
         *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
+    };
+    const long S = (long)gridDim.x * 256, n8 = n / 8;
+    long i = blockIdx.x * 256L + threadIdx.x;
+    for (; i + 3 * S < n8; i += 4 * S) {  // 4 chunks in flight per thread
+        float f[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load8(h + (i + u * S) * 8, f[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) one(i + u * S, f[u]);
+    }
+    for (; i < n8; i += S) {
+        float f[8];
+        load8(h + i * 8, f);
+        one(i, f);
     }
     m = block_max(m, sm);
     if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));

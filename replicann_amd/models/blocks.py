@@ -114,7 +114,8 @@ class Attention(nn.Module):
             return self.c_proj(a, residual=residual)
         a = ops.attention_packed(qkv, causal=self.causal, dropout_p=self.attn_dropout,
                                  training=self.training,
-                                 producer_bias=self.c_attn.bias)
+                                 producer_bias=self.c_attn.bias,
+                                 consumer8=self.c_attn.fp8_state if torch.is_grad_enabled() else None)
         a = a.reshape(B, T, E)
         if self.resid_dropout > 0 and self.training:
             return residual + ops.dropout(self.c_proj(a), self.resid_dropout, True)

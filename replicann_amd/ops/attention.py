@@ -22,6 +22,8 @@ Supported semantics (all needed for reference parity, SURVEY.md §2.1 Q1–Q4):
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _ext
@@ -121,16 +123,23 @@ def attention(q, k, v, *, scale=None, causal=False, bias=None, mask=None, dropou
     return attention_reference(q, k, v, scale, causal, bias, p, training)
 
 
+# the attention backward's e5m2 dQKV for an fp8 QKV projection (REPLICANN_FP8_ATTN_Q8=0: off, A/B)
+ATTN_Q8 = os.environ.get("REPLICANN_FP8_ATTN_Q8", "1") == "1"
+
+
 class _AttnPackedFn(torch.autograd.Function):
     """Attention on a packed (B, T, 3, H, D) QKV tensor; backward writes one packed dQKV."""
 
     @staticmethod
-    def forward(ctx, qkv, bias, scale, causal, dropout_p, seed, producer_bias):
+    def forward(ctx, qkv, bias, scale, causal, dropout_p, seed, producer_bias, consumer8=None):
         q, k, v = qkv.unbind(2)
         o, lse = _ext.ops().attn_fwd(q, k, v, bias, scale, causal, dropout_p, 0, seed)
         ctx.save_for_backward(qkv, o, lse, bias)
         ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed = scale, causal, dropout_p, seed
         ctx.producer_bias = producer_bias
+        # the fp8 projection that produced qkv (its backward consumes dQKV): the plan its forward recorded
+        ctx.consumer8 = consumer8
+        ctx.plan8 = tuple(consumer8.bwd_plan) if consumer8 is not None else (False, False)
         return o
 
     @staticmethod
@@ -145,22 +154,37 @@ class _AttnPackedFn(torch.autograd.Function):
         pb = ctx.producer_bias
         B, T, _, H, D = qkv.shape
         pb_acc = _direct_grad(pb) if (pb is not None and attention_is_mfma(D) and pb.numel() == 3 * H * D) else None
-        _ext.ops().attn_bwd_out(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
-                                ctx.dropout_p, 0, dq, dk, dv, pb_acc, ctx.seed)
+        c8 = ctx.consumer8
+        done = False
+        if ATTN_Q8 and c8 is not None and c8.g_ready and (pb_acc is not None or pb is None) and any(ctx.plan8):
+            # dQKV also in e5m2 from the kernels (the consumer's delayed scale): the projection's fp8
+            # gradients skip their quantisation pass; when it takes BOTH in fp8 (and its bias gradient came
+            # from these kernels) the bf16 dQKV is never read, so it is not written at all
+            q8 = torch.empty(qkv.shape, device=qkv.device, dtype=torch.uint8)
+            q8_only = all(ctx.plan8)
+            done = _ext.ops().attn_bwd_out_q8(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
+                                              ctx.dropout_p, 0, dq, dk, dv, pb_acc, ctx.seed, q8,
+                                              c8.gslot(qkv.device), q8_only)
+            if done:
+                c8.goffer(dqkv, q8)
+        if not done:
+            _ext.ops().attn_bwd_out(do.contiguous(), q, k, v, o, lse, bias, ctx.scale, ctx.causal,
+                                    ctx.dropout_p, 0, dq, dk, dv, pb_acc, ctx.seed)
         if pb_acc is not None:  # Σ_rows dQKV reduced in the kernels: the c_attn bias gradient
             pb._rn_bias_done = True
             _notify(pb)
-        return dqkv, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None
 
 
 def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dropout_p=0.0,
-                     training=False, producer_bias=None):
+                     training=False, producer_bias=None, consumer8=None):
     """Attention over a packed (B, T, 3, H, D) tensor → (B, T, H, D).
 
     ``producer_bias``: bias of the projection that produced ``qkv`` (3·H·D); its gradient
     Σ_rows dQKV is then reduced by the attention backward kernels (per-block column
     partials) and accumulated into the flat gradient, and the projection skips its own
-    bias pass."""
+    bias pass.  ``consumer8``: the Fp8State of that projection when it runs in fp8 — the backward kernels
+    then also emit dQKV in e5m2 for its fp8 gradients (see _AttnPackedFn.backward)."""
     B, T, three, H, D = qkv.shape
     if scale is None:
         scale = D ** -0.5
@@ -171,7 +195,7 @@ def attention_packed(qkv, *, scale=None, causal=False, bias=None, mask=None, dro
         b3 = _bias_3d(bias, B, T, T)
         from .rng import next_seed
         seed = next_seed(qkv.device) if p > 0 else None
-        return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed, producer_bias)
+        return _AttnPackedFn.apply(qkv, b3, float(scale), bool(causal), float(p), seed, producer_bias, consumer8)
     q, k, v = qkv.unbind(2)
     return attention_reference(q, k, v, scale, causal, bias, p, training)
 

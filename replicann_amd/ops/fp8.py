@@ -166,6 +166,10 @@ class Fp8State:
         self.fed = 0  # activations taken from a producer kernel instead of a quantisation pass
         self.wcache = None  # Fp8WeightCache holding this GEMM's e4m3 weight (refreshed by the optimizer)
         self._ti = None  # inference scratch slots (see roll_slot)
+        self._goffer = None  # (dY tensor, its e5m2 copy) written by the producing backward kernel (attention)
+        # set by the fp8 linear's forward: (fp8 weight gradient, fp8 data gradient) its backward will take —
+        # the producer of its dY may then skip the bf16 dY altogether
+        self.bwd_plan = (False, False)
         self.grad_mode = True  # grad mode at the op's entry (autograd Functions run forward under no_grad)
 
     @property
@@ -200,8 +204,26 @@ class Fp8State:
         g = self.gt
         self.g_ready = bool(g is not None and float(g[0, 0]) > 0)
 
+    def gslot(self, device):
+        """The gradient slot (allocating it on first use) — for a producer kernel that emits dY in e5m2."""
+        if self.gt is None or self.gt.device != device:
+            self.gt = torch.zeros(1, 4, device=device, dtype=torch.float32)
+            self.g_ready = False
+        return self.gt[0]
+
+    def goffer(self, dy, q):
+        """A producer wrote ``dy``'s e5m2 copy ``q`` with the gradient slot (rolled, amax recorded): the
+        next gquant of the same tensor returns it."""
+        self._goffer = (dy, q)
+
     def gquant(self, dy):
         """dY in e5m2 with the gradient slot: current scaling on the first call, delayed after."""
+        if self._goffer is not None:
+            src, q = self._goffer
+            self._goffer = None
+            if src.data_ptr() == dy.data_ptr() and src.numel() == dy.numel():
+                self.g_ready = True
+                return q.view(dy.shape), self.gt[0]
         if self.gt is None or self.gt.device != dy.device:
             self.gt = torch.zeros(1, 4, device=dy.device, dtype=torch.float32)
             self.g_ready = False

@@ -174,6 +174,11 @@ class _LinearFn(torch.autograd.Function):
             if fp8.fp8_bwd and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
                 # keep the e4m3 operands for the fp8 weight / data gradients
                 y, ctx.x8 = fp8_forward(x2, weight, bias, res2, act, preact, fp8, keep=True)
+                from .fp8 import fp8_dgrad_ok, fp8_wgrad_ok
+                dy_meta = torch.empty((x2.shape[0], weight.shape[0]), device="meta")
+                # which gradients the backward will take in fp8 (then nothing reads dY in bf16 there)
+                fp8.bwd_plan = (not ctx.needs_input_grad[1] or (ctx.x8[0] is not None and fp8_wgrad_ok(dy_meta, ctx.x8[0])),
+                                not ctx.needs_input_grad[0] or (ctx.x8[2] is not None and fp8_dgrad_ok(dy_meta, weight.shape[1])))
             else:
                 y = fp8_forward(x2, weight, bias, res2, act, preact, fp8)
         elif native:
