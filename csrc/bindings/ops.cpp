@@ -75,7 +75,8 @@ int rn_attn_fwd(const void*, const void*, const void*, void*, float*, const floa
                 int, int, float, int, float, uint64_t, const uint64_t*, hipStream_t);
 int rn_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const float*, int,
                 void*, void*, void*, float*, float*, float*, const long*, int, int, int, int, int, float, int, float,
-                uint64_t, const uint64_t*, float*, void*, float*, int, hipStream_t);
+                uint64_t, const uint64_t*, float*, void*, float*, int, float*, hipStream_t);
+long rn_attn_q8_part_floats(int, int, int, int);
 void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
 int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
@@ -793,12 +794,13 @@ bool attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const T
                     Tq == Tk, "qkv bias gradient: packed self-attention with head_dim 32, 64 or 128 only");
         bsum = at::empty({(int64_t)B * nblk, 3L * H * D}, q.options().dtype(at::kFloat));
     }
+    Tensor q8part = q8 ? at::empty({rn_attn_q8_part_floats(B, H, Tq, Tk)}, q.options().dtype(at::kFloat)) : Tensor();
     int rc = rn_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                          bias && bias->defined() ? bias->data_ptr<float>() : nullptr, bias_b, dq.data_ptr(), dk.data_ptr(),
                          dv.data_ptr(), delta.data_ptr<float>(), dk32.defined() ? dk32.data_ptr<float>() : nullptr,
                          dv32.defined() ? dv32.data_ptr<float>() : nullptr, s.data(), B, H, Tq, Tk, D, (float)scale,
                          causal, (float)p, (uint64_t)seed, seed_ptr(seed_buf), want_bg ? bsum.data_ptr<float>() : nullptr,
-                         q8, q8st, q8_only ? 1 : 0, cur_stream());
+                         q8, q8st, q8_only ? 1 : 0, q8 ? q8part.data_ptr<float>() : nullptr, cur_stream());
     if (rc == -3 && q8) return false;
     TORCH_CHECK(rc == 0, "attention backward: unsupported shape D=", D);
     if (want_bg) {

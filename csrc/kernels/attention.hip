@@ -68,6 +68,10 @@ struct AttnArgs {
     uint8_t* q8v;
     float* q8st;
     int q8_only;
+    // per-wave amax partials (no same-address atomics: one per wave serialised 32 k atomics per launch
+    // and tripled the kernels' time): dQ kernel at q8part[4·block + wave], dK/dV kernel at q8part2[...]
+    float* q8part;
+    float* q8part2;
 };
 
 // 4 values of a gradient row as e5m2 (one 4-B store) with the delayed scale, their amax folded into m
@@ -79,9 +83,19 @@ RN_DEV void attn_q8_store4(uint8_t* dst, float a, float b, float c, float d, flo
     w = __builtin_amdgcn_cvt_pk_bf8_f32(fminf(fmaxf(c * inv, -lim), lim), fminf(fmaxf(d * inv, -lim), lim), w, true);
     *reinterpret_cast<int*>(dst) = w;
 }
-RN_DEV void attn_q8_amax(const AttnArgs& p, float m) {
+RN_DEV void attn_q8_amax(float* part, float m) {
     m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int*>(p.q8st + 1), __float_as_int(m));
+    if ((threadIdx.x & 63) == 0) part[blockIdx.x * 4 + (threadIdx.x >> 6)] = m;
+}
+// the partials of both kernels -> the slot's amax (state[1], zeroed by the roll)
+__global__ void __launch_bounds__(256) attn_amax_reduce_k(const float* __restrict__ part, int n, float* __restrict__ st) {
+    __shared__ float red[4];
+    float m = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, part[i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) st[1] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
 // (bh, block) of this workgroup; `reverse`: the head's heaviest (last) causal block first
@@ -988,7 +1002,7 @@ __global__ void __launch_bounds__(256, ((DROP || BIAS) && OCC > 2) ? 2 : OCC) at
             }
         }
     }
-    if (p.q8) attn_q8_amax(p, q8m);
+    if (p.q8) attn_q8_amax(p.q8part2, q8m);
 }
 
 // dQ: grid (B*H, ceil(Tq/(64·QG))); query group qg (< QG) of wave w owns queries
@@ -1212,7 +1226,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
             }
         }
     }
-    if (p.q8) attn_q8_amax(p, q8m);
+    if (p.q8) attn_q8_amax(p.q8part, q8m);
 }
 
 // ============================== generic path (any D <= 256) ==============================
@@ -1468,17 +1482,22 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
 // strides: q,k,v,o,do,dq,dk,dv (each b,t,h).  delta: B*H*Tq floats workspace.
 // dk32/dv32: generic path scratch (B*Tk*H*D floats each, zeroed by caller) or null.
 void rn_fp8_roll_bf8(float* state, hipStream_t st);  // fp8.hip
+long rn_attn_q8_part_floats(int B, int H, int Tq, int Tk);
 
 int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                 const float* bias, int bias_b, void* dq, void* dk, void* dv, float* delta, float* dk32, float* dv32,
                 const long* s, int B, int H, int Tq, int Tk, int D, float scale, int causal, float p_drop,
-                uint64_t seed, const uint64_t* seed_ptr, float* bsum, void* q8, float* q8st, int q8_only, hipStream_t st) {
+                uint64_t seed, const uint64_t* seed_ptr, float* bsum, void* q8, float* q8st, int q8_only, float* q8part,
+                hipStream_t st) {
     AttnArgs a = {};
     // q8: the e5m2 twin of the buffer dq / dk / dv live in (same element offsets from dq)
     a.q8 = (uint8_t*)q8; a.q8st = q8st; a.q8_only = q8_only;
     if (q8) {
         a.q8k = (uint8_t*)q8 + ((const bf16*)dk - (const bf16*)dq);
         a.q8v = (uint8_t*)q8 + ((const bf16*)dv - (const bf16*)dq);
+        // q8part: >= 8·B·H·ceil(T/64) floats (rn_attn_q8_part_floats): both kernels' per-wave partials
+        a.q8part = q8part;
+        a.q8part2 = q8part + 4L * B * H * ((Tq + 63) / 64);
     }
     a.seed_ptr = seed_ptr;
     a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (bf16*)o; a.lse = (float*)lse;
@@ -1497,7 +1516,10 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
     a.lse_log2 = mfma_head(D) && (a.q_st % 8 == 0) && (a.k_st % 8 == 0) && (a.v_st % 8 == 0) && (a.o_st % 4 == 0);
     if (fast && !a.lse_log2) return -1;  // cannot happen (the backward test is stricter); never mix units
     if (q8 && !(fast && D == 64)) return -3;  // e5m2 dQKV: the D = 64 kernels only (the caller quantises instead)
-    if (q8) rn_fp8_roll_bf8(q8st, st);        // the consumer's delayed e5m2 scale, before both kernels
+    if (q8) {
+        rn_fp8_roll_bf8(q8st, st);  // the consumer's delayed e5m2 scale, before both kernels
+        (void)hipMemsetAsync(q8part, 0, (size_t)rn_attn_q8_part_floats(B, H, Tq, Tk) * sizeof(float), st);
+    }
     if (fast && D != 64) {
         if (D == 32) attn_bwd_mfma<32>(a, st);
         else attn_bwd_mfma<128>(a, st);
@@ -1522,6 +1544,10 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         } else {
             RN_DISPATCH3(attn_bwd_dkdv64_k, g1, 36864, st, a);
         }
+        if (q8) {  // (the buffer was zeroed before the launches: a wave that never reaches its store leaves 0)
+            const int nk = (!bias && p_drop == 0.f) ? B * H * ((Tk + 127) / 128) : B * H * ((Tk + 63) / 64);
+            attn_amax_reduce_k<<<1, 256, 0, st>>>(a.q8part, (int)(a.q8part2 - a.q8part) + 4 * nk, q8st);
+        }
     } else {
         if (D > 256 || Tk > 12000 || Tq > 12000) return -1;
         // dQ + delta per query row, then dK/dV per key row: no atomics, bitwise repeatable
@@ -1541,5 +1567,8 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
 }
 
 int rn_attn_is_fast(int D) { return mfma_head(D); }
+long rn_attn_q8_part_floats(int B, int H, int Tq, int Tk) {
+    return 4L * B * H * ((Tq + 63) / 64) + 4L * B * H * ((Tk + 63) / 64);
+}
 
 }  // extern "C"
