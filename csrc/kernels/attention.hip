@@ -29,6 +29,7 @@
 // and fp32 atomics for dK/dV (not bitwise deterministic).
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -87,15 +88,17 @@ RN_DEV void attn_q8_amax(float* part, float m) {
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) part[blockIdx.x * 4 + (threadIdx.x >> 6)] = m;
 }
-// the partials of both kernels -> the slot's amax (state[1], zeroed by the roll)
+// the partials of both kernels -> the slot's amax (state[1], zeroed by the roll): a grid-strided max, one
+// atomic per block (a single block took 86 us for the 262 k partials of a GPT-2-medium step)
 __global__ void __launch_bounds__(256) attn_amax_reduce_k(const float* __restrict__ part, int n, float* __restrict__ st) {
     __shared__ float red[4];
     float m = 0.f;
-    for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, part[i]);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) m = fmaxf(m, part[i]);
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) st[1] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (threadIdx.x == 0)
+        atomicMax(reinterpret_cast<int*>(st + 1), __float_as_int(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 // (bh, block) of this workgroup; `reverse`: the head's heaviest (last) causal block first
@@ -1546,7 +1549,8 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         }
         if (q8) {  // (the buffer was zeroed before the launches: a wave that never reaches its store leaves 0)
             const int nk = (!bias && p_drop == 0.f) ? B * H * ((Tk + 127) / 128) : B * H * ((Tk + 63) / 64);
-            attn_amax_reduce_k<<<1, 256, 0, st>>>(a.q8part, (int)(a.q8part2 - a.q8part) + 4 * nk, q8st);
+            const int n = (int)(a.q8part2 - a.q8part) + 4 * nk;
+            attn_amax_reduce_k<<<std::min(256, (n + 4095) / 4096), 256, 0, st>>>(a.q8part, n, q8st);
         }
     } else {
         if (D > 256 || Tk > 12000 || Tq > 12000) return -1;

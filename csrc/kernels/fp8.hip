@@ -8,6 +8,7 @@
 // * the GEMM runs on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales:
 //   2x the bf16 MFMA rate per clock (MI355X_MICROARCH.md §Matrix cores), with the
 //   product of the two tensor scales applied as the epilogue alpha.
+#include <algorithm>
 #include <cstdlib>
 
 #include "gemm_impl.h"
@@ -454,16 +455,8 @@ __global__ void __launch_bounds__(256) gelu_q8_k(const bf16* __restrict__ h, lon
         w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
         *reinterpret_cast<int2*>(q + i * 8) = make_int2(w0, w1);
     };
-    const long S = (long)gridDim.x * 256, n8 = n / 8;
-    long i = blockIdx.x * 256L + threadIdx.x;
-    for (; i + 3 * S < n8; i += 4 * S) {  // 4 chunks in flight per thread
-        float f[4][8];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) load8(h + (i + u * S) * 8, f[u]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) one(i + u * S, f[u]);
-    }
-    for (; i < n8; i += S) {
+    // one chunk per iteration over a large grid (the 4-chunk unroll measured slower here: 225 vs 179 us)
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 8; i += (long)gridDim.x * 256) {
         float f[8];
         load8(h + i * 8, f);
         one(i, f);
@@ -473,7 +466,8 @@ __global__ void __launch_bounds__(256) gelu_q8_k(const bf16* __restrict__ h, lon
 }
 void rn_gelu_q8(const void* h, long n, void* q, float* state, hipStream_t st) {
     fp8_roll_k<<<1, 1, 0, st>>>(state);
-    gelu_q8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)h, n, (uint8_t*)q, state);
+    const long blocks = (n / 8 + 255) / 256;
+    gelu_q8_k<<<(int)std::min<long>(std::max<long>(blocks, 1), 8192), 256, 0, st>>>((const bf16*)h, n, (uint8_t*)q, state);
 }
 
 void rn_bf8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
