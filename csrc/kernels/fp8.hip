@@ -74,13 +74,28 @@ __global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long 
 // Delayed scaling (one pass over x): the scale comes from the amax recorded by the PREVIOUS
 // quantisation of this tensor (x2 headroom), and this pass records the current amax for the
 // next one.  state: [0] scale used, [1] amax of the last pass, [2] amax the scale came from.
-__device__ inline void fp8_roll_k_body(float* __restrict__ state) {
+// delayed-scaling headroom: scale = pow2_ceil(hr · previous amax / max); REPLICANN_FP8_HEADROOM (e4m3
+// activations / weights) and REPLICANN_FP8_GHEADROOM (e5m2 gradients), default 2 (A/B)
+static float fp8_env_hr(const char* name) {
+    const char* e = std::getenv(name);
+    const float v = e ? (float)std::atof(e) : 2.f;
+    return v > 0.f ? v : 2.f;
+}
+static float fp8_hr() {
+    static const float v = fp8_env_hr("REPLICANN_FP8_HEADROOM");
+    return v;
+}
+static float fp8_ghr() {
+    static const float v = fp8_env_hr("REPLICANN_FP8_GHEADROOM");
+    return v;
+}
+__device__ inline void fp8_roll_k_body(float* __restrict__ state, float hr) {
     const float a = state[1];
     state[2] = a;
-    state[0] = a > 0.f ? pow2_ceil(2.f * a / E4M3_MAX) : 1.f;
+    state[0] = a > 0.f ? pow2_ceil(hr * a / E4M3_MAX) : 1.f;
     state[1] = 0.f;
 }
-__global__ void fp8_roll_k(float* __restrict__ state) { fp8_roll_k_body(state); }
+__global__ void fp8_roll_k(float* __restrict__ state, float hr) { fp8_roll_k_body(state, hr); }
 
 __global__ void __launch_bounds__(256) quant_delayed_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
                                                        float* __restrict__ state) {
@@ -117,10 +132,10 @@ __global__ void __launch_bounds__(256) quant_delayed_k(const bf16* __restrict__ 
 // x2 headroom, this pass records the new amax).  state as quant_delayed_k; the roll is folded in
 // (block 0 rolls nothing: the host launches fp8_roll_fmt_k first).
 constexpr float E5M2_MAX = 57344.f;
-__global__ void fp8_roll_bf8_k(float* __restrict__ state) {
+__global__ void fp8_roll_bf8_k(float* __restrict__ state, float hr) {
     const float a = state[1];
     state[2] = a;
-    state[0] = a > 0.f ? pow2_ceil(2.f * a / E5M2_MAX) : 1.f;
+    state[0] = a > 0.f ? pow2_ceil(hr * a / E5M2_MAX) : 1.f;
     state[1] = 0.f;
 }
 __global__ void __launch_bounds__(256) quant_delayed_bf8_k(const bf16* __restrict__ x, long n, uint8_t* __restrict__ q,
@@ -283,9 +298,9 @@ __global__ void dequant_k(const uint8_t* __restrict__ q, long n, const float* __
 // right after the optimizer step, in two launches for the whole model.  segs: int64 [nseg][4] =
 // (element offset in the flat bf16 parameter buffer, numel, byte offset in the e4m3 buffer,
 // address of the weight's Fp8State slot).  Delayed scaling as fp8_roll_k / quant_delayed_k.
-__global__ void fp8_roll_many_k(const long* __restrict__ segs, int nseg) {
+__global__ void fp8_roll_many_k(const long* __restrict__ segs, int nseg, float hr) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nseg) fp8_roll_k_body(reinterpret_cast<float*>(segs[i * 4 + 3]));
+    if (i < nseg) fp8_roll_k_body(reinterpret_cast<float*>(segs[i * 4 + 3]), hr);
 }
 
 __global__ void __launch_bounds__(256) fp8_quant_many_k(const bf16* __restrict__ flat, const long* __restrict__ segs,
@@ -363,7 +378,7 @@ void rn_fp8_quantize(const void* x, long n, void* q, float* state, hipStream_t s
 
 // One-pass delayed-scaling quantisation (state as fp8_roll_k / quant_delayed_k); graph-capturable.
 void rn_fp8_quantize_delayed(const void* x, long n, void* q, float* state, hipStream_t st) {
-    fp8_roll_k<<<1, 1, 0, st>>>(state);
+    fp8_roll_k<<<1, 1, 0, st>>>(state, fp8_hr());
     quant_delayed_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
 
@@ -373,14 +388,14 @@ void rn_fp8_quantize_delayed(const void* x, long n, void* q, float* state, hipSt
 void rn_fp8_quant_many(const void* flat, const long* segs, int nseg, long max_n, void* qbuf, int roll,
                        hipStream_t st) {
     if (nseg <= 0) return;
-    if (roll) fp8_roll_many_k<<<(nseg + 255) / 256, 256, 0, st>>>(segs, nseg);
+    if (roll) fp8_roll_many_k<<<(nseg + 255) / 256, 256, 0, st>>>(segs, nseg, fp8_hr());
     long per = (max_n / 8 + 255) / 256;  // blocks that cover the largest weight in one sweep
     const int bx = (int)(per < 1 ? 1 : (per > 64 ? 64 : per));
     fp8_quant_many_k<<<dim3(bx, nseg), 256, 0, st>>>((const bf16*)flat, segs, (uint8_t*)qbuf);
 }
 
 // The delayed-scaling roll alone (for producers that quantise inside their own kernel).
-void rn_fp8_roll(float* state, hipStream_t st) { fp8_roll_k<<<1, 1, 0, st>>>(state); }
+void rn_fp8_roll(float* state, hipStream_t st) { fp8_roll_k<<<1, 1, 0, st>>>(state, fp8_hr()); }
 
 void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipStream_t st) {
     dequant_k<<<gridn(n), 256, 0, st>>>((const uint8_t*)q, n, state, (bf16*)y);
@@ -390,7 +405,7 @@ void rn_fp8_dequantize(const void* q, long n, const float* state, void* y, hipSt
 // current scaling (memset + amax + quantise); state as rn_fp8_quantize_delayed
 void rn_bf8_quantize(const void* x, long n, void* q, float* state, int delayed, hipStream_t st) {
     if (delayed) {
-        fp8_roll_bf8_k<<<1, 1, 0, st>>>(state);
+        fp8_roll_bf8_k<<<1, 1, 0, st>>>(state, fp8_ghr());
         quant_delayed_bf8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
         return;
     }
@@ -398,7 +413,7 @@ void rn_bf8_quantize(const void* x, long n, void* q, float* state, int delayed, 
     amax_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, state);
     quant_bf8_k<<<gridn(n / 8 + 1), 256, 0, st>>>((const bf16*)x, n, (uint8_t*)q, state);
 }
-void rn_fp8_roll_bf8(float* state, hipStream_t st) { fp8_roll_bf8_k<<<1, 1, 0, st>>>(state); }
+void rn_fp8_roll_bf8(float* state, hipStream_t st) { fp8_roll_bf8_k<<<1, 1, 0, st>>>(state, fp8_ghr()); }
 
 // dH = dU ⊙ d in e5m2 (+ column partials [G][N] of dH when colpart): see act_mul_bf8_k.  N % 8 == 0.
 int rn_act_mul_bf8_groups(long M, int N) {
@@ -415,7 +430,7 @@ static void act_mul_bf8_run(const void* du, const void* d, long M, int N, void* 
     const int blocks = (int)((threads + 255) / 256);
     const bf16 *a = (const bf16*)du, *b = (const bf16*)d;
     if (delayed) {
-        fp8_roll_bf8_k<<<1, 1, 0, st>>>(state);
+        fp8_roll_bf8_k<<<1, 1, 0, st>>>(state, fp8_ghr());
         act_mul_bf8_k<2, FROM_H><<<blocks, 256, 0, st>>>(a, b, M, N, (uint8_t*)q, state, colpart, G);
         return;
     }
@@ -465,7 +480,7 @@ __global__ void __launch_bounds__(256) gelu_q8_k(const bf16* __restrict__ h, lon
     if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(state + 1), __float_as_int(m));
 }
 void rn_gelu_q8(const void* h, long n, void* q, float* state, hipStream_t st) {
-    fp8_roll_k<<<1, 1, 0, st>>>(state);
+    fp8_roll_k<<<1, 1, 0, st>>>(state, fp8_hr());
     const long blocks = (n / 8 + 255) / 256;
     gelu_q8_k<<<(int)std::min<long>(std::max<long>(blocks, 1), 8192), 256, 0, st>>>((const bf16*)h, n, (uint8_t*)q, state);
 }
@@ -494,7 +509,7 @@ int rn_gemm_fp8(const void* A8, const void* B8, void* C, const void* bias, const
         if (rn_gemm_launch_w1(w, 1, ACT_NONE, st, false) == 0) return 0;
     }
     scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
-    if (q8) fp8_roll_k<<<1, 1, 0, st>>>(q8st);
+    if (q8) fp8_roll_k<<<1, 1, 0, st>>>(q8st, fp8_hr());
     rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.bias = (const bf16*)bias; a.res = (const bf16*)res;
     a.pre = (bf16*)pre; a.ws = nullptr; a.alpha = alpha_ws;
