@@ -43,6 +43,7 @@ int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, 
 void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
 void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
 void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int, hipStream_t);
+int rn_xent_fwd_q8(void*, const int64_t*, float*, float*, int, int, int, long, void*, hipStream_t);
 void rn_xent_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, long, hipStream_t);
 void rn_emb_fwd(const int64_t*, const void*, const void*, void*, int, int, int, int, hipStream_t);
 void rn_vit_join_fwd(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
@@ -99,9 +100,9 @@ void rn_gelu_q8(const void*, long, void*, float*, hipStream_t);
 void rn_bf8_dequantize(const void*, long, const float*, void*, hipStream_t);
 long rn_gemm_fp8_wgrad_ws(int, int, int);
 int rn_gemm_fp8_wgrad(const void*, const void*, void*, const float*, const float*, float*, float*, int, int, int, long,
-                      long, long, int, int, int, hipStream_t);
+                      long, long, int, int, int, hipStream_t, const float*);
 int rn_gemm_fp8_dgrad(const void*, const void*, void*, const float*, const float*, float*, int, int, int, long, long,
-                      long, int, hipStream_t);
+                      long, int, hipStream_t, const float*);
 int rn_gemm_fp8(const void*, const void*, void*, const void*, const void*, void*, const float*, const float*, float*,
                 int, int, int, long, long, long, int, hipStream_t, void*, float*);
 long rn_bn_ws_floats(int, int);
@@ -482,6 +483,23 @@ std::tuple<Tensor, Tensor> xent_fwd(const Tensor& logits, const Tensor& target, 
     Tensor lse = at::empty({M}, logits.options().dtype(at::kFloat));
     if (M) rn_xent_fwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), M, V,
                        (int)nvalid, (long)ignore, write_grad, cur_stream());
+    return {loss, lse};
+}
+// the fp8 LM head's loss: as xent_fwd(write_grad) but the gradient goes to q8 (uint8 [M][V]) as e5m2 of
+// (softmax - onehot) · 2^15; the logits are left unchanged
+std::tuple<Tensor, Tensor> xent_fwd_q8(const Tensor& logits, const Tensor& target, int64_t nvalid, int64_t ignore,
+                                       const Tensor& q8) {
+    CHECK_BF16(logits); CHECK_CONTIG(logits); GUARD(logits);
+    TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous());
+    TORCH_CHECK(q8.scalar_type() == at::kByte && q8.is_contiguous() && q8.sizes() == logits.sizes());
+    const int M = logits.size(0), V = logits.size(1);
+    Tensor loss = at::empty({M}, logits.options().dtype(at::kFloat));
+    Tensor lse = at::empty({M}, logits.options().dtype(at::kFloat));
+    if (M) {
+        int rc = rn_xent_fwd_q8(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                lse.data_ptr<float>(), M, V, (int)nvalid, (long)ignore, q8.data_ptr(), cur_stream());
+        TORCH_CHECK(rc == 0, "xent_fwd_q8: V must be a multiple of 8 and <= 65536, got ", V);
+    }
     return {loss, lse};
 }
 void xent_bwd(const Tensor& logits, const Tensor& target, const Tensor& lse, const Tensor& gscale, const Tensor& grad,
@@ -1131,7 +1149,7 @@ Tensor bf8_dequantize(const Tensor& q, const Tensor& state) {
 // fp8 weight gradient: out[M,N] (+)= sa·sb · a8ᵀ · b8 with a8 [K][M] (e5m2 if a_bf8, else e4m3) and
 // b8 [K][N] e4m3, K = tokens (csrc/include/gemm_pk.h, fp8 MN-contiguous operands)
 void gemm_fp8_wgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb, const Tensor& out,
-                    bool accumulate, bool a_bf8) {
+                    bool accumulate, bool a_bf8, const optional<Tensor>& post) {
     GUARD(a8);
     TORCH_CHECK(a8.scalar_type() == at::kByte && b8.scalar_type() == at::kByte, "fp8 operands are uint8 storage");
     TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.size(0) == b8.size(0) && a8.stride(1) == 1 && b8.stride(1) == 1);
@@ -1143,12 +1161,13 @@ void gemm_fp8_wgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const 
     int rc = rn_gemm_fp8_wgrad(a8.data_ptr(), b8.data_ptr(), out.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(),
                                alpha.data_ptr<float>(), ws.data_ptr<float>(), M, N, K, a8.stride(0), b8.stride(0),
                                out.stride(0), accumulate ? 1 : 0, out.scalar_type() == at::kFloat ? 1 : 0, a_bf8 ? 1 : 0,
-                               cur_stream());
+                               cur_stream(), post ? post->data_ptr<float>() : nullptr);
     TORCH_CHECK(rc == 0, "gemm_fp8_wgrad: M, N and row strides must be multiples of 16 and K of 128, got M=", M,
                 " N=", N, " K=", K);
 }
 // fp8 data gradient: dY8 [M][K] (e5m2 if a_bf8) · W8 [K][N] (the e4m3 weight as stored) -> bf16 [M][N]
-Tensor gemm_fp8_dgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb, bool a_bf8) {
+Tensor gemm_fp8_dgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, const Tensor& sb, bool a_bf8,
+                      const optional<Tensor>& post) {
     GUARD(a8);
     TORCH_CHECK(a8.scalar_type() == at::kByte && b8.scalar_type() == at::kByte, "fp8 operands are uint8 storage");
     TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.size(1) == b8.size(0) && a8.stride(1) == 1 && b8.stride(1) == 1);
@@ -1158,7 +1177,7 @@ Tensor gemm_fp8_dgrad(const Tensor& a8, const Tensor& b8, const Tensor& sa, cons
     if (M == 0) return c;
     int rc = rn_gemm_fp8_dgrad(a8.data_ptr(), b8.data_ptr(), c.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(),
                                alpha.data_ptr<float>(), M, N, K, a8.stride(0), b8.stride(0), c.stride(0), a_bf8 ? 1 : 0,
-                               cur_stream());
+                               cur_stream(), post ? post->data_ptr<float>() : nullptr);
     TORCH_CHECK(rc == 0, "gemm_fp8_dgrad: K, N and row strides must be multiples of 16, got K=", K, " N=", N);
     return c;
 }
@@ -1234,6 +1253,7 @@ TORCH_LIBRARY(replicann, m) {
     m.def("softmax_fwd(Tensor x, float scale) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y, float scale) -> Tensor");
     m.def("xent_fwd(Tensor(a!) logits, Tensor target, int nvalid, int ignore, bool write_grad=False) -> (Tensor, Tensor)");
+    m.def("xent_fwd_q8(Tensor logits, Tensor target, int nvalid, int ignore, Tensor(a!) q8) -> (Tensor, Tensor)");
     m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale, Tensor(a!) grad, int nvalid, int ignore) -> ()");
     m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("layernorm_fwd_q8(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps, Tensor(a!) state) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
@@ -1286,8 +1306,9 @@ TORCH_LIBRARY(replicann, m) {
     m.def("act_mul_bf8(Tensor du, Tensor d, Tensor(a!) state, bool delayed, Tensor(b!)? bias_grad=None, bool from_h=False) -> Tensor");
     m.def("gelu_q8(Tensor h, Tensor(a!) state) -> Tensor");
     m.def("bf8_dequantize(Tensor q, Tensor state) -> Tensor");
-    m.def("gemm_fp8_wgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) out, bool accumulate, bool a_bf8) -> ()");
-    m.def("gemm_fp8_dgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, bool a_bf8) -> Tensor");
+    m.def("gemm_fp8_wgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) out, bool accumulate, bool a_bf8, "
+          "Tensor? post=None) -> ()");
+    m.def("gemm_fp8_dgrad(Tensor a8, Tensor b8, Tensor sa, Tensor sb, bool a_bf8, Tensor? post=None) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, Tensor? residual, int act, Tensor? preact) -> Tensor");
     m.def("gemm_fp8_q8(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor? bias, int act, Tensor(a!) preact, Tensor(b!) q8_state) -> (Tensor, Tensor)");
     m.def("fp8_quant_many(Tensor flat, Tensor segs, int max_n, Tensor(a!) qbuf, bool roll=True) -> ()");
@@ -1314,6 +1335,7 @@ TORCH_LIBRARY_IMPL(replicann, CUDA, m) {
     m.impl("softmax_fwd", &softmax_fwd);
     m.impl("softmax_bwd", &softmax_bwd);
     m.impl("xent_fwd", &xent_fwd);
+    m.impl("xent_fwd_q8", &xent_fwd_q8);
     m.impl("xent_bwd", &xent_bwd);
     m.impl("layernorm_fwd", &layernorm_fwd);
     m.impl("layernorm_fwd_q8", &layernorm_fwd_q8);

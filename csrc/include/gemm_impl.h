@@ -77,6 +77,9 @@ struct GemmArgs {
     const float* sb;
     // cfg 11 tile walk: tile-rows per group (0: GROUP_M)
     int group_m;
+    // split-K reduction only: optional device scalar multiplying the slab sum (the fp8 weight gradient of the
+    // LM head: the loss gradient's g / n; the slabs themselves carry only the power-of-two tensor scales)
+    const float* reduce_alpha;
 };
 
 template <int BN, int NT>
@@ -887,6 +890,7 @@ __global__ void __launch_bounds__(256) splitk_group_k(float* __restrict__ ws, lo
 template <int ACT, bool BATCH = true>
 __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
     const long total4 = ((long)p.M * p.N + 3) / 4;
+    const float ra = p.reduce_alpha ? *p.reduce_alpha : 1.f;
     for (long q = blockIdx.x * 256L + threadIdx.x; q < total4; q += (long)gridDim.x * 256) {
         const long e0 = q * 4;
         float v[4] = {0.f, 0.f, 0.f, 0.f};
@@ -915,6 +919,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
             if (e >= MN) break;
             const int m = e / p.N, n = e % p.N;
             float x = v[t];
+            if (p.reduce_alpha) x *= ra;
             if (p.bias) x += (float)p.bias[n];
             if constexpr (act_fwd(ACT)) {
                 float pv;

@@ -162,11 +162,13 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
     static_assert(AKC || (FP8 && !BKC && SPLIT), "w1 MN-contiguous A: the fp8 weight gradient (split-K slabs)");
     static_assert(!RES || (BKC && !ALPHA), "w1 residual: x·Wᵀ layout, no alpha");
     static_assert(ACT == ACT_NONE, "w1: forward epilogues without activation (activations: cfg 9)");
-    static_assert(!(FP8 && ALPHA), "fp8: the scales ride the MFMA");
+    // fp8: the power-of-two tensor scales ride the MFMA; ALPHA (fp8 MN-contiguous B only: the fp8 LM head's data
+    // gradient) multiplies in one more device scalar (the loss gradient's g / n)
+    static_assert(!(FP8 && ALPHA) || !BKC, "fp8 alpha: MN-contiguous B only");
     // fp8 with an MN-contiguous B (the data gradient dY·W, W read as stored): transposing tr_b8 fragment
     // reads in plain column order, so a lane holds two 4-column runs per output pair (8-B stores)
     constexpr bool F8MN = FP8 && !BKC;
-    static_assert(!F8MN || (!RES && !ALPHA), "w1 fp8 MN-contiguous B: plain epilogue");
+    static_assert(!F8MN || (!RES && !(ALPHA && SPLIT)), "w1 fp8 MN-contiguous B: plain / alpha epilogue");
     constexpr int SPP = F8MN ? 8 : 4;  // epilogue stores per output pair
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;

@@ -339,8 +339,9 @@ __global__ void __launch_bounds__(256) fp8_quant_many_k(const bf16* __restrict__
 }
 
 // alpha = sa * sb on device
-__global__ void scale_mul_k(const float* __restrict__ sa, const float* __restrict__ sb, float* __restrict__ alpha) {
-    alpha[0] = sa[0] * sb[0];
+__global__ void scale_mul_k(const float* __restrict__ sa, const float* __restrict__ sb, float* __restrict__ alpha,
+                            const float* __restrict__ post = nullptr) {
+    alpha[0] = sa[0] * sb[0] * (post ? post[0] : 1.f);
 }
 
 inline int gridn(long n) {
@@ -561,7 +562,7 @@ long rn_gemm_fp8_wgrad_split(int M, int N, int K) {
 long rn_gemm_fp8_wgrad_ws(int M, int N, int K) { return rn_gemm_fp8_wgrad_split(M, N, K) * (long)M * N; }
 int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, const float* sb, float* alpha_ws,
                       float* ws, int M, int N, int K, long lda, long ldb, long ldc, int accumulate, int out_f32,
-                      int a_bf8, hipStream_t st) {
+                      int a_bf8, hipStream_t st, const float* post) {
     if (M % 16 || N % 16 || lda % 16 || ldb % 16 || K % 128 || M <= 0 || N <= 0) return -1;
     const int split = (int)rn_gemm_fp8_wgrad_split(M, N, K);
     const int kern = fp8_gemm_kernel();
@@ -571,10 +572,10 @@ int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, 
         rn_gemm_detail::GemmArgs w = {};
         w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C; w.ws = ws;
         w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
-        w.out_f32 = out_f32; w.accumulate = accumulate;
+        w.out_f32 = out_f32; w.accumulate = accumulate; w.reduce_alpha = post;
         if (rn_gemm_launch_w1_wgrad(w, a_bf8 ? 2 : 1, split, st) == 0) return 0;
     }
-    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
+    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws, post);
     const int kt = K / 128, per = (kt + split - 1) / split;
     rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.ws = ws; a.alpha = alpha_ws;
@@ -590,8 +591,9 @@ int rn_gemm_fp8_wgrad(const void* A8, const void* B8, void* C, const float* sa, 
 // C[M,N] (bf16) = sa·sb · A8[M][K] · B8[K][N]: the fp8 data gradient dX = dY·W with dY (A8, e5m2 if
 // a_bf8) K-contiguous and the weight W [out = K][in = N] as stored (the forward's e4m3 weight copy),
 // read transposed.  K, N, lda, ldb, ldc multiples of 16 (bytes for the fp8 operands).
+// post (optional device scalar): one more output multiplier (the fp8 LM head's g / n)
 int rn_gemm_fp8_dgrad(const void* A8, const void* B8, void* C, const float* sa, const float* sb, float* alpha_ws,
-                      int M, int N, int K, long lda, long ldb, long ldc, int a_bf8, hipStream_t st) {
+                      int M, int N, int K, long lda, long ldb, long ldc, int a_bf8, hipStream_t st, const float* post) {
     if (K % 16 || N % 16 || lda % 16 || ldb % 16 || ldc % 8 || M <= 0) return -1;
     const int kern = fp8_gemm_kernel();
     if ((kern == 11 || kern < 0) && K % 128 == 0 && K >= 256) {
@@ -599,10 +601,10 @@ int rn_gemm_fp8_dgrad(const void* A8, const void* B8, void* C, const float* sa, 
         // power-of-two scales ride the scaled MFMA, no alpha pass)
         rn_gemm_detail::GemmArgs w = {};
         w.A = (const bf16*)A8; w.B = (const bf16*)B8; w.C = C;
-        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb;
+        w.M = M; w.N = N; w.K = K; w.lda = lda; w.ldb = ldb; w.ldc = ldc; w.sa = sa; w.sb = sb; w.alpha = post;
         if (rn_gemm_launch_w1(w, a_bf8 ? 2 : 1, ACT_NONE, st, true) == 0) return 0;
     }
-    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws);
+    scale_mul_k<<<1, 1, 0, st>>>(sa, sb, alpha_ws, post);
     rn_gemm_detail::GemmArgs a = {};
     a.A = (const bf16*)A8; a.B = (const bf16*)B8; a.C = C; a.alpha = alpha_ws;
     a.M = M; a.N = N; a.K = K / 2;

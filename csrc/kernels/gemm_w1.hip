@@ -26,7 +26,8 @@ int rn_gemm_launch_w1(GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn) {
     if (a.K % 128 || a.K < 256 || a.N % 8 || a.ldc % 8 || a.lda % 16 || a.ldb % 16) return -1;
     if (act != ACT_NONE) return -1;
     if (a.alpha && a.bias) return -1;
-    if (bmn && fp8 && (a.N % 16 || a.bias || a.res || a.alpha)) return -1;  // fp8 MN-contiguous B: plain epilogue
+    if (bmn && fp8 && (a.N % 16 || a.bias || a.res)) return -1;  // fp8 MN-contiguous B: plain / alpha epilogue
+    if (fp8 && !bmn && a.alpha) return -1;
     if (a.res && (bmn || a.alpha || a.K / 128 < 6)) return -1;  // residual bodies: K-tiles 1-4 of >= 6
     a.tiles_m = (a.M + 255) / 256;
     a.tiles_n = (a.N + 255) / 256;
@@ -55,8 +56,10 @@ int rn_gemm_launch_w1(GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn) {
         else launch_w1_t<0, ACT_NONE, false, true, 0, true>(a, st);
         return 0;
     }
-    if (fp8 && bmn) {  // the fp8 data gradient (A e4m3 or, fp8 == 2, e5m2)
-        if (fp8 == 2) launch_w1_t<2, ACT_NONE, false, false>(a, st);
+    if (fp8 && bmn) {  // the fp8 data gradient (A e4m3 or, fp8 == 2, e5m2; alpha: the fp8 LM head's g / n)
+        if (fp8 == 2 && a.alpha) launch_w1_t<2, ACT_NONE, true, false>(a, st);
+        else if (fp8 == 2) launch_w1_t<2, ACT_NONE, false, false>(a, st);
+        else if (a.alpha) launch_w1_t<1, ACT_NONE, true, false>(a, st);
         else launch_w1_t<1, ACT_NONE, false, false>(a, st);
     } else if (fp8) launch_w1_t<1, ACT_NONE, false, true>(a, st);
     else if (bmn) {
@@ -70,7 +73,8 @@ int rn_gemm_launch_w1(GemmArgs& a, int fp8, int act, hipStream_t st, bool bmn) {
 // The fp8 weight gradient dW = dYᵀ·X on the one-wave-per-SIMD kernel: A = dY [K = tokens][M = out] (e5m2 if
 // fp8 == 2), B = X [K][N = in] (e4m3), both MN-contiguous as stored; split-K fp32 slabs in ws (split × M × N
 // floats) summed by splitk_reduce_k into C (bf16 or fp32, accumulate or not).  K, lda, ldb in bytes;
-// M, N % 16; K / 128 divisible by split with >= 2 K-tiles per slab.
+// M, N % 16; K / 128 divisible by split with >= 2 K-tiles per slab.  a.reduce_alpha (optional device scalar)
+// multiplies the slab sum.
 int rn_gemm_launch_w1_wgrad(GemmArgs& a, int fp8, int split, hipStream_t st) {
     a.group_m = w1_group_m(a);
     const int kt = a.K / 128;

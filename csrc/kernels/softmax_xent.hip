@@ -187,10 +187,15 @@ __global__ void __launch_bounds__(1024) xent_row_k(bf16* __restrict__ logits, co
 // The logits are loaded non-temporally (the 6.6 GB GPT-2 logits stream cannot stay in any cache
 // between the LM-head GEMM, this pass and the backward GEMMs: 2.42 -> 2.38 ms); the gradient stores
 // stay plain (non-temporal stores measured 1.5x slower, 3.54-3.68 ms, gpu_r3zt).
-template <int CH>
+// Q8: the gradient goes to q8 (row stride V bytes) as e5m2 of (softmax - onehot) · 2^15 instead of bf16 over
+// the logits — the fp8 LM head's backward operand (ops/loss.py _LinearXentFp8Fn).  |softmax - onehot| <= 1, so the
+// fixed power-of-two scale XQ8_SCALE keeps every value below e5m2's 57344 and puts probabilities down to 2^-31 in
+// its range: no amax pass, no delayed-scaling slot.
+constexpr float XQ8_SCALE = 32768.f;
+template <int CH, bool Q8 = false>
 __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                     float* __restrict__ loss, float* __restrict__ lse_out, int V,
-                                                    int nvalid, long ignore) {
+                                                    int nvalid, long ignore, uint8_t* __restrict__ q8 = nullptr) {
     constexpr float L2E = 1.4426950408889634f;
     __shared__ float sm_m[16], sm_s[16];
     bf16* row = logits + (long)blockIdx.x * V;
@@ -273,6 +278,30 @@ __global__ void __launch_bounds__(1024) xent_row2_k(bf16* __restrict__ logits, c
     // this thread's e values were taken relative to ITS local max (mL): rescale to the row's lse
     // (a thread without a valid column has e = 0 and m = -inf: f = 0, never 0 · inf)
     const float f = (ign || m_own == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(mL - lse * L2E);
+    if constexpr (Q8) {
+        uint8_t* qrow = q8 + (long)blockIdx.x * V;
+        const float fq = f * XQ8_SCALE;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int i = threadIdx.x + k * 1024;
+            if (i < n8) {
+                float g[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) g[j] = (float)v[k][j] * fq;
+                int w0 = 0, w1 = 0;
+                w0 = __builtin_amdgcn_cvt_pk_bf8_f32(g[0], g[1], w0, false);
+                w0 = __builtin_amdgcn_cvt_pk_bf8_f32(g[2], g[3], w0, true);
+                w1 = __builtin_amdgcn_cvt_pk_bf8_f32(g[4], g[5], w1, false);
+                w1 = __builtin_amdgcn_cvt_pk_bf8_f32(g[6], g[7], w1, true);
+                *reinterpret_cast<uint2*>(qrow + i * 8) = make_uint2((uint32_t)w0, (uint32_t)w1);
+            }
+        }
+        if (!ign && threadIdx.x == (int)((t >> 3) & 1023)) {  // the one-hot term, as below
+            const float et = (float)(bf16)__builtin_amdgcn_exp2f(fmaf(xt, L2E, -mL));
+            qrow[t] = (uint8_t)(__builtin_amdgcn_cvt_pk_bf8_f32((et * f - 1.f) * XQ8_SCALE, 0.f, 0, false) & 0xFF);
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
         const int i = threadIdx.x + k * 1024;
@@ -343,6 +372,18 @@ void rn_xent_fwd(void* logits, const int64_t* tgt, float* loss, float* lse, int 
     }
     if (write_grad) xent_fwd_k<true><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
     else xent_fwd_k<false><<<M, TPB, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore);
+}
+// the fp8 LM head's loss: rn_xent_fwd with write_grad, the gradient to q8 as e5m2 · 2^15 (xent_row2_k<.., true>);
+// -1 if V is outside the row kernel's range (the caller keeps the bf16 path)
+int rn_xent_fwd_q8(void* logits, const int64_t* tgt, float* loss, float* lse, int M, int V, int nvalid, long ignore,
+                   void* q8, hipStream_t st) {
+    if (V % 8 || V > 8 * 1024 * 8) return -1;
+    const int ch = (V / 8 + 1023) / 1024;
+#define RN_XQ(C) xent_row2_k<C, true><<<M, 1024, 0, st>>>((bf16*)logits, tgt, loss, lse, V, nvalid, ignore, (uint8_t*)q8)
+    if (ch <= 1) RN_XQ(1); else if (ch <= 2) RN_XQ(2); else if (ch <= 4) RN_XQ(4); else if (ch <= 7) RN_XQ(7);
+    else RN_XQ(8);
+#undef RN_XQ
+    return 0;
 }
 void rn_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* grad, int M,
                  int V, int nvalid, long ignore, hipStream_t st) {

@@ -65,6 +65,25 @@ class Linear(nn.Module):
         return ops.linear(x, self.weight, self.bias, act=act, residual=residual, fp8=self.fp8_state)
 
 
+class Fp8Slots(nn.Module):
+    """Delayed-scaling state of an fp8 GEMM whose weight lives elsewhere — the GPT-2 LM head, whose weight is
+    the tied token embedding: the activation / weight slots as a checkpointed buffer, as :class:`Linear`'s."""
+
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("fp8_scales", torch.zeros(2, 4))
+        self.fp8_state = ops.Fp8State(owner=self)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, *args, **kwargs):
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, *args, **kwargs)
+        key = prefix + "fp8_scales"
+        if key not in state_dict:  # a checkpoint of a model without the fp8 head: empty slots
+            self.fp8_scales.zero_()
+            if key in missing_keys:
+                missing_keys.remove(key)
+        self.fp8_state.sync_ready()
+
+
 class LayerNorm(nn.Module):
     def __init__(self, n, eps=1e-5):
         super().__init__()

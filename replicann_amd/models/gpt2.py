@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .blocks import KVCache, LayerNorm, PreLNBlock
+from .blocks import Fp8Slots, KVCache, LayerNorm, PreLNBlock
 
 
 @dataclass(frozen=True)
@@ -43,6 +43,13 @@ class GPT2Config:
     # (profiles/fp8_gemm_ab_r2r.txt).  c_attn / c_fc take e4m3 straight from the LayerNorm kernel,
     # the MLP c_proj from c_fc's GEMM epilogue (REPLICANN_FP8_PROJ=1: on, for A/B)
     fp8_proj: bool = os.environ.get("REPLICANN_FP8_PROJ", "0") == "1"
+    # fp8 LM head (fp8 models, training steps only; ops.loss._LinearXentFp8Fn): 1 = logits from e4m3 h · e4m3
+    # wte, the loss gradient straight to e5m2 by the cross-entropy kernel, both head gradients on the fp8 GEMMs;
+    # 2 = the same gradients with the logits GEMM kept in bf16 (the loss itself unquantised); 0 = bf16 head.
+    # Default 1: GPT-2-medium-fp8 132.0 ms/step against 139.9 (bf16 head) and 166.0 (bf16) on one box; the
+    # held-out loss after 50 steps is within 1.4 % of the bf16 model's (1.1 % with the bf16 head)
+    # (profiles/gpt2m_fp8_head_r5op.txt)
+    fp8_head: int = int(os.environ.get("REPLICANN_FP8_HEAD", "1"))
     # LM head + loss over row chunks of this many tokens (0: the whole batch at once).  Bounds the
     # logits buffer (rows x vocab_pad bf16: 6.6 GB at b64 x 1024) for long sequences / big batches
     ce_chunk: int = 0
@@ -89,6 +96,8 @@ class GPT2(nn.Module):
             for _ in range(cfg.n_layer)
         )
         self.ln_f = LayerNorm(cfg.n_embd, cfg.ln_eps)
+        # the fp8 LM head's scale slots (the weight is wte); absent unless fp8 and fp8_head
+        self.head8 = Fp8Slots() if (cfg.fp8 and cfg.fp8_head > 0) else None
 
     def num_params(self, non_embedding=False):
         n = sum(p.numel() for p in self.parameters())
@@ -97,7 +106,9 @@ class GPT2(nn.Module):
             n -= self.wpe.numel()
         return n
 
-    def hidden(self, idx):
+    def hidden(self, idx, fp8_head=None):
+        """Final-LayerNorm output (B, T, n_embd); ``fp8_head``: the fp8 LM head's state, whose e4m3 input the
+        LayerNorm kernel then writes as well."""
         x = ops.embedding(idx, self.wte, self.wpe)
         if self.config.dropout > 0 and self.training:
             x = ops.dropout(x, self.config.dropout, True)
@@ -105,18 +116,21 @@ class GPT2(nn.Module):
         for blk in self.h:
             x = blk(x, prev)
             prev = blk.out_bias()
-        return self.ln_f(x, producer_bias=prev)
+        return self.ln_f(x, producer_bias=prev, fp8=fp8_head)
 
     def forward(self, idx, targets=None):
         """idx (B, T) → logits (B, T, vocab_pad) [, mean CE loss when targets given].
 
         With ``targets`` only the loss is returned (logits are consumed in place).
         """
-        h = self.hidden(idx)
+        fp8h = (self.head8.fp8_state if self.head8 is not None and targets is not None and self.training
+                and torch.is_grad_enabled() and self.wte.is_cuda else None)
+        h = self.hidden(idx, fp8h)
         if targets is None:
             return ops.linear(h, self.wte)[..., : self.config.vocab_size]
         return ops.linear_cross_entropy(h, self.wte, targets, n_valid_cols=self.config.vocab_size,
-                                        chunk_rows=self.config.ce_chunk)
+                                        chunk_rows=self.config.ce_chunk, fp8=fp8h,
+                                        fp8_logits=self.config.fp8_head != 2)
 
     @torch.no_grad()
     def decode_step(self, idx, cache):

@@ -157,14 +157,89 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         return out_h, out_w, None, None, None, None
 
 
-def linear_cross_entropy(h, weight, target, *, n_valid_cols=None, ignore_index=-100, chunk_rows=0):
+XQ8_SCALE = 32768.0  # e5m2 loss-gradient scale of the fp8 LM head (csrc/kernels/softmax_xent.hip XQ8_SCALE)
+
+
+class _LinearXentFp8Fn(torch.autograd.Function):
+    """The LM head + cross-entropy in fp8 (training steps of the fp8 models, ``GPT2Config.fp8_head``):
+
+    * logits = e4m3(h) · e4m3(W)ᵀ on the one-wave-per-SIMD fp8 GEMM (h's e4m3 copy from the final LayerNorm
+      kernel, W = the tied embedding quantised with delayed scaling), bf16 logits;
+    * the CE kernel writes the UNSCALED gradient (softmax − onehot) as e5m2 · 2^15 (``xent_fwd_q8``): a fixed
+      power-of-two scale, |softmax − onehot| <= 1, so no amax pass.  The bf16 logits die with the forward;
+      the 1-byte gradient is what the backward keeps;
+    * backward: dh = dlogits8 · W8 (fp8 data-gradient GEMM, W read as stored) and dW += dlogits8ᵀ · h8 (fp8
+      split-K weight gradient into the flat fp32 gradient), with g / n as one more device scalar (the
+      GEMM's alpha / the split-K reduction's multiplier).
+
+    Same operand shapes as :class:`_LinearXentFn`; GPT-2-medium b64: 3 × 6.75 TFLOP of bf16 GEMM → fp8.
+    ``fp8_logits`` False: the logits GEMM stays bf16 (the loss value carries no e4m3 noise), the two gradient
+    GEMMs are fp8 as above."""
+
+    @staticmethod
+    def forward(ctx, h, weight, target, n_valid_cols, ignore_index, state, fp8_logits=True):
+        ops = _ext.ops()
+        shp = h.shape
+        h2 = h.reshape(-1, shp[-1]).contiguous()
+        xq, xs = state.quant(h2, 0)
+        wq, ws = state.quant(weight.contiguous(), 1)
+        if fp8_logits:
+            logits = ops.gemm_fp8(xq, wq, xs, ws, None, None, 0, None)
+        else:
+            logits = ops.gemm(h2, weight, False, True, None, None, 0, None, None, False, 0, False, None, -1)
+        tg = target.reshape(-1).long().contiguous()
+        q8 = torch.empty(logits.shape, dtype=torch.uint8, device=logits.device)
+        loss_rows, _ = ops.xent_fwd_q8(logits, tg, n_valid_cols, ignore_index, q8)
+        del logits
+        n = (tg != ignore_index).sum().clamp_min(1).float()
+        gs = torch.full((4,), 1.0 / XQ8_SCALE, dtype=torch.float32, device=h2.device)
+        ctx.save_for_backward(weight, xq, xs.clone(), wq, ws.clone(), q8, n, gs)
+        ctx.shp = shp
+        return loss_rows.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        from .linear import _direct_grad, _notify
+        weight, xq, xs, wq, ws, q8, n, gs = ctx.saved_tensors
+        alpha = (g.float() / n).reshape(1)
+        ops = _ext.ops()
+        gh = gw = None
+        if ctx.needs_input_grad[0]:
+            gh = ops.gemm_fp8_dgrad(q8, wq, gs, ws, True, alpha).reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            acc = _direct_grad(weight)
+            if acc is not None:
+                ops.gemm_fp8_wgrad(q8, xq, gs, xs, acc, True, True, alpha)
+                _notify(weight)
+            else:
+                gw = torch.empty(weight.shape, dtype=torch.float32, device=q8.device)
+                ops.gemm_fp8_wgrad(q8, xq, gs, xs, gw, False, True, alpha)
+                gw = gw.to(weight.dtype)
+        return gh, gw, None, None, None, None, None
+
+
+def fp8_head_ok(h, weight) -> bool:
+    """Shapes the fp8 LM head takes: vocab rows % 128 (the data gradient's K-tiles), width % 128, tokens % 128
+    (the weight gradient's K-tiles), vocab <= 65536 (the CE row kernel)."""
+    rows = h.numel() // h.shape[-1]
+    V, E = weight.shape
+    return V % 128 == 0 and V <= 65536 and E % 128 == 0 and E >= 256 and rows % 128 == 0 and rows > 0
+
+
+def linear_cross_entropy(h, weight, target, *, n_valid_cols=None, ignore_index=-100, chunk_rows=0, fp8=None,
+                         fp8_logits=True):
     """mean CE(h·weightᵀ, target) without materialising a separate logits gradient.
 
     ``chunk_rows`` > 0 (GPU): the LM head and the loss run over row chunks of that size, so
-    the logits never exist for more than ``chunk_rows`` rows at once (``_ChunkedLinearXentFn``)."""
+    the logits never exist for more than ``chunk_rows`` rows at once (``_ChunkedLinearXentFn``).
+    ``fp8``: an :class:`~replicann_amd.ops.fp8.Fp8State` — the head in fp8 (``_LinearXentFp8Fn``; GPU, whole
+    batch, shapes per :func:`fp8_head_ok`; ``fp8_logits`` False: bf16 logits, fp8 gradients)."""
     nv = weight.shape[0] if n_valid_cols is None else n_valid_cols
     if _ext.use_native(h):
         rows = h.numel() // h.shape[-1]
+        if fp8 is not None and not (chunk_rows and chunk_rows < rows) and fp8_head_ok(h, weight):
+            fp8.enter()
+            return _LinearXentFp8Fn.apply(h, weight, target, nv, ignore_index, fp8, bool(fp8_logits))
         if chunk_rows and chunk_rows < rows:
             return _ChunkedLinearXentFn.apply(h, weight, target, nv, ignore_index, int(chunk_rows))
         return _LinearXentFn.apply(h, weight, target, nv, ignore_index)

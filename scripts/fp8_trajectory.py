@@ -17,22 +17,31 @@ def run(model, steps, batch, lr):
                       weight_decay=0.1, log_every=10**9, seed=7)
     tr = Trainer(cfg)
     out = [float(tr.step()) for _ in range(steps)]
+    # held-out loss of the trained model in eval mode (the next 4 batches of the same stream for both runs): the
+    # fp8 model's LM head runs in bf16 there, so this separates training quality from the fp8 head's logits
+    # noise in the training loss (E[lse(z + e)] > lse(z))
+    tr.model.eval()
+    with torch.no_grad():
+        ev = sum(float(tr.model(*(t.cuda() for t in next(tr.data)))) for _ in range(4)) / 4
+    tr.model.train()
     del tr
     torch.cuda.empty_cache()
-    return out
+    return out, ev
 
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     lr = float(sys.argv[3]) if len(sys.argv) > 3 else 1e-4
-    bf = run("gpt2-medium", steps, batch, lr)
-    f8 = run("gpt2-medium-fp8", steps, batch, lr)
+    bf, ev_bf = run("gpt2-medium", steps, batch, lr)
+    f8, ev_f8 = run("gpt2-medium-fp8", steps, batch, lr)
     dev = [abs(a - b) / abs(b) for a, b in zip(f8, bf)]
     for i, (a, b, d) in enumerate(zip(bf, f8, dev)):
         print(json.dumps({"step": i + 1, "bf16": round(a, 5), "fp8": round(b, 5), "rel_dev": round(d, 5)}))
     print(json.dumps({"summary": True, "steps": steps, "batch": batch, "lr": lr, "max_rel_dev": round(max(dev), 5),
-                      "final_bf16": round(bf[-1], 5), "final_fp8": round(f8[-1], 5)}))
+                      "final_bf16": round(bf[-1], 5), "final_fp8": round(f8[-1], 5),
+                      "eval_bf16": round(ev_bf, 5), "eval_fp8": round(ev_f8, 5),
+                      "eval_rel_dev": round(abs(ev_f8 - ev_bf) / abs(ev_bf), 5)}))
 
 
 if __name__ == "__main__":
