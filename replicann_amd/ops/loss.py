@@ -219,11 +219,11 @@ class _LinearXentFp8Fn(torch.autograd.Function):
 
 
 def fp8_head_ok(h, weight) -> bool:
-    """Shapes the fp8 LM head takes: vocab rows % 128 (the data gradient's K-tiles), width % 128, tokens % 128
-    (the weight gradient's K-tiles), vocab <= 65536 (the CE row kernel)."""
+    """Shapes the fp8 LM head takes: vocab rows % 128, >= 256 (the data gradient's K-tiles), width % 16,
+    tokens % 128 (the weight gradient's K-tiles), vocab <= 65536 (the CE row kernel)."""
     rows = h.numel() // h.shape[-1]
     V, E = weight.shape
-    return V % 128 == 0 and V <= 65536 and E % 128 == 0 and E >= 256 and rows % 128 == 0 and rows > 0
+    return V % 128 == 0 and 256 <= V <= 65536 and E % 16 == 0 and rows % 128 == 0 and rows > 0
 
 
 def linear_cross_entropy(h, weight, target, *, n_valid_cols=None, ignore_index=-100, chunk_rows=0, fp8=None,

@@ -9,24 +9,27 @@ import replicann_amd as R
 from replicann_amd.ops.fp8 import fp8_states
 
 
-def _model():
+def _model(head=0):
+    """fp8 GPT-2 tiny; the fp8 LM head (GPU-only) off unless ``head``."""
     torch.manual_seed(0)
-    return R.GPT2(R.GPT2Config.tiny(fp8=True))
+    return R.GPT2(R.GPT2Config.tiny(fp8=True, fp8_head=head))
 
 
 def test_fp8_scales_are_state_dict_buffers():
-    m = _model()
+    m = _model(head=1)
     keys = [k for k in m.state_dict() if k.endswith("fp8_scales")]
-    assert len(keys) == 3 * m.config.n_layer  # c_attn, c_fc, mlp c_proj per block
+    # c_attn, c_fc, mlp c_proj per block + the fp8 LM head's slots (GPT2Config.fp8_head)
+    assert len(keys) == 3 * m.config.n_layer + (1 if m.config.fp8_head else 0)
     ids = torch.randint(0, 1000, (2, 32))
     m(ids, ids)  # first quantisation: current scaling fills the slots
-    sts = fp8_states(m)
+    head = m.head8.fp8_state if m.head8 is not None else None
+    sts = [st for st in fp8_states(m) if st is not head]  # the fp8 LM head runs on the GPU only
     assert all(st.ready == [True, True] for st in sts)
-    m2 = _model()
+    m2 = _model(head=1)
     assert not any(any(st.ready) for st in fp8_states(m2))
     m2.load_state_dict(m.state_dict())
     for a, b in zip(fp8_states(m), fp8_states(m2)):
-        assert torch.equal(a.t, b.t) and b.ready == [True, True]
+        assert torch.equal(a.t, b.t) and b.ready == a.ready
 
 
 @pytest.mark.gpu
