@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def rel_err(a, b):
-    a, b = a.float(), b.float()
+    a, b = a.float().cpu(), b.float().cpu()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
@@ -703,9 +703,10 @@ def test_conv2d(cuda, cfg):
     y = ops.conv2d_nhwc(x, w, b, S, P)
     g = bf(*y.shape)
     y.backward(g)
-    xf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, w, b)]
+    torch.cuda.synchronize()  # a fault in the native kernels surfaces here, not in the reference
+    xf, wf, bf_ = [t.detach().float().cpu().requires_grad_() for t in (x, w, b)]
     yf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), bf_, S, P).permute(0, 2, 3, 1)
-    yf.backward(g.float())
+    yf.backward(g.float().cpu())
     assert rel_err(y, yf) < 1e-2
     for t, tf in ((x, xf), (w, wf), (b, bf_)):
         assert rel_err(t.grad, tf.grad) < 2e-2
@@ -743,9 +744,10 @@ def test_conv2d_implicit_gemm(cuda, C, OC, Kk, S, P, HW):
     y = ops.conv2d_nhwc(x, w, None, S, P)
     g = bf(*y.shape)
     y.backward(g)
-    xf, wf = [t.detach().float().requires_grad_() for t in (x, w)]
+    torch.cuda.synchronize()  # a fault in the native kernels surfaces here, not in the reference
+    xf, wf = [t.detach().float().cpu().requires_grad_() for t in (x, w)]
     yf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), None, S, P).permute(0, 2, 3, 1)
-    yf.backward(g.float())
+    yf.backward(g.float().cpu())
     assert y.shape == yf.shape
     assert rel_err(y, yf) < 1e-2
     assert rel_err(x.grad, xf.grad) < 2e-2
@@ -761,12 +763,13 @@ def test_batchnorm(cuda, relu):
     y = ops.batch_norm_nhwc(x, w, b, rm, rv, True, 0.1, 1e-5, relu)
     g = bf(*y.shape)
     y.backward(g)
-    xf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, w, b)]
-    rm2, rv2 = torch.zeros(40, device="cuda"), torch.ones(40, device="cuda")
+    torch.cuda.synchronize()  # a fault in the native kernels surfaces here, not in the reference
+    xf, wf, bf_ = [t.detach().float().cpu().requires_grad_() for t in (x, w, b)]
+    rm2, rv2 = torch.zeros(40), torch.ones(40)
     yf = F.batch_norm(xf.permute(0, 3, 1, 2), rm2, rv2, wf, bf_, True, 0.1, 1e-5).permute(0, 2, 3, 1)
     if relu:
         yf = F.relu(yf)
-    yf.backward(g.float())
+    yf.backward(g.float().cpu())
     assert rel_err(y, yf) < 1e-2
     assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
     for t, tf in ((x, xf), (w, wf), (b, bf_)):
@@ -785,17 +788,18 @@ def test_batchnorm_residual_relu(cuda, C):
     y = ops.batch_norm_nhwc(x, w, b, rm, rv, True, 0.1, 1e-5, True, residual=r)
     g = bf(*y.shape)
     y.backward(g)
-    xf, rf, wf, bf_ = [t.detach().float().requires_grad_() for t in (x, r, w, b)]
-    rm2, rv2 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    torch.cuda.synchronize()  # a fault in the native kernels surfaces here, not in the reference
+    xf, rf, wf, bf_ = [t.detach().float().cpu().requires_grad_() for t in (x, r, w, b)]
+    rm2, rv2 = torch.zeros(C), torch.ones(C)
     yf = F.relu(F.batch_norm(xf.permute(0, 3, 1, 2), rm2, rv2, wf, bf_, True, 0.1, 1e-5).permute(0, 2, 3, 1) + rf)
-    yf.backward(g.float())
+    yf.backward(g.float().cpu())
     assert rel_err(y, yf) < 1e-2
     assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
     for t, tf in ((x, xf), (r, rf), (w, wf), (b, bf_)):
         assert rel_err(t.grad, tf.grad) < 3e-2
     # eval mode (running statistics) with the residual
     ye = ops.batch_norm_nhwc(x.detach(), w.detach(), b.detach(), rm, rv, False, 0.1, 1e-5, True, residual=r.detach())
-    yef = F.relu(F.batch_norm(xf.detach().permute(0, 3, 1, 2), rm, rv, wf.detach(), bf_.detach(), False, 0.1,
+    yef = F.relu(F.batch_norm(xf.detach().permute(0, 3, 1, 2), rm.cpu(), rv.cpu(), wf.detach(), bf_.detach(), False, 0.1,
                               1e-5).permute(0, 2, 3, 1) + rf.detach())
     assert rel_err(ye, yef) < 1e-2
 
@@ -809,10 +813,11 @@ def test_maxpool_ties(cuda, C):
     y = ops.maxpool_nhwc(x, 3, 2, 1)
     g = bf(*y.shape)
     y.backward(g)
-    xf = x.detach().float().requires_grad_()
+    torch.cuda.synchronize()  # a fault in the native kernels surfaces here, not in the reference
+    xf = x.detach().float().cpu().requires_grad_()
     yf = F.max_pool2d(xf.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
-    yf.backward(g.float())
-    assert torch.equal(y.float(), yf)
+    yf.backward(g.float().cpu())
+    assert torch.equal(y.float().cpu(), yf)
     assert rel_err(x.grad, xf.grad) < 1e-2
 
 
@@ -822,9 +827,10 @@ def test_pools(cuda):
     y = ops.maxpool_nhwc(x, 3, 2, 1)
     g = bf(*y.shape)
     y.backward(g)
-    xf = x.detach().float().requires_grad_()
+    torch.cuda.synchronize()
+    xf = x.detach().float().cpu().requires_grad_()
     yf = F.max_pool2d(xf.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
-    yf.backward(g.float())
+    yf.backward(g.float().cpu())
     assert rel_err(y, yf) < 1e-2 and rel_err(x.grad, xf.grad) < 1e-2
     x2 = bf(3, 7, 7, 32).requires_grad_()
     a = ops.avgpool_nhwc(x2)
@@ -1069,11 +1075,12 @@ def test_conv_bn_fused_statistics(cuda, monkeypatch, fused, N, HW, C, OC):
     y = ops.batch_norm_nhwc(yc, g, b, rm, rv, True, 0.1, 1e-5, relu=True)
     go = bf(*y.shape)
     y.backward(go)
-    xf, wf, gf, bf_ = [t.detach().float().requires_grad_() for t in (x, w, g, b)]
-    rmf, rvf = torch.zeros(OC, device="cuda"), torch.ones(OC, device="cuda")
+    torch.cuda.synchronize()  # a fault in the native kernels surfaces here, not in the reference
+    xf, wf, gf, bf_ = [t.detach().float().cpu().requires_grad_() for t in (x, w, g, b)]
+    rmf, rvf = torch.zeros(OC), torch.ones(OC)
     ycf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), None, 1, 1)
     yf = F.relu(F.batch_norm(ycf, rmf, rvf, gf, bf_, True, 0.1, 1e-5)).permute(0, 2, 3, 1)
-    yf.backward(go.float())
+    yf.backward(go.float().cpu())
     assert rel_err(y, yf) < 2e-2
     assert rel_err(rm, rmf) < 2e-2 and rel_err(rv, rvf) < 2e-2
     for t, tf in ((x, xf), (w, wf), (g, gf), (b, bf_)):
