@@ -24,7 +24,7 @@ extern "C" {
 
 // Weight-gradient tile (mode 3; M = output channels, N = taps × channels):
 //   0: 128×128, 4 waves   1: 64×192, 4 waves (M = 64: no half-empty tile)
-//   2: 128×192, 8 waves   3: 256×128, 8 waves
+//   2: 128×192, 8 waves   3: 256×128, 8 waves   4: 64×192, 8 waves (32×48 per wave; M = 64)
 // REPLICANN_CONVW=<v> forces one (A/B timing); otherwise the measured choice per shape.
 int rn_conv_wgrad_variant(int M, int N) {
     static int forced = [] {
@@ -33,14 +33,16 @@ int rn_conv_wgrad_variant(int M, int N) {
     }();
     // measured (scripts/conv_ab.py, ResNet-18 B=256): 128×192 / 8 waves is fastest on every 3×3
     // layer shape (layer1 0.368 → 0.246 ms, layers 2-4 0.18-0.19 → 0.11-0.135 ms vs 128×128)
-    int v = forced >= 0 ? forced : 2;
-    if ((v == 1 || v == 2) && N % 192 != 0) v = 0;
-    if (v == 1 && M != 64) v = 0;
+    // 64-output-channel layers (ResNet layer 1): 64×192 / 8 waves, no half-empty 128-row tile — 0.192-0.197 →
+    // 0.166-0.169 ms (profiles/conv_wgrad_r5u.txt)
+    int v = forced >= 0 ? forced : (M == 64 && N % 192 == 0 ? 4 : 2);
+    if ((v == 1 || v == 2 || v == 4) && N % 192 != 0) v = 0;
+    if ((v == 1 || v == 4) && M != 64) v = 0;
     if (v == 3 && M < 256) v = 0;
     return v;
 }
 void rn_conv_wgrad_tile(int M, int N, int* bm, int* bn) {
-    static const int BMS[4] = {128, 64, 128, 256}, BNS[4] = {128, 192, 192, 128};
+    static const int BMS[5] = {128, 64, 128, 256, 64}, BNS[5] = {128, 192, 192, 128, 192};
     const int v = rn_conv_wgrad_variant(M, N);
     *bm = BMS[v];
     *bn = BNS[v];
@@ -92,6 +94,7 @@ int rn_conv_gemm(int mode, const void* A, const void* B, void* C, const void* bi
             case 1: conv_launch<64, 192, 1, 4, 3, false, false>(a, st); break;
             case 2: conv_launch<128, 192, 2, 4, 3, false, false>(a, st); break;
             case 3: conv_launch<256, 128, 4, 2, 3, false, false>(a, st); break;
+            case 4: conv_launch<64, 192, 2, 4, 3, false, false>(a, st); break;
             default: conv_launch<128, 128, 2, 2, 3, false, false>(a, st); break;
         }
         return 0;
