@@ -18,8 +18,9 @@ def _model(head=0):
 def test_fp8_scales_are_state_dict_buffers():
     m = _model(head=1)
     keys = [k for k in m.state_dict() if k.endswith("fp8_scales")]
-    # c_attn, c_fc, mlp c_proj per block + the fp8 LM head's slots (GPT2Config.fp8_head)
-    assert len(keys) == 3 * m.config.n_layer + (1 if m.config.fp8_head else 0)
+    # c_attn, c_fc, mlp c_proj (+ attention c_proj with fp8_proj) per block + the fp8 LM head's slots (fp8_head)
+    per_block = 4 if m.config.fp8_proj else 3
+    assert len(keys) == per_block * m.config.n_layer + (1 if m.config.fp8_head else 0)
     ids = torch.randint(0, 1000, (2, 32))
     m(ids, ids)  # first quantisation: current scaling fills the slots
     head = m.head8.fp8_state if m.head8 is not None else None

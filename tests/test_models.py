@@ -168,7 +168,7 @@ def test_gpt2_fp8_train_steps(cuda):
 @pytest.mark.gpu
 def test_gpt2_fp8_layernorm_fed_and_tracks_bf16(cuda):
     """fp8 GPT-2 blocks: c_attn / c_fc take their e4m3 input from the LayerNorm kernel (after the
-    first, current-scaling step), the output projections stay bf16, and the loss trajectory tracks
+    first, current-scaling step), the attention output projection is fp8 as configured, and the loss trajectory tracks
     the bf16 model's."""
     kw = {"n_embd": 256, "n_head": 4}
 
@@ -186,5 +186,6 @@ def test_gpt2_fp8_layernorm_fed_and_tracks_bf16(cuda):
         assert blk.attn.c_attn.fp8_state.wcache is tr8.fp8_cache
         assert blk.attn.c_attn.fp8_state.fed >= 7 and blk.mlp.c_fc.fp8_state.fed >= 7
         assert blk.mlp.c_proj.fp8_state.fed >= 7  # from c_fc's GEMM epilogue
-        assert blk.attn.c_proj.fp8_state is None
+        # the attention output projection: fp8 with its own quantisation pass iff GPT2Config.fp8_proj
+        assert (blk.attn.c_proj.fp8_state is not None) == tr8.model.config.fp8_proj
     assert all(abs(a - b) < 0.05 * abs(b) for a, b in zip(l8, l16)), (l8, l16)
