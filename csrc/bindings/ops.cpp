@@ -82,6 +82,8 @@ void rn_colsum_f32(const float*, int, int, float*, void*, int, hipStream_t);
 int rn_colsum_ws(int);
 int rn_attn_is_fast(int);
 void rn_conv_wgrad_tile(int, int, int*, int*);
+int rn_conv3x3_tiles(int, int, int);
+int rn_conv3x3(const void*, const void*, void*, float*, int, int, int, int, int, hipStream_t);
 int rn_conv_gemm(int, const void*, const void*, void*, const void*, float*, int, int, int, long, long, long, int, int,
                  int, int, int, int, int, int, int, int, int, long, int, int, int, float*, hipStream_t);
 void rn_im2col(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -875,6 +877,19 @@ static std::tuple<Tensor, Tensor> conv_fwd_implicit_impl(const Tensor& x, const 
     const int OH = (H + 2 * P - KH) / S + 1, OW = (W + 2 * P - KW) / S + 1;
     Tensor y = at::empty({N, OH, OW, OC}, x.options());
     const int M = N * OH * OW, K = KH * KW * C;
+    // 3×3 / stride 1 / pad 1, 64 → 64 channels (ResNet layer 1): the halo-tile kernel (conv3x3.hip); its
+    // statistics partials are per tile of whole image rows instead of per 256 pixels
+    const bool has_bias = bias && bias->defined();
+    if (KH == 3 && KW == 3 && S == 1 && P == 1 && C == 64 && OC == 64 && !has_bias && M > 0) {
+        const int tiles = rn_conv3x3_tiles(N, H, W);
+        if (tiles > 0) {
+            Tensor part3 = stats ? at::empty({tiles, 2L * OC}, x.options().dtype(at::kFloat))
+                                 : at::empty({0}, x.options().dtype(at::kFloat));
+            if (rn_conv3x3(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part3.data_ptr<float>() : nullptr, N, H,
+                           W, 0, 0, cur_stream()) == 0)
+                return {y, part3};
+        }
+    }
     Tensor part = stats ? at::empty({(M + 255) / 256, 2L * OC}, x.options().dtype(at::kFloat))
                         : at::empty({0}, x.options().dtype(at::kFloat));
     if (M == 0) return {y, part};
@@ -912,6 +927,10 @@ Tensor conv_dgrad_implicit(const Tensor& dy, const Tensor& w, int64_t H, int64_t
     Tensor dx = grad_out(out, accumulate, {N, H, W, C}, dy, "conv dgrad");
     const int M = N * (int)H * (int)W, K = KH * KW * OC;
     if (M == 0) return dx;
+    if (KH == 3 && KW == 3 && P == 1 && C == 64 && OC == 64 &&
+        rn_conv3x3(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, N, (int)H, (int)W, 1, accumulate ? 1 : 0,
+                   cur_stream()) == 0)
+        return dx;  // the halo-tile kernel (conv3x3.hip), flipped / transposed weights
     const int rc = rn_conv_gemm(2, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, nullptr, M, C, K, 0, 0, C, OH,
                                 OW, OC, (int)H, (int)W, KH, KW, 1, (int)P, OC, C, (long)KH * KW * C, 1, 0,
                                 accumulate ? 1 : 0, nullptr, cur_stream());
