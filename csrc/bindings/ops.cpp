@@ -39,7 +39,7 @@ void rn_fp8_quant_many(const void*, const long*, int, long, void*, int, hipStrea
 int rn_ln_bwd_waves(int);
 long rn_ln_bwd_ws(int, int);
 int rn_ln_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
-              void*, void*, void*, float*, int, int, int, hipStream_t);
+              void*, void*, void*, float*, int, int, int, hipStream_t, void*, float*);
 void rn_softmax_fwd(const void*, void*, int, int, float, hipStream_t);
 void rn_softmax_bwd(const void*, const void*, void*, int, int, float, hipStream_t);
 void rn_xent_fwd(void*, const int64_t*, float*, float*, int, int, int, long, int, hipStream_t);
@@ -553,7 +553,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> layernorm_fwd_q8(const Tensor
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optional<Tensor>& gh, const Tensor& h,
                                                  const Tensor& w, const Tensor& mean, const Tensor& rstd,
                                                  const optional<Tensor>& dw_accum, const optional<Tensor>& db_accum,
-                                                 const optional<Tensor>& dxs_accum) {
+                                                 const optional<Tensor>& dxs_accum, const optional<Tensor>& q8,
+                                                 const optional<Tensor>& q8_state) {
     CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(h); GUARD(dy);
     if (dxs_accum && dxs_accum->defined()) {
         CHECK_BF16(*dxs_accum);
@@ -565,11 +566,22 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const optiona
     Tensor dw = accum ? *dw_accum : at::empty({E}, w.options());  // parameter dtype (bf16)
     Tensor db = accum ? *db_accum : at::empty({E}, w.options());
     Tensor part = at::empty({rn_ln_bwd_ws(M, E)}, dy.options().dtype(at::kFloat));
+    // q8 + q8_state: dx also in e5m2 for the fp8 linear that produced the LayerNorm input (its gradient slot)
+    void* q8_ptr = nullptr;
+    float* q8_st = nullptr;
+    if (q8 && q8->defined()) {
+        TORCH_CHECK(q8->scalar_type() == at::kByte && q8->is_contiguous() && q8->numel() == dy.numel() &&
+                    q8->device() == dy.device(), "layernorm_bwd: q8 must be a contiguous uint8 twin of dy");
+        TORCH_CHECK(q8_state && q8_state->defined() && q8_state->scalar_type() == at::kFloat && q8_state->numel() >= 4 &&
+                    q8_state->device() == dy.device(), "layernorm_bwd: q8 needs a 4-float fp32 scale slot");
+        q8_ptr = q8->data_ptr();
+        q8_st = q8_state->data_ptr<float>();
+    }
     if (M) {
         int rc = rn_ln_bwd(dy.data_ptr(), optr(gh), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), dx.data_ptr(), nullptr, nullptr, dw.data_ptr(), db.data_ptr(),
                            (dxs_accum && dxs_accum->defined()) ? dxs_accum->data_ptr() : nullptr,
-                           part.data_ptr<float>(), M, E, accum, cur_stream());
+                           part.data_ptr<float>(), M, E, accum, cur_stream(), q8_ptr, q8_st);
         TORCH_CHECK(rc == 0, "layernorm_bwd: unsupported E=", E);
     } else if (!accum) { dw.zero_(); db.zero_(); }
     return {dx, dw, db};
@@ -1277,7 +1289,8 @@ TORCH_LIBRARY(replicann, m) {
     m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("layernorm_fwd_q8(Tensor x, Tensor? r, Tensor w, Tensor? b, float eps, Tensor(a!) state) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd(Tensor dy, Tensor? gh, Tensor h, Tensor w, Tensor mean, Tensor rstd, "
-          "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None, Tensor(c!)? dxs_accum=None) -> (Tensor, Tensor, Tensor)");
+          "Tensor(a!)? dw_accum=None, Tensor(b!)? db_accum=None, Tensor(c!)? dxs_accum=None, Tensor(d!)? q8=None, "
+          "Tensor(e!)? q8_state=None) -> (Tensor, Tensor, Tensor)");
     m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor? wpe) -> Tensor");
     m.def("vit_join_fwd(Tensor patch, Tensor cls, Tensor pos) -> Tensor");
     m.def("vit_join_bwd(Tensor dx, Tensor(a!) gcls, Tensor(b!) gpos) -> Tensor");

@@ -139,11 +139,15 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const bf16* __restrict__ x, cons
 // Σdx (DXS) is the bias gradient of the linear layer whose output fed this
 // LayerNorm (x = x_prev + a·Wᵀ + b ⇒ db = Σ_rows dx): computed here for free
 // instead of a separate pass over dx.
-template <int NV, bool GH, bool DXS>
+// Q8: dx also as e5m2 with the delayed scale q8st[0] (rolled by the host) — the bytes the consumer's delayed
+// quantisation pass would write from the stored bf16 dx — and amax(|dx|) recorded into q8st[1] (one atomic per
+// block): the fp8 linear that produced this LayerNorm's input takes its dY operand from here
+template <int NV, bool GH, bool DXS, bool Q8 = false>
 __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ gh,
                                                 const bf16* __restrict__ h, const bf16* __restrict__ w,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                bf16* __restrict__ dx, float* __restrict__ part, int M, int E) {
+                                                bf16* __restrict__ dx, float* __restrict__ part, int M, int E,
+                                                uint8_t* __restrict__ q8 = nullptr, float* __restrict__ q8st = nullptr) {
     constexpr int Q = DXS ? 3 : 2;
     __shared__ float red[3][NV * 512];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -179,6 +183,8 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
             }
         }
     };
+    [[maybe_unused]] const float q8inv = Q8 ? 1.f / q8st[0] : 1.f;
+    [[maybe_unused]] float q8m = 0.f;
     if (wave < M) fetch(wave);
     for (int row = wave; row < M; row += nwaves) {
         const float mu = mun, rs = rsn;
@@ -225,12 +231,36 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const bf16* __restrict__ dy, con
                     for (int j = 0; j < 8; ++j) o[j] += (float)ghv[i][j];
                 }
                 store8(dx + (long)row * E + c * 8, o);
+                if constexpr (Q8) {
+                    constexpr float LIM = 57344.f;
+                    float f[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float v = (float)(bf16)o[j];
+                        q8m = fmaxf(q8m, fabsf(v));
+                        f[j] = fminf(fmaxf(v * q8inv, -LIM), LIM);
+                    }
+                    int w0 = 0, w1 = 0;
+                    w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], w0, false);
+                    w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w0, true);
+                    w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], w1, false);
+                    w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], w1, true);
+                    *reinterpret_cast<int2*>(q8 + (long)row * E + c * 8) = make_int2(w0, w1);
+                }
                 if constexpr (DXS) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) acc[Q - 1][i][j] += (float)(bf16)o[j];  // Σ of the stored dx
                 }
             }
         }
+    }
+    if constexpr (Q8) {  // block amax → one atomic (max is order-independent: bitwise repeatable)
+        __shared__ float qm[4];
+        q8m = wave_max(q8m);
+        if (lane == 0) qm[wv] = q8m;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<int*>(q8st + 1), __float_as_int(fmaxf(fmaxf(qm[0], qm[1]), fmaxf(qm[2], qm[3]))));
     }
     // fold the 4 waves: waves 1..3 park their partials in LDS, wave 0 adds (fixed order)
 #pragma unroll
@@ -322,16 +352,20 @@ long rn_ln_bwd_ws(int M, int E) { return 3L * (rn_ln_bwd_blocks(M) + RN_COLRED_S
 // ws: rn_ln_bwd_ws(M, E) floats.  dw/db (fp32) and dw16/db16 (bf16) outputs, any may be null.
 // dxs16 (optional, bf16, always accumulated into): Σ_rows dx — the bias gradient of the layer
 // that produced this LayerNorm's input.
+void rn_fp8_roll_bf8(float* state, hipStream_t st);  // fp8.hip
+// q8 / q8st (optional): dx also in e5m2 with the consumer's delayed scale (q8st rolled here), see ln_bwd_k
 int rn_ln_bwd(const void* dy, const void* gh, const void* h, const void* w, const float* mean, const float* rstd,
               void* dx, float* dw, float* db, void* dw16, void* db16, void* dxs16, float* ws, int M, int E,
-              int accum, hipStream_t st) {
+              int accum, hipStream_t st, void* q8, float* q8st) {
     if (E % 8 != 0 || E > 8192) return -1;
     const int nv = rn_ln_nv(E);
     const int B = rn_ln_bwd_blocks(M);
     const int Q = dxs16 ? 3 : 2;
     float* part = ws;
     float* tmp = ws + (long)B * Q * E;
-#define RN_LNB(NV, G, D) ln_bwd_k<NV, G, D><<<B, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, E)
+    if (q8) rn_fp8_roll_bf8(q8st, st);
+#define RN_LNB(NV, G, D) do { if (q8) ln_bwd_k<NV, G, D, true><<<B, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, E, (uint8_t*)q8, q8st); \
+                           else ln_bwd_k<NV, G, D><<<B, 256, 0, st>>>((const bf16*)dy, (const bf16*)gh, (const bf16*)h, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, E); } while (0)
 #define RN_LNB2(NV) { if (gh) { if (dxs16) RN_LNB(NV, true, true); else RN_LNB(NV, true, false); } \
                       else { if (dxs16) RN_LNB(NV, false, true); else RN_LNB(NV, false, false); } }
     if (nv <= 1) RN_LNB2(1) else if (nv <= 2) RN_LNB2(2) else if (nv <= 4) RN_LNB2(4) else if (nv <= 8) RN_LNB2(8)

@@ -91,9 +91,9 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(n))
         self.eps = eps
 
-    def forward(self, x, return_sum=False, producer_bias=None, fp8=None):
+    def forward(self, x, return_sum=False, producer_bias=None, fp8=None, producer_fp8=None):
         return ops.layer_norm(x, self.weight, self.bias, self.eps, return_sum=return_sum,
-                              producer_bias=producer_bias, fp8=fp8)
+                              producer_bias=producer_bias, fp8=fp8, producer_fp8=producer_fp8)
 
 
 class Attention(nn.Module):
@@ -108,6 +108,10 @@ class Attention(nn.Module):
     def out_bias(self):
         """Bias whose gradient equals Σ_rows of the block output's gradient (None if dropout intervenes)."""
         return self.c_proj.bias if not (self.resid_dropout > 0 and self.training) else None
+
+    def out_fp8(self):
+        """fp8 state of the projection whose output IS the block output (None: bf16, or dropout intervenes)."""
+        return self.c_proj.fp8_state if self.out_bias() is not None else None
 
     def forward(self, h, residual, cache=None, layer=0):
         """``cache``: a :class:`KVCache` (inference) — this call's keys / values are appended at the
@@ -151,6 +155,9 @@ class MLP(nn.Module):
 
     def out_bias(self):
         return self.c_proj.bias if not (self.dropout > 0 and self.training) else None
+
+    def out_fp8(self):
+        return self.c_proj.fp8_state if self.out_bias() is not None else None
 
     def forward(self, h, residual):
         if self.dropout > 0 and self.training:
@@ -230,13 +237,18 @@ class PreLNBlock(nn.Module):
     def out_bias(self):
         return self.mlp.out_bias()
 
-    def forward(self, x, prev_bias=None, cache=None, layer=0):
-        """``prev_bias``: out_bias() of the block that produced x (its gradient is
-        then reduced inside ln_1's backward kernel).  ``cache`` / ``layer``: incremental
-        decoding (see :class:`KVCache`)."""
+    def out_fp8(self):
+        return self.mlp.out_fp8()
+
+    def forward(self, x, prev_bias=None, cache=None, layer=0, prev_fp8=None):
+        """``prev_bias`` / ``prev_fp8``: out_bias() / out_fp8() of the block that produced x (its bias gradient is
+        then reduced inside ln_1's backward kernel, and an fp8 projection takes its e5m2 dY from there).
+        ``cache`` / ``layer``: incremental decoding (see :class:`KVCache`)."""
         # fp8 blocks: the LayerNorms also emit the e4m3 input of c_attn / c_fc
-        h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias, fp8=self.attn.c_attn.fp8_state)
+        h, x = self.ln_1(x, return_sum=True, producer_bias=prev_bias, fp8=self.attn.c_attn.fp8_state,
+                         producer_fp8=prev_fp8)
         x = self.attn(h, residual=x, cache=cache, layer=layer)
-        h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias(), fp8=self.mlp.c_fc.fp8_state)
+        h, x = self.ln_2(x, return_sum=True, producer_bias=self.attn.out_bias(), fp8=self.mlp.c_fc.fp8_state,
+                         producer_fp8=self.attn.out_fp8())
         x = self.mlp(h, residual=x)
         return x

@@ -113,11 +113,11 @@ class GPT2(nn.Module):
         x = ops.embedding(idx, self.wte, self.wpe)
         if self.config.dropout > 0 and self.training:
             x = ops.dropout(x, self.config.dropout, True)
-        prev = None
+        prev = prev8 = None
         for blk in self.h:
-            x = blk(x, prev)
-            prev = blk.out_bias()
-        return self.ln_f(x, producer_bias=prev, fp8=fp8_head)
+            x = blk(x, prev, prev_fp8=prev8)
+            prev, prev8 = blk.out_bias(), blk.out_fp8()
+        return self.ln_f(x, producer_bias=prev, fp8=fp8_head, producer_fp8=prev8)
 
     def forward(self, idx, targets=None):
         """idx (B, T) → logits (B, T, vocab_pad) [, mean CE loss when targets given].

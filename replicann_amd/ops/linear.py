@@ -366,6 +366,7 @@ class _MLPFn(torch.autograd.Function):
             h, sv1 = fp8_forward(x2, w1, b1, None, ACT_NONE, None, fp8[0], keep=True)
             slot = fp8[1].roll_slot(0)
             fp8[1].offer(h, ops.gelu_q8(h, slot), slot)
+            fp8[1].bwd_plan = (True, True)  # the fused backward takes dY in e5m2 (a producer may offer it)
             y, sv2 = fp8_forward(h, w2, b2, res2, ACT_NONE, None, fp8[1], keep=True)
             ctx.x8 = (sv1, sv2)
             ctx.pre_is_h = True

@@ -18,6 +18,12 @@ import torch.nn.functional as F
 
 from .. import _ext
 
+import os
+
+# the fp8 linear that produced a LayerNorm's input takes its e5m2 dY from the LayerNorm backward kernel
+# (_LayerNormFn, producer_fp8); 0: its own quantisation pass (A/B)
+FP8_LN_Q8 = os.environ.get("REPLICANN_FP8_LN_Q8", "1") == "1"
+
 
 class _LayerNormFn(torch.autograd.Function):
     """y = LN(x [+ residual]).
@@ -32,10 +38,15 @@ class _LayerNormFn(torch.autograd.Function):
     a·Wᵀ + b).  Its gradient Σ_rows dx is then produced by this backward kernel
     for free and accumulated straight into the flat gradient buffer; the
     linear's backward sees ``_rn_bias_done`` and skips its own bias pass.
+
+    ``producer_fp8``: the :class:`~replicann_amd.ops.fp8.Fp8State` of that linear when it is an fp8 layer whose
+    backward takes dY in e5m2 (``bwd_plan``): the backward kernel then also writes dx in e5m2 with that layer's
+    delayed gradient scale and offers it (``Fp8State.goffer``), so the linear needs no quantisation pass over
+    its dY (``REPLICANN_FP8_LN_Q8``).
     """
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual, two_out, producer_bias, fp8=None):
+    def forward(ctx, x, weight, bias, eps, residual, two_out, producer_bias, fp8=None, producer_fp8=None):
         shp = x.shape
         E = shp[-1]
         x2 = x.reshape(-1, E).contiguous()
@@ -51,6 +62,7 @@ class _LayerNormFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)  # an unused second output → gh None → no zero-tensor read
         ctx.bias_ref = bias
         ctx.producer_bias = producer_bias if residual is None else None
+        ctx.producer_fp8 = producer_fp8 if residual is None else None
         ctx.has_res = residual is not None
         ctx.has_bias = bias is not None
         ctx.shp = shp
@@ -75,8 +87,18 @@ class _LayerNormFn(torch.autograd.Function):
         direct = dw_acc is not None and db_acc is not None
         pb = ctx.producer_bias
         pb_acc = _direct_grad(pb) if (pb is not None and direct) else None
+        # the producing fp8 linear's dY in e5m2 from this kernel (its delayed gradient scale seeded, and its
+        # backward planned in fp8)
+        pf = ctx.producer_fp8
+        q8 = slot = None
+        if (pf is not None and FP8_LN_Q8 and pf.g_ready and any(pf.bwd_plan) and pf.gt is not None
+                and pf.gt.device == gy2.device):
+            slot = pf.gslot(gy2.device)
+            q8 = torch.empty(gy2.shape, dtype=torch.uint8, device=gy2.device)
         dx, dw, db = _ext.ops().layernorm_bwd(gy2, gh2, h, weight, mean, rstd, dw_acc if direct else None,
-                                              db_acc if direct else None, pb_acc)
+                                              db_acc if direct else None, pb_acc, q8, slot)
+        if q8 is not None:
+            pf.goffer(dx, q8)
         dx = dx.reshape(ctx.shp)
         if pb_acc is not None:
             pb._rn_bias_done = True  # consumed (and reset) by the producer linear's backward
@@ -85,16 +107,18 @@ class _LayerNormFn(torch.autograd.Function):
         if direct:  # gradients already accumulated in the flat buffer
             _notify(weight)
             _notify(bias)
-            return dx, None, None, None, g_res, None, None, None
-        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None, g_res, None, None, None)
+            return dx, None, None, None, g_res, None, None, None, None
+        return (dx, dw.to(weight.dtype), db.to(weight.dtype) if ctx.has_bias else None, None, g_res, None, None, None,
+                None)
 
 
-def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, producer_bias=None, fp8=None):
+def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, producer_bias=None, fp8=None,
+               producer_fp8=None):
     """LayerNorm over the last dim.  With ``residual``: h = x + residual, y = LN(h).
 
     Returns y, or (y, h) when ``return_sum`` (h = x when there is no residual;
     use that h as the block's residual so both gradients meet in one kernel).
-    ``producer_bias``: see :class:`_LayerNormFn`.
+    ``producer_bias``, ``producer_fp8``: see :class:`_LayerNormFn`.
     ``fp8``: the :class:`~replicann_amd.ops.fp8.Fp8State` of the fp8 GEMM that consumes y — the
     kernel then also writes y in e4m3 (delayed scaling) and hands it to that GEMM, which skips its
     own quantisation pass.
@@ -102,7 +126,7 @@ def layer_norm(x, weight, bias=None, eps=1e-5, residual=None, return_sum=False, 
     if _ext.use_native(x):
         if fp8 is not None:
             fp8.enter()
-        out = _LayerNormFn.apply(x, weight, bias, eps, residual, return_sum, producer_bias, fp8)
+        out = _LayerNormFn.apply(x, weight, bias, eps, residual, return_sum, producer_bias, fp8, producer_fp8)
         if residual is None and not return_sum:
             return out
         return out if return_sum else out[0]
