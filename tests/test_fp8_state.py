@@ -104,3 +104,25 @@ def test_fp8_dgrad_cpu_emulation_tracks_bf16_grads():
     for n in grads["fp8"]:
         a, b = grads["fp8"][n].float(), grads["bf16"][n].float()
         assert ((a - b).norm() / b.norm().clamp_min(1e-12)) < 0.15, n
+
+
+def test_fp8_head_slots_checkpoint_compat():
+    """The fp8 LM head's slots (GPT2Config.fp8_head) are a state_dict buffer; a checkpoint written without
+    them (bf16 head, or an older fp8 model) loads strictly into a head model with empty slots, and the CPU
+    path ignores the fp8 head (plain fp32 loss)."""
+    from replicann_amd import ops
+    from replicann_amd.ops.fp8 import Fp8State
+
+    m_head = _model(head=1)
+    assert "head8.fp8_scales" in m_head.state_dict()
+    m_plain = _model(head=0)
+    assert "head8.fp8_scales" not in m_plain.state_dict()
+    m_head.load_state_dict(m_plain.state_dict())  # strict: the missing head slots are filled, not an error
+    assert m_head.head8.fp8_state.ready == [False, False]
+    torch.manual_seed(2)
+    h = torch.randn(64, 128)
+    w = torch.randn(1024, 128) * 0.05
+    t = torch.randint(0, 1000, (64,))
+    a = ops.linear_cross_entropy(h, w, t, n_valid_cols=1000, fp8=Fp8State())
+    b = ops.linear_cross_entropy(h, w, t, n_valid_cols=1000)
+    assert torch.equal(a, b)
