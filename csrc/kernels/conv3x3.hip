@@ -262,16 +262,21 @@ int rn_conv3x3(const void* in, const void* w, void* out, float* part, int N, int
     a.N = N; a.H = H; a.W = W; a.TR = conv3x3_rows(H, W, &fm); a.waves = a.TR * W / (16 * fm); a.tiles = tiles;
     a.accumulate = accumulate; a.dgrad = dgrad;
     const size_t lds = conv3x3_lds(a.TR, W, fm);
-    static int attr_dev = -1;
+    // the >64 KiB dynamic-LDS opt-in is per device (a process may drive several GPUs): once per device
+    static uint64_t attr_devs = 0;
+    static int cu_count[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (attr_dev != dev) {
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(attr_devs & bit)) {
         (void)hipFuncSetAttribute((const void*)conv3x3_k<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)conv3x3_k<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_dev = dev;
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        cu_count[dev & 63] = cus > 0 ? cus : 256;
+        attr_devs |= bit;
     }
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus = cu_count[dev & 63];
     const int grid = tiles < cus ? tiles : cus;
     if (fm == 4) conv3x3_k<4><<<grid, a.waves * 64, lds, st>>>(a);
     else conv3x3_k<2><<<grid, a.waves * 64, lds, st>>>(a);
