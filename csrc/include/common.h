@@ -305,16 +305,11 @@ __global__ void __launch_bounds__(1024) rn_colsum1_k(const float* __restrict__ i
     if (out.o16[k]) out.o16[k][o] = (__bf16)(acc + (out.accum[k] ? (float)out.o16[k][o] : 0.f));
 }
 
-static inline bool rn_colsum1_on() {
-    static const bool on = [] { const char* e = std::getenv("REPLICANN_COLSUM_1PASS"); return !(e && e[0] == '0'); }();
-    return on;
-}
-
 // Segmented column reduction: out.seg columns per output segment (≤ 3 segments).
 // tmp must hold RN_COLRED_S * C floats.
 static inline void rn_colreduce_seg(const float* in, int R, int C, float* tmp, const RnColOut& out,
                                     hipStream_t st) {
-    if (R <= RN_COLSUM1_R && rn_colsum1_on()) {
+    if (R <= RN_COLSUM1_R) {
         rn_colsum1_k<<<(C + 63) / 64, 1024, 0, st>>>(in, R, C, out);
         return;
     }

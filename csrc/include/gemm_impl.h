@@ -886,8 +886,7 @@ __global__ void __launch_bounds__(256) splitk_group_k(float* __restrict__ ws, lo
 // Sum split-K slabs (fixed order) + epilogue.  4 consecutive columns per thread.
 // BATCH: the slab loads are issued 4 at a time before their (in-order) adds, so a thread has 4
 // loads in flight instead of one dependent load per slab — same summation order, same bits
-// (REPLICANN_SPLITK_BATCH=0 restores the one-at-a-time loop, A/B).
-template <int ACT, bool BATCH = true>
+template <int ACT>
 __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
     const long total4 = ((long)p.M * p.N + 3) / 4;
     const float ra = p.reduce_alpha ? *p.reduce_alpha : 1.f;
@@ -898,15 +897,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
         const bool vec = (p.N % 4 == 0);
         const long step = p.slab_step > 1 ? (long)p.slab_step * MN : MN;
         int s0 = 0;
-        if constexpr (BATCH) {
-            if (vec) {
-                for (; s0 + 4 <= p.split; s0 += 4) {
-                    float4 t[4];
+        if (vec) {
+            for (; s0 + 4 <= p.split; s0 += 4) {
+                float4 t[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(p.ws + (s0 + u) * step + e0);
+                for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(p.ws + (s0 + u) * step + e0);
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) { v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w; }
-                }
+                for (int u = 0; u < 4; ++u) { v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w; }
             }
         }
         for (int s = s0; s < p.split; ++s) {
@@ -937,11 +934,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_k(GemmArgs p) {
             }
         }
     }
-}
-
-inline bool splitk_batch() {
-    static const bool on = [] { const char* e = std::getenv("REPLICANN_SPLITK_BATCH"); return !(e && e[0] == '0'); }();
-    return on;
 }
 
 // true the first time `mask`'s owner launches on the current device (the >64 KiB LDS opt-in
@@ -980,11 +972,9 @@ void launch_t(GemmArgs& a, hipStream_t st) {
             GemmArgs r = a;
             r.split = (a.split + per - 1) / per;
             r.slab_step = per;
-            if (splitk_batch()) splitk_reduce_k<ACT, true><<<g, 256, 0, st>>>(r);
-            else splitk_reduce_k<ACT, false><<<g, 256, 0, st>>>(r);
+            splitk_reduce_k<ACT><<<g, 256, 0, st>>>(r);
         } else {
-            if (splitk_batch()) splitk_reduce_k<ACT, true><<<g, 256, 0, st>>>(a);
-            else splitk_reduce_k<ACT, false><<<g, 256, 0, st>>>(a);
+            splitk_reduce_k<ACT><<<g, 256, 0, st>>>(a);
         }
     } else {
         kmain<<<tiles, NT, lds, st>>>(a);

@@ -924,15 +924,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
 extern "C" int* rn_gemm_sched_slot(int dev, hipStream_t st);
 extern "C" int rn_gemm_get_reserve();
 namespace rn_gemm_detail {
-// non-temporal output stores: plain bf16 outputs over 1 GiB (REPLICANN_GEMM_ST_NT=0 disables;
-// REPLICANN_GEMM_ST_NT_MB moves the size threshold; 256 MiB also caught outputs the next kernel reads
-// at once, +0.14-0.4 ms per GPT-2-small step, profiles/r3s_resume_xent_gelu.txt item 17)
+// non-temporal output stores: plain bf16 outputs over 1 GiB (a 256 MiB threshold also caught outputs
+// the next kernel reads at once, +0.14-0.4 ms per GPT-2-small step, profiles/r3s_resume_xent_gelu.txt
+// item 17)
 // (a non-temporal store of the activation epilogue's second output, read only by the backward, was
 // measured as no change and removed in round 4)
 inline int rn_gemm_st_nt(const GemmArgs& a) {
-    static const bool on = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT"); return !(e && e[0] == '0'); }();
-    static const long thr = [] { const char* e = std::getenv("REPLICANN_GEMM_ST_NT_MB"); return (e ? std::atol(e) : 1024L) << 20; }();
-    return (on && a.split <= 1 && (long)a.M * a.N * 2 > thr) ? 1 : 0;
+    return (a.split <= 1 && (long)a.M * a.N * 2 > (1024L << 20)) ? 1 : 0;
 }
 }  // namespace rn_gemm_detail
 namespace rn_gemm_detail {

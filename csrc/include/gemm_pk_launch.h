@@ -53,8 +53,7 @@ inline void pk_splitk_reduce(GemmArgs& a, int act, hipStream_t st) {
         case ACT_MUL_BWD: splitk_reduce_k<ACT_MUL_BWD><<<g, 256, 0, st>>>(a); break;
         case ACT_RELU_BWD: splitk_reduce_k<ACT_RELU_BWD><<<g, 256, 0, st>>>(a); break;
         default:
-            if (splitk_batch()) splitk_reduce_k<ACT_NONE, true><<<g, 256, 0, st>>>(a);
-            else splitk_reduce_k<ACT_NONE, false><<<g, 256, 0, st>>>(a);
+            splitk_reduce_k<ACT_NONE><<<g, 256, 0, st>>>(a);
             break;
     }
 }

@@ -320,8 +320,8 @@ __global__ void opt_prep_k(float* __restrict__ st, float base_lr, float warmup, 
 }
 
 inline int grid_for(long work) {
-    // REPLICANN_OPT_BLOCKS: grid cap of the optimizer / embedding streaming kernels (A/B; default 4096)
-    static const long cap = [] { const char* e = std::getenv("REPLICANN_OPT_BLOCKS"); return e ? std::atol(e) : 4096L; }();
+    // grid cap of the optimizer / embedding streaming kernels (grid-stride loops past it)
+    constexpr long cap = 4096L;
     long g = (work + 255) / 256;
     return (int)(g < cap ? (g > 0 ? g : 1) : cap);
 }

@@ -74,21 +74,10 @@ __global__ void __launch_bounds__(256) quant_k(const bf16* __restrict__ x, long 
 // Delayed scaling (one pass over x): the scale comes from the amax recorded by the PREVIOUS
 // quantisation of this tensor (x2 headroom), and this pass records the current amax for the
 // next one.  state: [0] scale used, [1] amax of the last pass, [2] amax the scale came from.
-// delayed-scaling headroom: scale = pow2_ceil(hr · previous amax / max); REPLICANN_FP8_HEADROOM (e4m3
-// activations / weights) and REPLICANN_FP8_GHEADROOM (e5m2 gradients), default 2 (A/B)
-static float fp8_env_hr(const char* name) {
-    const char* e = std::getenv(name);
-    const float v = e ? (float)std::atof(e) : 2.f;
-    return v > 0.f ? v : 2.f;
-}
-static float fp8_hr() {
-    static const float v = fp8_env_hr("REPLICANN_FP8_HEADROOM");
-    return v;
-}
-static float fp8_ghr() {
-    static const float v = fp8_env_hr("REPLICANN_FP8_GHEADROOM");
-    return v;
-}
+// delayed-scaling headroom: scale = pow2_ceil(2 · previous amax / max) for the e4m3 (activations,
+// weights) and e5m2 (gradients) slots (headroom 4 / 8 measured in round 5: profiles/fp8_headroom_proj_r5x.txt)
+static float fp8_hr() { return 2.f; }
+static float fp8_ghr() { return 2.f; }
 __device__ inline void fp8_roll_k_body(float* __restrict__ state, float hr) {
     const float a = state[1];
     state[2] = a;

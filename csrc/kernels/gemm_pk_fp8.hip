@@ -21,7 +21,7 @@ void rn_gemm_launch_pk_fp8_wgrad(GemmArgs& a, int a_bf8, hipStream_t st) {
     else launch_pk_t<false, false, ACT_NONE, true, true, 0, 1>(a, st);
     const long total4 = ((long)a.M * a.N + 3) / 4;
     const int g = (int)std::min<long>((total4 + 255) / 256, 4096);
-    splitk_reduce_k<ACT_NONE, true><<<g, 256, 0, st>>>(a);
+    splitk_reduce_k<ACT_NONE><<<g, 256, 0, st>>>(a);
 }
 
 // fp8 data gradient dX = dY·W: A = dY [M][K] (e5m2 if a_bf8, else e4m3; K-contiguous, as produced),

@@ -331,16 +331,10 @@ int rn_ln_fwd(const void* x, const void* r, const void* w, const void* b, void* 
     return 0;
 }
 
-// waves of the backward grid (each loops over rows with a one-row prefetch); REPLICANN_LN_BWD_WAVES
-// overrides (A/B).  2048 (8 per CU): with the prefetch this keeps HBM as busy as 8192 did and writes
+// waves of the backward grid (each loops over rows with a one-row prefetch): 2048 (8 per CU): with the prefetch this keeps HBM as busy as 8192 did and writes
 // 4x fewer column-partial rows for the reduction that follows (GPT-2-small step -0.3 ms, call gpu_r3zn)
 int rn_ln_bwd_blocks(int M) {
-    static int cap = -1;
-    if (cap < 0) {
-        const char* e = std::getenv("REPLICANN_LN_BWD_WAVES");
-        cap = e ? std::atoi(e) : 2048;
-        if (cap < 4) cap = 4;
-    }
+    constexpr int cap = 2048;
     int W = M < cap ? M : cap;
     return (W + 3) / 4;
 }

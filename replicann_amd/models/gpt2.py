@@ -43,17 +43,24 @@ class GPT2Config:
     # round 5 call V: with the fp8 LM head 131.5 vs 133.6 ms/step, and over steps 40-49 of the 50-step trajectory the
     # loss stays within 0.5 % of bf16 (held-out loss 0.24 % behind, against 1.4 % with this projection in bf16); the
     # early descent (steps 6-9) deviates up to 8 % (profiles/gpt2m_fp8_proj_r5v.txt).  REPLICANN_FP8_PROJ=0: bf16
-    fp8_proj: bool = os.environ.get("REPLICANN_FP8_PROJ", "1") == "1"
+    # (None: resolved from the environment when the config is built, not at import time)
+    fp8_proj: bool | None = None
     # fp8 LM head (fp8 models, training steps only; ops.loss._LinearXentFp8Fn): 1 = logits from e4m3 h · e4m3
     # wte, the loss gradient straight to e5m2 by the cross-entropy kernel, both head gradients on the fp8 GEMMs;
     # 2 = the same gradients with the logits GEMM kept in bf16 (the loss itself unquantised); 0 = bf16 head.
     # Default 1: GPT-2-medium-fp8 132.0 ms/step against 139.9 (bf16 head) and 166.0 (bf16) on one box; the
     # held-out loss after 50 steps is within 1.4 % of the bf16 model's (1.1 % with the bf16 head)
     # (profiles/gpt2m_fp8_head_r5op.txt)
-    fp8_head: int = int(os.environ.get("REPLICANN_FP8_HEAD", "1"))
+    fp8_head: int | None = None
     # LM head + loss over row chunks of this many tokens (0: the whole batch at once).  Bounds the
     # logits buffer (rows x vocab_pad bf16: 6.6 GB at b64 x 1024) for long sequences / big batches
     ce_chunk: int = 0
+
+    def __post_init__(self):
+        if self.fp8_proj is None:
+            object.__setattr__(self, "fp8_proj", os.environ.get("REPLICANN_FP8_PROJ", "1") == "1")
+        if self.fp8_head is None:
+            object.__setattr__(self, "fp8_head", int(os.environ.get("REPLICANN_FP8_HEAD", "1")))
 
     @staticmethod
     def small(**kw):
@@ -100,6 +107,16 @@ class GPT2(nn.Module):
         # the fp8 LM head's scale slots (the weight is wte); absent unless fp8 and fp8_head
         self.head8 = Fp8Slots() if (cfg.fp8 and cfg.fp8_head > 0) else None
 
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        # a checkpoint of an fp8-head model loads into a model without the head's slots (fp8_head=0, a bf16
+        # model): the slots are simply not needed — not an unexpected-key error
+        if self.head8 is None:
+            for k in [k for k in state_dict if k.startswith(prefix + "head8.")]:
+                state_dict.pop(k)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+
     def num_params(self, non_embedding=False):
         n = sum(p.numel() for p in self.parameters())
         n -= (self.wte.shape[0] - self.config.vocab_size) * self.config.n_embd  # zero pad rows
@@ -126,6 +143,14 @@ class GPT2(nn.Module):
         """
         fp8h = (self.head8.fp8_state if self.head8 is not None and targets is not None and self.training
                 and torch.is_grad_enabled() and self.wte.is_cuda else None)
+        if fp8h is not None:
+            # decide here whether the fp8 head will run: otherwise ln_f would write (and roll the slot for) an
+            # e4m3 copy nobody consumes (chunked head, or shapes the fp8 head does not take)
+            rows = idx.numel()
+            chunk = self.config.ce_chunk
+            if (chunk and chunk < rows) or not ops.loss.fp8_head_ok(idx.new_empty((rows, self.config.n_embd),
+                                                                                   device="meta"), self.wte):
+                fp8h = None
         h = self.hidden(idx, fp8h)
         if targets is None:
             return ops.linear(h, self.wte)[..., : self.config.vocab_size]

@@ -22,7 +22,6 @@ Supported semantics (all needed for reference parity, SURVEY.md §2.1 Q1–Q4):
 
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -123,8 +122,9 @@ def attention(q, k, v, *, scale=None, causal=False, bias=None, mask=None, dropou
     return attention_reference(q, k, v, scale, causal, bias, p, training)
 
 
-# the attention backward's e5m2 dQKV for an fp8 QKV projection (REPLICANN_FP8_ATTN_Q8=0: off, A/B)
-ATTN_Q8 = os.environ.get("REPLICANN_FP8_ATTN_Q8", "1") == "1"
+# the attention backward's e5m2 dQKV for an fp8 QKV projection (a test hook, not an env knob: the tests
+# compare it with the path where c_attn quantises a bf16 dQKV itself)
+ATTN_Q8 = True
 
 
 class _AttnPackedFn(torch.autograd.Function):

@@ -32,8 +32,13 @@ from .. import _ext
 from .linear import _direct_grad, _notify, gemm
 
 
+# BatchNorm statistics reduced by the producing conv's epilogue (a test hook, not an env knob:
+# tests/test_ops_gpu.py compares it with the BN's own statistics pass)
+BN_FUSED_STATS = True
+
+
 def _fused_bn_stats():
-    return os.environ.get("REPLICANN_BN_FUSED_STATS", "1") != "0"
+    return BN_FUSED_STATS
 
 
 class GradJoin:

@@ -34,9 +34,11 @@ E5M2_MAX = 57344.0
 FP8_WGRAD = os.environ.get("REPLICANN_FP8_WGRAD", "1") == "1"
 FP8_DGRAD = os.environ.get("REPLICANN_FP8_DGRAD", "1") == "1"
 # fp8 MLP backward with both layers' fp8 gradients: the MLP c_proj data gradient on the fp8 GEMM and the
-# GELU backward fused into the e5m2 quantisation of dH (ops.linear._MLPFn._fp8_backward); 0: the bf16
-# c_proj dgrad with the multiply in its epilogue + a separate e5m2 pass (A/B)
-FP8_MLP_FUSE = os.environ.get("REPLICANN_FP8_MLP_FUSE", "1") == "1"
+# GELU backward fused into the e5m2 quantisation of dH (ops.linear._MLPFn._fp8_backward).  The unfused
+# path (bf16 c_proj dgrad with the multiply in its epilogue + a separate e5m2 pass) still serves the
+# shapes the fused one does not take; tests flip this module attribute to compare the two (no env knob:
+# the fused path won in round 5, profiles/gpt2m_fp8_r5g.txt).
+FP8_MLP_FUSE = True
 
 
 def pow2_ceil(s):
@@ -49,6 +51,13 @@ def pow2_ceil(s):
     m, e = torch.frexp(s)  # s = m · 2^e, m in [0.5, 1)
     e = torch.where(m == 0.5, e - 1, e)
     return torch.ldexp(torch.tensor(1.0), e).float()
+
+
+def _pow2_ceil_pos(s):
+    """Element-wise pow2_ceil of the positive entries of a scale tensor (others unchanged)."""
+    m, e = torch.frexp(s)
+    e = torch.where(m == 0.5, e - 1, e)
+    return torch.where(s > 0, torch.ldexp(torch.ones_like(s), e), s)
 
 
 def quantize_fp8(x):
@@ -198,10 +207,20 @@ class Fp8State:
             self._gt = value
 
     def sync_ready(self):
-        """ready[i] = slot i holds a scale (host sync: call at load time, never inside a step)."""
+        """ready[i] = slot i holds a scale (host sync: call at load time, never inside a step).
+
+        Loaded scales are also rounded up to powers of two: the one-wave-per-SIMD fp8 GEMM feeds only
+        the exponent byte of a scale to the scaled MFMA, so a checkpoint written before every quantiser
+        rounded its scale up (2·amax/448, any mantissa) would otherwise run its first resumed step with
+        every tensor silently scaled by 2^floor(log2 s)/s.  Power-of-two scales
+        (every checkpoint since) are unchanged, so bit-exact resume holds."""
         t = self.t
+        if t is not None:
+            t[:, 0] = _pow2_ceil_pos(t[:, 0])
         self.ready = [bool(t is not None and float(t[i, 0]) > 0) for i in range(2)]
         g = self.gt
+        if g is not None:
+            g[:, 0] = _pow2_ceil_pos(g[:, 0])
         self.g_ready = bool(g is not None and float(g[0, 0]) > 0)
 
     def gslot(self, device):

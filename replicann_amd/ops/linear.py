@@ -18,7 +18,6 @@ CPU tensors take the plain ATen path (same math, fp32 accumulation).
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 import torch.nn.functional as F
@@ -169,6 +168,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.x8 = None
         if fp8 is not None:
             from .fp8 import fp8_forward
+            fp8.bwd_plan = (False, False)  # re-decided by every forward (a stale plan would skip a bf16 dY)
             if res2 is not None and not res2.is_contiguous():
                 res2 = res2.contiguous()
             if fp8.fp8_bwd and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
@@ -277,12 +277,8 @@ def linear_kv_append(x, weight, bias, kv, pos):
 # --------------------------------------------------------------------------
 ACT_BWD = {ACT_RELU: 3, ACT_GELU: 4}  # GEMM epilogue codes: out = (A·B) ⊙ act'(pre)
 # The MLP's GELU saves gelu'(h) (forward epilogue code 5) and its dgrad multiplies by it (code 6)
-# (REPLICANN_MLP_GELU=pre: save h and re-derive gelu'(h) in the dgrad epilogue — A/B only)
-if os.environ.get("REPLICANN_MLP_GELU", "deriv") == "pre":
-    _MLP_FWD_ACT, _MLP_BWD_ACT = {ACT_RELU: ACT_RELU, ACT_GELU: ACT_GELU}, dict(ACT_BWD)
-else:
-    _MLP_FWD_ACT = {ACT_RELU: ACT_RELU, ACT_GELU: ACT_GELU_D}
-    _MLP_BWD_ACT = {ACT_RELU: 3, ACT_GELU: ACT_MUL_BWD}
+_MLP_FWD_ACT = {ACT_RELU: ACT_RELU, ACT_GELU: ACT_GELU_D}
+_MLP_BWD_ACT = {ACT_RELU: 3, ACT_GELU: ACT_MUL_BWD}
 
 
 def _bias_grad(g2, bias, native):
@@ -357,6 +353,10 @@ class _MLPFn(torch.autograd.Function):
         pre = torch.empty(x2.shape[0], w1.shape[0], device=x.device, dtype=x.dtype)
         ctx.x8 = (None, None)
         ctx.pre_is_h = False
+        if fp8 is not None:  # re-decided by every forward (a stale plan would skip a bf16 dY)
+            for st in fp8:
+                if st is not None:
+                    st.bwd_plan = (False, False)
         if fp8 is not None and _MLPFn._fp8_keep_h(ctx, x2, w1, w2, act, fp8):
             # the all-fp8 MLP (both layers' fp8 gradients, fused backward): c_fc on the one-wave-per-SIMD
             # fp8 GEMM writes h = x·W1ᵀ + b1 only, ONE pass makes e4m3(gelu(h)) for the MLP c_proj
@@ -412,8 +412,12 @@ class _MLPFn(torch.autograd.Function):
             return False
         M, N = x2.shape[0], w1.shape[0]
         probe = x2.new_empty((M, N))  # (shape only)
-        return (N % 8 == 0 and fp8_dgrad_ok(probe, w1.shape[1]) and fp8_dgrad_ok(x2.new_empty((M, w2.shape[0])), N)
-                and x2.shape[1] % 16 == 0 and N % 16 == 0)
+        dy_probe = x2.new_empty((M, w2.shape[0]))
+        # both weight gradients must take the fp8 GEMM too (tokens % 128): the bf16 fallback of _wgrad would
+        # read h where it needs gelu(h) (c_proj) and dU where it needs dH (c_fc) — ADVICE r5 (high)
+        return (N % 8 == 0 and fp8_dgrad_ok(probe, w1.shape[1]) and fp8_dgrad_ok(dy_probe, N)
+                and x2.shape[1] % 16 == 0 and N % 16 == 0
+                and fp8_wgrad_ok(probe, x2) and fp8_wgrad_ok(dy_probe, probe))
 
     @staticmethod
     def _fp8_backward(ctx, gy, gy2, x2, w1, pre, u, w2, sv1, sv2):
@@ -427,6 +431,8 @@ class _MLPFn(torch.autograd.Function):
         nig = ctx.needs_input_grad
         if ctx.pre_is_h:  # the forward kept h: this path is the only one that can take it (_fp8_keep_h)
             assert sv1 is not None and sv2 is not None and sv1[0] is not None and sv2[0] is not None
+            # ... and both weight gradients must run on the fp8 GEMM (the bf16 fallback would read h / dU)
+            assert _fp8_wgrad_ok(gy2, sv2[0]) and _fp8_wgrad_ok(u, sv1[0]), "keep-h MLP without fp8 weight gradients"
         elif not (FP8_MLP_FUSE and nig[0] and nig[1] and _MLP_BWD_ACT[ctx.act] == ACT_MUL_BWD and sv1 is not None and sv2 is not None
                 and sv1[0] is not None and sv1[2] is not None and sv2[2] is not None
                 and fp8_dgrad_ok(gy2, w2.shape[1]) and fp8_dgrad_ok(u, w1.shape[1]) and _fp8_wgrad_ok(u, sv1[0])

@@ -18,11 +18,10 @@ import torch.nn.functional as F
 
 from .. import _ext
 
-import os
 
 # the fp8 linear that produced a LayerNorm's input takes its e5m2 dY from the LayerNorm backward kernel
 # (_LayerNormFn, producer_fp8); 0: its own quantisation pass (A/B)
-FP8_LN_Q8 = os.environ.get("REPLICANN_FP8_LN_Q8", "1") == "1"
+FP8_LN_Q8 = True  # (a test hook, not an env knob: tests/test_fp8_ln_q8_gpu.py compares both paths)
 
 
 class _LayerNormFn(torch.autograd.Function):
@@ -42,7 +41,7 @@ class _LayerNormFn(torch.autograd.Function):
     ``producer_fp8``: the :class:`~replicann_amd.ops.fp8.Fp8State` of that linear when it is an fp8 layer whose
     backward takes dY in e5m2 (``bwd_plan``): the backward kernel then also writes dx in e5m2 with that layer's
     delayed gradient scale and offers it (``Fp8State.goffer``), so the linear needs no quantisation pass over
-    its dY (``REPLICANN_FP8_LN_Q8``).
+    its dY (``FP8_LN_Q8``).
     """
 
     @staticmethod

@@ -3,6 +3,7 @@ tree's, the timing-only GEMM ablation kernels stay out of a default build, and t
 tuning tables round-trip into the native autotuner cache."""
 
 import json
+import shutil
 from pathlib import Path
 
 import pytest
@@ -72,3 +73,23 @@ def test_committed_tuning_tables_round_trip():
         table = json.loads(torch.ops.replicann.gemm_tuning_table())
         for e in entries:
             assert e in table
+
+
+@pytest.mark.skipif(not SO.exists() or shutil.which("nm") is None, reason="extension not built / no nm")
+def test_release_library_has_no_ablation_kernels():
+    """The timing-only GEMM ablations (DBG != 0: operand DMA out of range, every tile at (0,0) —
+    WRONG outputs by design) exist only in a REPLICANN_DEV build; a release _C.so must not carry
+    a single instantiation of them."""
+    import re
+    import subprocess
+
+    stamp = SO.with_suffix(".srcstamp")
+    if stamp.exists() and "-DREPLICANN_DEV=1" in stamp.read_text():
+        pytest.skip("developer build")
+    out = subprocess.run(["nm", "-DC", "--defined-only", str(SO)], capture_output=True, text=True, check=True).stdout
+    pk = re.findall(r"gemm_pk<([^>]*)>", out)
+    w1 = re.findall(r"gemm_w1<([^>]*)>", out)
+    assert pk and w1, "expected the production GEMM kernels in the library"
+    # template argument 5 of gemm_pk and 4 of gemm_w1 is DBG
+    assert all(a.split(", ")[5] == "0" for a in pk), sorted({a for a in pk if a.split(", ")[5] != "0"})
+    assert all(a.split(", ")[4] == "0" for a in w1), sorted({a for a in w1 if a.split(", ")[4] != "0"})

@@ -126,3 +126,51 @@ def test_fp8_head_slots_checkpoint_compat():
     a = ops.linear_cross_entropy(h, w, t, n_valid_cols=1000, fp8=Fp8State())
     b = ops.linear_cross_entropy(h, w, t, n_valid_cols=1000)
     assert torch.equal(a, b)
+
+
+def test_fp8_head_checkpoint_loads_into_model_without_head():
+    """the other direction — a checkpoint with the fp8 head's slots loads strictly into a
+    model built with fp8_head=0 (the slots are dropped, not an unexpected-key error)."""
+    m_head = _model(head=1)
+    m_plain = _model(head=0)
+    m_plain.load_state_dict(m_head.state_dict())  # strict
+    for k, v in m_plain.state_dict().items():
+        assert torch.equal(v, m_head.state_dict()[k]), k
+
+
+def test_fp8_config_env_defaults_resolved_at_construction(monkeypatch):
+    """The fp8_head / fp8_proj defaults follow the environment when the config is BUILT (not at import)."""
+    monkeypatch.setenv("REPLICANN_FP8_HEAD", "0")
+    monkeypatch.setenv("REPLICANN_FP8_PROJ", "0")
+    cfg = R.GPT2Config.tiny(fp8=True)
+    assert cfg.fp8_head == 0 and cfg.fp8_proj is False
+    monkeypatch.setenv("REPLICANN_FP8_HEAD", "2")
+    assert R.GPT2Config.tiny(fp8=True).fp8_head == 2
+    assert R.GPT2Config.tiny(fp8=True, fp8_head=1).fp8_head == 1
+
+
+def test_fp8_non_pow2_scales_are_rounded_on_load():
+    """a checkpoint whose slots hold non-power-of-two scales (written before every
+    quantiser rounded up) loads with every positive scale rounded UP to a power of two — the one-wave fp8
+    GEMM feeds only the exponent byte to the scaled MFMA — and power-of-two scales load unchanged."""
+    m = _model()
+    ids = torch.randint(0, 1000, (2, 32))
+    m(ids, ids)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    keys = [k for k in sd if k.endswith("fp8_scales")]
+    pow2 = {k: sd[k].clone() for k in keys}
+    for k in keys:
+        sd[k][:, 0] = sd[k][:, 0] * 0.75  # no longer powers of two
+    m2 = _model()
+    m2.load_state_dict(sd)
+    for k, t in m2.state_dict().items():
+        if k.endswith("fp8_scales"):
+            s = t[:, 0]
+            m_, _ = torch.frexp(s[s > 0])
+            assert torch.all(m_ == 0.5), (k, s)
+            assert torch.all(s >= sd[k][:, 0])  # rounded up, never down (no overflow of the e4m3 range)
+            assert torch.equal(s, pow2[k][:, 0])  # 0.75 · 2^e rounds back to 2^e
+    m3 = _model()
+    m3.load_state_dict(m.state_dict())  # pow2 scales: unchanged, bit for bit
+    for k in keys:
+        assert torch.equal(m3.state_dict()[k], m.state_dict()[k])

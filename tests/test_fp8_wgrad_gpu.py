@@ -270,6 +270,42 @@ def test_fp8_mlp_keep_h_tracks_unfused(cuda, monkeypatch):
         assert abs(x - y) <= 0.02 * abs(y), (a, b)
 
 
+def test_fp8_mlp_ragged_tokens_gradients_match_unfused(cuda, monkeypatch):
+    """with B·T % 128 != 0 the fp8 weight gradients fall back to bf16, so the MLP must not
+    keep h (the bf16 fallback would take c_proj's dW from h instead of gelu(h) and c_fc's from dU instead of
+    dH).  Every step's flat gradient of the fused-default model must match the FP8_MLP_FUSE=False model's."""
+    import replicann_amd as R
+    import replicann_amd.ops.fp8 as F
+    from replicann_amd.optim import FusedAdamW
+    from replicann_amd.utils.flat import FlatParams
+
+    def run(fuse):
+        monkeypatch.setattr(F, "FP8_MLP_FUSE", fuse)
+        torch.manual_seed(0)
+        m = R.GPT2(R.GPT2Config.tiny(fp8=True)).to(cuda)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        for st in F.fp8_states(m):
+            st.wgrad = st.dgrad = True
+        flat = FlatParams(m)
+        opt = FusedAdamW(flat, lr=1e-3)
+        gen = torch.Generator(device=cuda).manual_seed(11)
+        grads = []
+        for _ in range(4):
+            ids = torch.randint(0, 1000, (3, 101), device=cuda, generator=gen)  # 300 tokens: % 128 != 0
+            opt.zero_grad()
+            m(ids[:, :-1], ids[:, 1:]).backward()
+            g = flat.grad.float().clone()
+            assert torch.isfinite(g).all()
+            grads.append(g)
+            opt.step()
+        return grads
+
+    ga, gb = run(True), run(False)
+    for a, b in zip(ga, gb):
+        assert ((a - b).norm() / b.norm()).item() < 0.02
+
+
 def test_fp8_attention_q8_dqkv_tracks_quantise_pass(cuda, monkeypatch):
     """GPT-2 (tiny, fp8, fp8 backward): the attention backward's own e5m2 dQKV (no bf16 dQKV when c_attn
     takes both gradients in fp8) trains like the path that quantises a bf16 dQKV (REPLICANN_FP8_ATTN_Q8=0)."""

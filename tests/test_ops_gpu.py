@@ -1094,9 +1094,10 @@ def test_conv_bn_direct_grad_accumulation(cuda):
 @pytest.mark.parametrize("N,HW,C,OC", [(3, 15, 64, 128), (2, 9, 128, 64), (3, 16, 64, 64), (2, 56, 64, 64)])
 def test_conv_bn_fused_statistics(cuda, monkeypatch, fused, N, HW, C, OC):
     """Implicit-conv forward emitting the BatchNorm batch statistics from its GEMM epilogue
-    (REPLICANN_BN_FUSED_STATS=1, M % 256 != 0 here) vs the BN's own statistics pass, both
+    (ops.conv.BN_FUSED_STATS, M % 256 != 0 here) vs the BN's own statistics pass, both
     against fp32 conv + batch_norm (outputs, running statistics, input / weight gradients)."""
-    monkeypatch.setenv("REPLICANN_BN_FUSED_STATS", fused)
+    from replicann_amd.ops import conv as conv_mod
+    monkeypatch.setattr(conv_mod, "BN_FUSED_STATS", fused == "1")
     torch.manual_seed(29)
     x = bf(N, HW, HW, C).requires_grad_()
     w = bf(OC, 3, 3, C, scale=0.05).requires_grad_()
