@@ -77,6 +77,8 @@ struct GemmArgs {
     const float* sb;
     // cfg 11 tile walk: tile-rows per group (0: GROUP_M)
     int group_m;
+    // persistent kernels (cfg 9 / 11): 1 = never use the XCD-banded tile order (band_tile; A/B only)
+    int no_band;
     // split-K reduction only: optional device scalar multiplying the slab sum (the fp8 weight gradient of the
     // LM head: the loss gradient's g / n; the slabs themselves carry only the power-of-two tensor scales)
     const float* reduce_alpha;
@@ -188,6 +190,33 @@ RN_DEV void group_tile_g(int id, int tiles_m, int tiles_n, int gm, int& tm, int&
     const int in = id % per_group;
     tm = first_m + in % gsz;
     tn = in / gsz;
+}
+
+// XCD-banded order of the persistent kernels' static walk (round 6).  Unit u = bid + s·grid (bid the
+// xcd_remap'ed block id: hardware blocks with blockIdx % 8 == x hold bids [x·per, (x+1)·per)) is
+// mapped so that XCD x computes ALL tiles of the tile-row band [x·tm/8, (x+1)·tm/8) and nothing else:
+// every A panel is fetched into exactly one XCD's L2 (the grouped walk over the whole grid split a
+// group's tile-rows across two XCDs, so about a third of A was fetched twice from the fabric).  Inside
+// the band the walk is the usual GROUP_M-grouped order.  A bijection on [0, tm·tn) when
+// band_ok(): grid % 8 == 0, tm % 8 == 0 and tm·tn % grid == 0 (every block the same number of
+// items) — true for every GPT-2 GEMM without split-K; other shapes keep the grouped walk.  The
+// dynamic schedule's home queues hand out the same units per XCD, so it inherits the banding.
+RN_DEV bool band_ok(int grid, int tiles_m, int tiles_n) {
+    return (grid & 7) == 0 && (tiles_m & 7) == 0 && (tiles_m * tiles_n) % grid == 0;
+}
+RN_DEV void band_tile(int u, int grid, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+    const int per = grid >> 3;
+    const int s = u / grid, r = u - s * grid;
+    const int x = r / per;
+    const int bx = tiles_m >> 3;
+    group_tile_g(r - x * per + s * per, bx, tiles_n, gm, tm, tn);
+    tm += x * bx;
+}
+
+// REPLICANN_GEMM_BAND=0: the grouped walk over the whole grid instead of the XCD-banded one (A/B)
+inline int rn_gemm_no_band() {
+    static const int v = [] { const char* e = std::getenv("REPLICANN_GEMM_BAND"); return (e && e[0] == '0') ? 1 : 0; }();
+    return v;
 }
 
 RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, int& tn) {

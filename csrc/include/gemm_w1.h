@@ -201,7 +201,9 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             sd = it / tiles;
             it -= sd * tiles;
         }
-        group_tile_g(it, p.tiles_m, p.tiles_n, p.group_m > 0 ? p.group_m : GROUP_M, tm, tn);
+        if (!SPLIT && !p.no_band && band_ok(grid, p.tiles_m, p.tiles_n))
+            band_tile(it, grid, p.tiles_m, p.tiles_n, p.group_m > 0 ? p.group_m : GROUP_M, tm, tn);
+        else group_tile_g(it, p.tiles_m, p.tiles_n, p.group_m > 0 ? p.group_m : GROUP_M, tm, tn);
         m0 = tm * 256;
         n0 = tn * 256;
         kt0 = sd * nk;
@@ -757,6 +759,7 @@ void launch_w1_t(GemmArgs& a, hipStream_t st) {
     }
     const int items = a.tiles_m * a.tiles_n * (SPLIT ? a.split : 1);
     const int grid = items < cu_n ? items : cu_n;
+    a.no_band = rn_gemm_no_band();
     kern<<<grid, 256, W1_LDS, st>>>(a);
 }
 
