@@ -77,8 +77,6 @@ struct GemmArgs {
     const float* sb;
     // cfg 11 tile walk: tile-rows per group (0: GROUP_M)
     int group_m;
-    // persistent kernels (cfg 9 / 11): 1 = never use the XCD-banded tile order (band_tile; A/B only)
-    int no_band;
     // split-K reduction only: optional device scalar multiplying the slab sum (the fp8 weight gradient of the
     // LM head: the loss gradient's g / n; the slabs themselves carry only the power-of-two tensor scales)
     const float* reduce_alpha;
@@ -192,7 +190,7 @@ RN_DEV void group_tile_g(int id, int tiles_m, int tiles_n, int gm, int& tm, int&
     tn = in / gsz;
 }
 
-// XCD-banded order of the persistent kernels' static walk (round 6).  Unit u = bid + s·grid (bid the
+// XCD-banded order of the one-wave-per-SIMD kernel's static walk (cfg 11, round 6).  Unit u = bid + s·grid (bid the
 // xcd_remap'ed block id: hardware blocks with blockIdx % 8 == x hold bids [x·per, (x+1)·per)) is
 // mapped so that XCD x computes ALL tiles of the tile-row band [x·tm/8, (x+1)·tm/8) and nothing else:
 // every A panel is fetched into exactly one XCD's L2 (the grouped walk over the whole grid split a
@@ -200,7 +198,11 @@ RN_DEV void group_tile_g(int id, int tiles_m, int tiles_n, int gm, int& tm, int&
 // the band the walk is the usual GROUP_M-grouped order.  A bijection on [0, tm·tn) when
 // band_ok(): grid % 8 == 0, tm % 8 == 0 and tm·tn % grid == 0 (every block the same number of
 // items) — true for every GPT-2 GEMM without split-K; other shapes keep the grouped walk.  The
-// dynamic schedule's home queues hand out the same units per XCD, so it inherits the banding.
+// Measured (profiles/gemm_band_r6b.txt): fp8 c_attn / c_fc shape (65536 x 3072 x 1024) 1410 -> 1516 TF/s,
+// MLP c_proj (K 4096) 1768 -> 1808.  On cfg 9 (bf16) the same order changed nothing — identical L2
+// hit / miss / memory-side request counts: with 3 to 12 tile columns a 32-CU round covers a
+// fractional number of tile-rows, so about a third of the A panels straddle two rounds and are
+// fetched again after the round between evicted them, whichever XCD owns them (docs/DESIGN.md §3).
 RN_DEV bool band_ok(int grid, int tiles_m, int tiles_n) {
     return (grid & 7) == 0 && (tiles_m & 7) == 0 && (tiles_m * tiles_n) % grid == 0;
 }
@@ -213,11 +215,6 @@ RN_DEV void band_tile(int u, int grid, int tiles_m, int tiles_n, int gm, int& tm
     tm += x * bx;
 }
 
-// REPLICANN_GEMM_BAND=0: the grouped walk over the whole grid instead of the XCD-banded one (A/B)
-inline int rn_gemm_no_band() {
-    static const int v = [] { const char* e = std::getenv("REPLICANN_GEMM_BAND"); return (e && e[0] == '0') ? 1 : 0; }();
-    return v;
-}
 
 RN_DEV void map_tile(int bid, int nblocks, int tiles_m, int tiles_n, int& tm, int& tn) {
     group_tile(xcd_remap(bid, nblocks), tiles_m, tiles_n, tm, tn);

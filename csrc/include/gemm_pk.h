@@ -315,8 +315,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     const int grid = gridDim.x;
     const int bid = xcd_remap(blockIdx.x, grid);
     const int nk = p.k_per_split / BK;
-    // XCD-banded static walk (gemm_impl.h band_tile): no split-K, shapes that band evenly
-    const bool band = !SPLIT && p.split == 1 && !p.no_band && band_ok(grid, p.tiles_m, p.tiles_n);
 
     // ---- tile schedule (see the header): static walk or dynamic queue over the items ----
     // DYN (a separate instantiation, so the static walk carries none of the queue's code; the
@@ -357,8 +355,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pk(GemmArgs p) {
     auto item_coords = [&](int item, int& m0, int& n0, int& kb, int& ke, int& tm) {
         const int sid = item / tiles;
         int tn;
-        if (band) band_tile(item, grid, p.tiles_m, p.tiles_n, GROUP_M, tm, tn);
-        else group_tile(item - sid * tiles, p.tiles_m, p.tiles_n, tm, tn);
+        group_tile(item - sid * tiles, p.tiles_m, p.tiles_n, tm, tn);
         m0 = tm * BM;
         n0 = tn * BN;
         kb = sid * p.k_per_split;
@@ -969,7 +966,6 @@ void launch_pk_t(GemmArgs& a, hipStream_t st) {
         cus = cu_n;
     }
     a.st_nt = rn_gemm_st_nt(a);
-    a.no_band = rn_gemm_no_band();
     const int reserve = rn_gemm_get_reserve();
     if (reserve > 0 && reserve < cus) cus -= reserve;
     if (!DYN) a.sched = nullptr;

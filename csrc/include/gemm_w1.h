@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w1(GemmArgs p) {
             sd = it / tiles;
             it -= sd * tiles;
         }
-        if (!SPLIT && !p.no_band && band_ok(grid, p.tiles_m, p.tiles_n))
+        if (!SPLIT && band_ok(grid, p.tiles_m, p.tiles_n))
             band_tile(it, grid, p.tiles_m, p.tiles_n, p.group_m > 0 ? p.group_m : GROUP_M, tm, tn);
         else group_tile_g(it, p.tiles_m, p.tiles_n, p.group_m > 0 ? p.group_m : GROUP_M, tm, tn);
         m0 = tm * 256;
@@ -759,7 +759,6 @@ void launch_w1_t(GemmArgs& a, hipStream_t st) {
     }
     const int items = a.tiles_m * a.tiles_n * (SPLIT ? a.split : 1);
     const int grid = items < cu_n ? items : cu_n;
-    a.no_band = rn_gemm_no_band();
     kern<<<grid, 256, W1_LDS, st>>>(a);
 }
 

@@ -1232,6 +1232,260 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
     if (p.q8) attn_q8_amax(p.q8part, q8m);
 }
 
+// ======================= D = 64 on v_mfma_f32_32x32x16_bf16 (round 6) =======================
+// The causal forward re-tiled for the 32×32×16 MFMA.  Why: the 16×16×32 kernels above run with the
+// softmax VALU beside their MFMAs, and a 16×16×32 MFMA holds the SIMD's vector issue for 8 of its 16
+// cycles while a 32×32×16 one holds it for 8 of 32 (MI355X_MICROARCH.md, 'vector-instruction ISSUE
+// cost'): for the same FLOPs the larger shape issues half the MFMA instructions and leaves 3× the issue
+// cycles between them.
+//   * the softmax row (the query) is the accumulator COLUMN (lane & 31), the keys sit in the 16
+//     accumulator registers: a 32×32 result is the next MFMA's B operand after pairwise bf16 packing
+//     (registers 8s'..8s'+7 = k-step s', element j of lane half h = row 16s' + 8(j>>2) + 4h + (j&3):
+//     cdna_hip_programming.md §3), and V's column read (ds_read_b64_tr_b16 from the row-major LDS tile)
+//     takes the same rows, so P never crosses lanes or LDS; a row max is 16 v_max3 + one permlane32 swap;
+//   * LDS tiles [64 rows][64 bf16], 16-B chunk c of row r at c ^ swz32(r): conflict-free for the
+//     32×32×16 row fragments (ds_read_b128 lane groups of the §LDS table) AND the transposed fragments
+//     (4 consecutive rows × 4 chunks per 32-lane half); one image serves both (SQ_LDS_BANK_CONFLICT 0);
+//   * row sums from a P·1 MFMA, the O rescale deferred until a row max grows past 2^8 (T13), mask work
+//     only on the 32-key blocks the diagonal / Tk tail cuts.
+// Measured (profiles/attention_r6.txt, GPT-2-small b64 causal): forward 0.187 -> 0.179 ms per layer.  The
+// same re-tiling of dQ and dK/dV (with the dP accumulators started at −δ straight from LDS) was built,
+// fp32-tested and measured SLOWER (0.559 -> 0.594 ms: dQ 238 -> 258 us, dK/dV 347 -> 352 us; MFMA busy
+// 0.31-0.32 either way, 254 VGPRs in dK/dV); as the non-causal ViT forward (T = 197: 0.205 -> 0.212 ms)
+// — both removed.  Their unmasked loops were already lean (per 32 MFMAs: 32 fma / exp / mul / cvt_pk),
+// so the remaining gap is stall structure (WAIT_ANY ≈ 0.3-0.4), not instruction count.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+#define MFMA32 __builtin_amdgcn_mfma_f32_32x32x16_bf16
+
+RN_DEV int swz32(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+
+// rows [r0, r0+64) (valid < rlim) of a [T][stride] bf16 matrix (64 columns) into a swz32 tile
+RN_DEV void stage32_async(const u32x4& rs, long st, int r0, int rlim, const char* lds, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ins = wave * 2 + i;
+        const int r = ins * 8 + (lane >> 3);
+        const int cg = (lane & 7) ^ swz32(r);
+        const bool ok = (r0 + r) < rlim;
+        const uint32_t voff = ok ? (uint32_t)((((long)(r0 + r)) * st + cg * 8) * 2) : 0xFFFFFFF0u;
+        dma16_async(rs, voff, lds_addr(lds + ins * 1024));
+    }
+}
+
+// per-lane LDS offsets of the 32×32×16 fragments in a swz32 tile (rows of a 32-row block r0 = 32·X):
+//   row fragment (A operand, row r0 + (lane&31), k-step s = columns 16s + 8h .. +7): rf[s]
+//   transposed fragment (A operand, row = column 32·jd + (lane&31) of the tile, k-step rows
+//   r0 + 16s' + 8(j>>2) + 4h + (j&3)): two ds_read_b64_tr_b16 at cf[jd][0] / cf[jd][1]
+struct Frag32 {
+    uint32_t rf[4];
+    uint32_t cf[2][2];
+};
+RN_DEV Frag32 make_frag32(int lane) {
+    Frag32 f;
+    const int r = lane & 31, h = lane >> 5;
+    const int sw = swz32(r);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f.rf[s] = r * 128 + (((2 * s + h) ^ sw) << 4);
+    const int i = lane & 15, qq = i >> 2, pp = i & 3, gp = (lane >> 4) & 1;
+#pragma unroll
+    for (int jd = 0; jd < 2; ++jd)
+#pragma unroll
+        for (int sec = 0; sec < 2; ++sec) {
+            const int R = 4 * h + qq + 8 * sec;
+            const int ch = 4 * jd + 2 * gp + (pp >> 1);
+            f.cf[jd][sec] = R * 128 + ((ch ^ swz32(R)) << 4) + (pp & 1) * 8;
+        }
+    return f;
+}
+// row fragment of 32-row block X, k-step s
+RN_DEV s16x8 rfrag32(const char* t, int X, int s, const Frag32& f) {
+    return *reinterpret_cast<const s16x8*>(t + X * 32 * 128 + f.rf[s]);
+}
+// transposed fragment: tile rows 16·ks + … (ks = 0..3 over the 64-row tile), tile columns 32·jd + (lane&31)
+RN_DEV s16x8 tfrag32(const char* t, int ks, int jd, const Frag32& f) {
+    const char* a = t + ks * 16 * 128;
+    s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + f.cf[jd][0]));
+    s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + f.cf[jd][1]));
+    s16x8 r;
+    r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+    r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+    return r;
+}
+// registers 8s'..8s'+7 of a 32×32 accumulator as a bf16 B-operand fragment (k-step s')
+RN_DEV s16x8 pack16(const f32x16& x, int s2) {
+    s16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = bfbits(x[8 * s2 + j]);
+    return r;
+}
+RN_DEV float swap_max(float x) {
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+RN_DEV float swap_sum(float x) {
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+// accumulator row of register i for lane half h
+RN_DEV constexpr int arow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// store a wave's [64 d][32 cols] accumulator pair as rows (col = this lane's row of the output):
+// out[d] = x·mul in bf16 (and, q8, e5m2 of the bf16 value with the delayed scale)
+RN_DEV void store_rows32(const f32x16 (&x)[2], float mul, bf16* dst, uint8_t* q8dst, bool bf, float q8inv, float& q8m,
+                         int h) {
+#pragma unroll
+    for (int jd = 0; jd < 2; ++jd)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            const int d = 32 * jd + 8 * c4 + 4 * h;
+            const bf16x4 v = {(bf16)(x[jd][4 * c4] * mul), (bf16)(x[jd][4 * c4 + 1] * mul), (bf16)(x[jd][4 * c4 + 2] * mul),
+                              (bf16)(x[jd][4 * c4 + 3] * mul)};
+            if (q8dst) attn_q8_store4(q8dst + d, (float)v[0], (float)v[1], (float)v[2], (float)v[3], q8inv, q8m);
+            if (bf) *reinterpret_cast<bf16x4*>(dst + d) = v;
+        }
+}
+
+// ---------------- forward: 4 waves × 32 queries, 64-key tiles ----------------
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) attn_fwd32_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Frag32 fo = make_frag32(lane);
+    int bh, qb;
+    blk_map(p, (p.Tq + 127) / 128, CAUSAL, bh, qb);
+    const int b = bh / p.H, hh = bh % p.H;
+    const int q0 = qb * 128 + wave * 32;  // this wave's first query
+    const int qg = q0 + r;                // this lane's query
+    const int off = p.Tk - p.Tq;
+    const float sl2 = p.scale * LOG2E;
+    const bf16* qbase = p.q + b * p.q_sb + hh * p.q_sh;
+    const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + hh * p.k_sh);
+    const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + hh * p.v_sh);
+    int kv_end = p.Tk;
+    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
+    int nfull = p.Tk / 64;  // tiles every key of which every query of the block sees
+    if (CAUSAL) nfull = min(nfull, max(0, (qb * 128 + off + 1) / 64));
+    nfull = min(nfull, nkv);
+#define Kt(i) (smem + (i) * 16384)
+#define Vt(i) (smem + 8192 + (i) * 16384)
+    if (nkv > 0) {
+        stage32_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
+        stage32_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+    }
+    s16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = gload16(qbase + (long)qg * p.q_st + 16 * s + 8 * h, qg < p.Tq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(qf[s]));
+    // Online softmax in log2 units (ms = running row max × sl2) with a deferred rescale (cdna_hip_programming.md
+    // T13): O and the row sum are rescaled only when some row's tile max exceeds ms by more than THR, so p ≤
+    // 2^THR (exact in fp32, the usual relative error in the bf16 P operand).  Row sums come from a P·1 MFMA
+    // (every register of lsum holds the running sum of its column; [0] is read): 2 MFMAs per 32 keys
+    // instead of 32 adds, the VALU being this kernel's bound (PMC, profiles/attention_r6f.txt).
+    constexpr float THR = 8.f;
+    float ms = -INFINITY;
+    f32x16 oacc[2], lsum;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; lsum[i] = 0.f; }
+    const short one = 0x3F80;  // bf16 1.0
+    const s16x8 ones = {one, one, one, one, one, one, one, one};
+
+    auto tile = [&](const int t, auto masked_c) {
+        constexpr bool MASKED = decltype(masked_c)::value;
+        const char* kt = Kt(t & 1);
+        const char* vt = Vt(t & 1);
+        const int kv0 = t * 64;
+        // 32-key block class (wave-uniform): 0 dead (past Tk / above every query of this wave), 1 every key
+        // visible to every query, 2 partial (the causal diagonal, the ragged Tk tail): per-element mask
+        auto cls = [&](int kb) -> int {
+            if constexpr (!MASKED) return 1;
+            const int k0 = kv0 + 32 * kb;
+            if (k0 >= p.Tk) return 0;
+            if (CAUSAL && k0 > min(q0 + 31, p.Tq - 1) + off) return 0;
+            return (k0 + 31 >= p.Tk || (CAUSAL && k0 + 31 > q0 + off)) ? 2 : 1;
+        };
+        f32x16 sacc[2];
+        float pm = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            const int c_ = cls(kb);
+            if (MASKED && c_ == 0) continue;
+            f32x16 a;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) a[i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) a = MFMA32(rfrag32(kt, kb, s, fo), qf[s], a, 0, 0, 0);
+            if (MASKED && c_ == 2) {
+                const int lim = CAUSAL ? min(qg + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (kv0 + 32 * kb + arow(i, h) > lim) a[i] = -INFINITY;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pm = fmaxf(pm, a[i]);
+            sacc[kb] = a;
+        }
+        pm = swap_max(pm) * sl2;
+        if (__builtin_amdgcn_ballot_w64(pm > ms + THR)) {  // wave-uniform, rare after the first tile
+            const float mn = fmaxf(ms, pm);
+            const float alpha = (ms == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ms - mn);
+            oacc[0] *= alpha;
+            oacc[1] *= alpha;
+            lsum[0] *= alpha;
+            ms = mn;
+        }
+        // (masked tiles: a row with no visible key so far keeps ms = -inf and p = 0)
+        const float nms = (MASKED && ms == -INFINITY) ? 0.f : -ms;
+        // O^T[d][q] += V^T[d][key] P^T[key][q];  lsum += 1 · P^T
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            if (MASKED && cls(kb) == 0) continue;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sacc[kb][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][i], sl2, nms));
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const s16x8 pb = pack16(sacc[kb], s2);
+#pragma unroll
+                for (int jd = 0; jd < 2; ++jd) oacc[jd] = MFMA32(tfrag32(vt, 2 * kb + s2, jd, fo), pb, oacc[jd], 0, 0, 0);
+                lsum = MFMA32(ones, pb, lsum, 0, 0, 0);
+            }
+        }
+    };
+    auto sync_prefetch = [&](int t) {
+        vm_wait_all();
+        __syncthreads();
+        if (t + 1 < nkv) {
+            stage32_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt((t & 1) ^ 1), wave, lane);
+            stage32_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
+        }
+    };
+    const int nf = q0 < p.Tq ? nfull : 0;
+    int t = 0;
+    for (; t < nf; ++t) {
+        sync_prefetch(t);
+        tile(t, std::false_type{});
+    }
+    for (; t < nkv; ++t) {
+        sync_prefetch(t);
+        if (CAUSAL && t * 64 > q0 + 31 + off) continue;  // wave-uniform: every query precedes the tile
+        if (q0 >= p.Tq) continue;
+        tile(t, std::true_type{});
+    }
+#undef Kt
+#undef Vt
+    const float lt = lsum[0];  // (the full sum over both lane halves' keys: the MFMA summed them)
+    if (qg < p.Tq) {
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        float dummy = 0.f;
+        store_rows32(oacc, inv, p.o + b * p.o_sb + (long)qg * p.o_st + hh * p.o_sh, nullptr, true, 0.f, dummy, h);
+        if (h == 0) p.lse[((long)b * p.H + hh) * p.Tq + qg] = (lt > 0.f) ? (ms + log2f(lt)) : INFINITY;
+    }
+}
+
+#undef MFMA32
+
 // ============================== generic path (any D <= 256) ==============================
 RN_DEV float bias_at(const AttnArgs& p, int b, int qi, int kj) {
     return p.bias ? p.bias[((long)(p.bias_b > 1 ? b : 0) * p.Tq + qi) * p.Tk + kj] : 0.f;
@@ -1468,9 +1722,12 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         dim3 grid(B * H * ((Tq + 127) / 128));
         // plain causal / non-causal: the split-loop v2 kernel with the LEAN softmax bookkeeping
         // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
-        if (!bias && p_drop == 0.f) {
-            if (causal) attn_fwd64v2_k<true, 3, true><<<grid, 256, 32768, st>>>(a);
-            else attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
+        // plain causal: the 32×32×16 kernel (GPT-2-small b64: 0.187 -> 0.179 ms per layer); plain non-causal: the
+        // 16×16×32 split-loop kernel (ViT-B/16 T = 197: 0.205 ms vs 0.212 for the 32×32 one) — profiles/attention_r6.txt
+        if (!bias && p_drop == 0.f && causal) {
+            attn_fwd32_k<true><<<grid, 256, 32768, st>>>(a);
+        } else if (!bias && p_drop == 0.f) {
+            attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
         } else {
             RN_DISPATCH3(attn_fwd64_k, grid, 32768, st, a);
         }

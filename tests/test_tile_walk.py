@@ -1,8 +1,8 @@
-"""The persistent GEMMs' XCD-banded tile order (csrc/include/gemm_impl.h band_tile, round 6), replicated
+"""The one-wave-per-SIMD GEMM's XCD-banded tile order (csrc/include/gemm_impl.h band_tile, round 6), replicated
 in Python: a bijection on the tiles whenever band_ok() admits the shape, every XCD (hardware blocks with
 blockIdx % 8 == x) computes exactly the tile-rows of its own band, and the static walk gives every block
-the same number of items.  (The GPU tests of cfg 9 / cfg 11 — tests/test_gemm_w1_gpu.py SHAPES
-(65536, 768, 768), (65536, 512, 128) — run the device code on banded shapes against fp32.)"""
+the same number of items.  (The cfg-11 GPU tests — tests/test_gemm_w1_gpu.py SHAPES (65536, 768, 768),
+(65536, 512, 128) and the fp8 (65536, 3072, 1024) case — run the device code on banded shapes against fp32.)"""
 
 import pytest
 
