@@ -32,7 +32,11 @@ def main():
     ap.add_argument("--bias", action="store_true")
     ap.add_argument("--res", action="store_true", help="residual epilogue (full-tile operand read)")
     ap.add_argument("--fp8", default=None, help="e4m3 x e4m3 forward GEMM (layout nt) on kernel 0 / 9 / 11")
+    ap.add_argument("--reserve", type=int, default=0, help="CUs the persistent kernel leaves idle (<= 128, multiple of 8)")
     a = ap.parse_args()
+    if a.reserve:
+        from replicann_amd import _ext
+        _ext.ops().gemm_set_reserve(a.reserve)
     ta, tb = a.layout[0] == "t", a.layout[1] == "t"
     torch.manual_seed(0)
     A = torch.randn(*((a.K, a.M) if ta else (a.M, a.K)), device="cuda").bfloat16()
