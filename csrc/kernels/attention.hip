@@ -1252,7 +1252,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq64_k(AttnArgs p) {
 // same re-tiling of dQ and dK/dV (with the dP accumulators started at −δ straight from LDS) was built,
 // fp32-tested and measured SLOWER (0.559 -> 0.594 ms: dQ 238 -> 258 us, dK/dV 347 -> 352 us; MFMA busy
 // 0.31-0.32 either way, 254 VGPRs in dK/dV); as the non-causal ViT forward (T = 197: 0.205 -> 0.212 ms)
-// — both removed.  Their unmasked loops were already lean (per 32 MFMAs: 32 fma / exp / mul / cvt_pk),
+// — both removed.  A software-pipelined dK/dV (query block 1's S / dP MFMAs issued before block 0's softmax
+// VALU, block 0's dV / dK before block 1's; 246 VGPRs) closed half the gap (+2 %), sched_group_barrier
+// interleaving of those phases nothing more, occupancy 1 (122 VGPR + 160 AGPR) lost 33 %: removed too.  Their unmasked loops were already lean (per 32 MFMAs: 32 fma / exp / mul / cvt_pk),
 // so the remaining gap is stall structure (WAIT_ANY ≈ 0.3-0.4), not instruction count.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define MFMA32 __builtin_amdgcn_mfma_f32_32x32x16_bf16
