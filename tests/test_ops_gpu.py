@@ -1155,3 +1155,37 @@ def test_dropout_device_seeds_graph_capture(cuda):
         replays.append(out.item())
     assert len(set(replays)) == 3, "each replay must draw new dropout masks"
     assert replays == eager, (replays, eager)
+
+
+@pytest.mark.parametrize("jump", [12.0, 6.0, 30.0])
+def test_attention_fwd32_deferred_rescale_forced(cuda, jump):
+    """The causal D = 64 forward (attn_fwd32_k) rescales O and the row sum only when a row's tile max exceeds
+    the running max by more than 2^8 (T13): a branch bounded random data rarely takes.  Force it (MI355X guide
+    rule 26): for chosen query rows one key of a LATER tile is a spike along that query (its score jumps by
+    `jump` log2 units over everything before it: 12 and 30 take the rescale, 6 stays under the threshold with
+    P up to 2^6), and check O, the backward's gradients and the base-2 lse the backward reads against a float64
+    reference over the full tensors."""
+    torch.manual_seed(21)
+    B, T, H, D = 1, 512, 2, 64
+    q = torch.randn(B, T, H, D, device="cuda")
+    k = torch.randn(B, T, H, D, device="cuda") * 0.3
+    v = torch.randn(B, T, H, D, device="cuda")
+    sl2 = 0.125 * 1.4426950408889634
+    for hh in range(H):
+        for i in range(200, T, 7):            # query rows
+            j = (i // 64 - 1) * 64 + (i % 53)  # a key in the tile before the diagonal tile (visible: j < i)
+            qi = q[0, i, hh]
+            k[0, j, hh] = qi / qi.dot(qi) * (jump / sl2)  # q_i · k_j = jump / sl2  →  jump in log2 units
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    qg, kg, vg = [t.clone().requires_grad_() for t in (q, k, v)]
+    o = ops.attention(qg, kg, vg, scale=0.125, causal=True)
+    go = torch.randn(B, T, H, D, device="cuda").bfloat16()
+    o.backward(go)
+    qd, kd, vd = [t.detach().double().requires_grad_() for t in (q, k, v)]
+    s = torch.einsum("bqhd,bkhd->bhqk", qd, kd) * 0.125
+    s = s.masked_fill(torch.triu(torch.ones(T, T, dtype=torch.bool, device="cuda"), 1), float("-inf"))
+    od = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), vd)
+    od.backward(go.double())
+    assert rel_err(o, od) < 1e-2
+    for t, td in ((qg, qd), (kg, kd), (vg, vd)):
+        assert rel_err(t.grad, td.grad) < 2e-2
