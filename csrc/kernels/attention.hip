@@ -1348,31 +1348,53 @@ RN_DEV void store_rows32(const f32x16 (&x)[2], float mul, bf16* dst, uint8_t* q8
 }
 
 // ---------------- forward: 4 waves × 32 queries, 64-key tiles ----------------
-template <bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) attn_fwd32_k(AttnArgs p) {
+// RES (Tq, Tk <= 256, RES_T): one workgroup of 8 waves per (b, h) holds the head's whole K and V in LDS
+// (staged once, 64 KiB, no barrier inside the key loop): K / V are read from HBM once per head instead
+// of once per 128-query block.  At ViT-B/16's T = 197 the streaming kernel reads K and V twice and
+// the forward is HBM-bound (Q + 2K + 2V + O per layer).
+constexpr int RES_T = 256;
+template <bool CAUSAL, bool RES = false>
+__global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const Frag32 fo = make_frag32(lane);
+    constexpr int QB = RES ? RES_T : 128;  // queries per workgroup
     int bh, qb;
-    blk_map(p, (p.Tq + 127) / 128, CAUSAL, bh, qb);
+    if constexpr (RES) {
+        bh = blockIdx.x;
+        qb = 0;
+    } else {
+        blk_map(p, (p.Tq + 127) / 128, CAUSAL, bh, qb);
+    }
     const int b = bh / p.H, hh = bh % p.H;
-    const int q0 = qb * 128 + wave * 32;  // this wave's first query
-    const int qg = q0 + r;                // this lane's query
+    const int q0 = qb * QB + wave * 32;  // this wave's first query
+    const int qg = q0 + r;               // this lane's query
     const int off = p.Tk - p.Tq;
     const float sl2 = p.scale * LOG2E;
     const bf16* qbase = p.q + b * p.q_sb + hh * p.q_sh;
     const u32x4 krs = make_rsrc_sgpr(p.k + b * p.k_sb + hh * p.k_sh);
     const u32x4 vrs = make_rsrc_sgpr(p.v + b * p.v_sb + hh * p.v_sh);
     int kv_end = p.Tk;
-    if (CAUSAL) kv_end = min(p.Tk, qb * 128 + 128 + off);
+    if (CAUSAL) kv_end = min(p.Tk, qb * QB + QB + off);
     const int nkv = kv_end > 0 ? (kv_end + 63) / 64 : 0;
     int nfull = p.Tk / 64;  // tiles every key of which every query of the block sees
-    if (CAUSAL) nfull = min(nfull, max(0, (qb * 128 + off + 1) / 64));
+    if (CAUSAL) nfull = min(nfull, max(0, (qb * QB + off + 1) / 64));
     nfull = min(nfull, nkv);
-#define Kt(i) (smem + (i) * 16384)
-#define Vt(i) (smem + 8192 + (i) * 16384)
-    if (nkv > 0) {
+    // streaming: double-buffered [K 64 rows | V 64 rows] pairs; RES: K rows [0, 256) then V rows [0, 256)
+#define Kt(i) (RES ? smem + (i) * 8192 : smem + ((i) & 1) * 16384)
+#define Vt(i) (RES ? smem + 32768 + (i) * 8192 : smem + 8192 + ((i) & 1) * 16384)
+    if constexpr (RES) {
+        // every 8-row piece of the nkv tiles (rows past Tk read as zeros: V's padding rows must be finite)
+        for (int ins = wave; ins < nkv * 8; ins += 8) {
+            const int row = ins * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz32(row);
+            const bool ok = row < p.Tk;
+            dma16_async(krs, ok ? (uint32_t)(((long)row * p.k_st + cg * 8) * 2) : 0xFFFFFFF0u, lds_addr(smem + ins * 1024));
+            dma16_async(vrs, ok ? (uint32_t)(((long)row * p.v_st + cg * 8) * 2) : 0xFFFFFFF0u,
+                        lds_addr(smem + 32768 + ins * 1024));
+        }
+    } else if (nkv > 0) {
         stage32_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
         stage32_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
     }
@@ -1396,8 +1418,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_k(AttnArgs p) {
 
     auto tile = [&](const int t, auto masked_c) {
         constexpr bool MASKED = decltype(masked_c)::value;
-        const char* kt = Kt(t & 1);
-        const char* vt = Vt(t & 1);
+        const char* kt = Kt(t);
+        const char* vt = Vt(t);
         const int kv0 = t * 64;
         // 32-key block class (wave-uniform): 0 dead (past Tk / above every query of this wave), 1 every key
         // visible to every query, 2 partial (the causal diagonal, the ragged Tk tail): per-element mask
@@ -1456,11 +1478,18 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_k(AttnArgs p) {
         }
     };
     auto sync_prefetch = [&](int t) {
+        if constexpr (RES) {
+            if (t == 0) {
+                vm_wait_all();
+                __syncthreads();
+            }
+            return;
+        }
         vm_wait_all();
         __syncthreads();
         if (t + 1 < nkv) {
-            stage32_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt((t & 1) ^ 1), wave, lane);
-            stage32_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt((t & 1) ^ 1), wave, lane);
+            stage32_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(t + 1), wave, lane);
+            stage32_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(t + 1), wave, lane);
         }
     };
     const int nf = q0 < p.Tq ? nfull : 0;
@@ -1483,6 +1512,257 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_k(AttnArgs p) {
         float dummy = 0.f;
         store_rows32(oacc, inv, p.o + b * p.o_sb + (long)qg * p.o_st + hh * p.o_sh, nullptr, true, 0.f, dummy, h);
         if (h == 0) p.lse[((long)b * p.H + hh) * p.Tq + qg] = (lt > 0.f) ? (ms + log2f(lt)) : INFINITY;
+    }
+}
+
+// ---------------- backward, whole head resident (Tq, Tk <= RES_T; non-causal, no bias / dropout / e5m2) ----------------
+// ViT-B/16 (T = 197) is HBM-bound in the streaming backward: the dQ kernel re-reads K / V per 128-query
+// block, the dK/dV kernel Q / dO per 128-key block, and δ makes a round trip.  Here one persistent 8-wave
+// workgroup per CU walks the heads; a head's Q, dO, K, V tiles sit in LDS (128 KiB) and every operand is read
+// from HBM once:
+//   A   δ of the wave's 32 queries from O / dO rows in registers; lse, −δ -> LDS      (barrier B0)
+//   P1  wave w owns keys [32w, 32w+32): K / V rows in registers (prefetched), loops over every query
+//       block from the Q / dO tiles: S, dP, P, dS; dV^T += dO^T P, dK^T += Q^T dS   (barrier B1)
+//       -> the Q / dO tiles of the NEXT head stream in during P2
+//   P2  wave w owns queries [32w, 32w+32): loops over every key block from the K / V tiles:
+//       S^T, dP^T, dS^T; dQ^T += K^T dS^T                                             (barrier B2)
+//       -> the K / V tiles of the next head stream in during the next A + P1
+// The 32×32×16 orientation and fragment helpers are the forward's (accumulator column = the row that
+// owns the result, reduced index in registers).  Rows past Tq / Tk are zero-filled by the DMA and lse = +inf
+// there, so only the ragged key block of P2 needs a mask.
+// QKV bias partials (bsum): Σ_rows dV = Σ_q dO (softmax rows sum to 1), Σ_rows dK = 0 (a key bias shifts
+// all of a query's scores alike), Σ_rows dQ = scale · Σ_key (Σ_q dS[q][key]) K[key] with the column sums
+// of dS from a 1·dS MFMA in P1 — all written into the head's first 64-row block (the consumer sums them all).
+constexpr int RES_LDS = 4 * 32768 + 3 * 1024 + 2 * 8 * 64 * 4;  // tiles, lse | −δ | Σ_q dS, bias partials
+__global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* const Qt = smem;
+    char* const Dt = smem + 32768;
+    char* const Kt = smem + 65536;
+    char* const Vt = smem + 98304;
+    float* const lseL = reinterpret_cast<float*>(smem + 131072);  // [256] lse, log2 units (+inf past Tq)
+    float* const ndL = lseL + 256;                                 // [256] −δ
+    float* const csL = ndL + 256;                                  // [256] Σ_q dS[q][key]
+    float* const bpL = csL + 256;                                  // [2][8][64] bias partials: dQ, dV
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Frag32 fo = make_frag32(lane);
+    const float sl2 = p.scale * LOG2E;
+    const int BH = p.B * p.H, E = p.H * 64;
+    const int nqb = (p.Tq + 31) / 32, nkb = (p.Tk + 31) / 32;
+    const int w0 = wave * 32;  // this wave's keys (P1) and queries (P2)
+    const short one = 0x3F80;
+    const s16x8 ones = {one, one, one, one, one, one, one, one};
+
+    s16x8 kf[4], vf[4], orw[4];
+    float lsel;
+    // registers of head bh: K / V rows w0 + r (P1's B operands), O rows w0 + r (δ), lse
+    auto issue_regs = [&](int bh) {
+        const int b = bh / p.H, hh = bh % p.H;
+        const int row = w0 + r;
+        const bool kok = row < p.Tk, qok = row < p.Tq;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int c = 16 * s + 8 * h;
+            kf[s] = gload16(p.k + b * p.k_sb + (long)row * p.k_st + hh * p.k_sh + c, kok);
+            vf[s] = gload16(p.v + b * p.v_sb + (long)row * p.v_st + hh * p.v_sh + c, kok);
+            orw[s] = gload16(p.o + b * p.o_sb + (long)row * p.o_st + hh * p.o_sh + c, qok);
+        }
+        lsel = qok ? p.lse[((long)b * p.H + hh) * p.Tq + row] : INFINITY;
+    };
+    // two [256][64] tiles by LDS-DMA, 4 + 4 pieces per wave whatever T (rows past `lim` zero-filled): the K / V
+    // pair must be this wave's 8 youngest loads (s_waitcnt vmcnt(8) below)
+    auto issue_tiles = [&](const bf16* x0, long st0, const bf16* x1, long st1, int lim, char* t0, char* t1) {
+        const u32x4 rs0 = make_rsrc_sgpr(x0), rs1 = make_rsrc_sgpr(x1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ins = wave + 8 * i;
+            const int row = ins * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz32(row);
+            const bool ok = row < lim;
+            dma16_async(rs0, ok ? (uint32_t)(((long)row * st0 + cg * 8) * 2) : 0xFFFFFFF0u, lds_addr(t0 + ins * 1024));
+            dma16_async(rs1, ok ? (uint32_t)(((long)row * st1 + cg * 8) * 2) : 0xFFFFFFF0u, lds_addr(t1 + ins * 1024));
+        }
+    };
+    auto issue_qdo = [&](int bh) {
+        const int b = bh / p.H, hh = bh % p.H;
+        issue_tiles(p.q + b * p.q_sb + hh * p.q_sh, p.q_st, p.dout + b * p.do_sb + hh * p.do_sh, p.do_st, p.Tq, Qt, Dt);
+    };
+    auto issue_kv = [&](int bh) {
+        const int b = bh / p.H, hh = bh % p.H;
+        issue_tiles(p.k + b * p.k_sb + hh * p.k_sh, p.k_st, p.v + b * p.v_sb + hh * p.v_sh, p.v_st, p.Tk, Kt, Vt);
+    };
+    auto tile_at = [](const char* t, int row, int d) -> float {
+        const unsigned short u =
+            *reinterpret_cast<const unsigned short*>(t + row * 128 + ((((d >> 3) ^ swz32(row)) << 4) | ((d & 7) << 1)));
+        return __uint_as_float((uint32_t)u << 16);
+    };
+
+    int bh = blockIdx.x;
+    if (bh < BH) {
+        issue_qdo(bh);
+        issue_regs(bh);
+        issue_kv(bh);
+    }
+    for (; bh < BH; bh += gridDim.x) {
+        const int b = bh / p.H, hh = bh % p.H;
+        const int nxt = bh + gridDim.x;
+        // ---- A ----
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // everything but this head's K / V pieces
+        __syncthreads();  // (every wave's Q / dO pieces)
+        float dsum = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const s16x8 dr = rfrag32(Dt, wave, s, fo);  // dO row w0 + r, the columns orw[s] holds
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                dsum += __uint_as_float((uint32_t)(unsigned short)orw[s][j] << 16) *
+                        __uint_as_float((uint32_t)(unsigned short)dr[j] << 16);
+        }
+        const float ndl = -swap_sum(dsum);  // −δ of query w0 + r (0 past Tq: zero rows)
+        const float lse2 = lsel;
+        if (h == 0) {
+            lseL[w0 + r] = lsel;
+            ndL[w0 + r] = ndl;
+        }
+        __syncthreads();  // B0: lse, −δ
+        if (p.bsum) {  // Σ_q dO[q][d] over this wave's 32 queries (thread = column d)
+            float a = 0.f;
+#pragma unroll 8
+            for (int i = 0; i < 32; ++i) a += tile_at(Dt, w0 + i, lane);
+            bpL[512 + wave * 64 + lane] = a;
+        }
+        // ---- P1: dK, dV of keys w0 .. w0+31 ----
+        f32x16 dk[2], dv[2], cs;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = cs[i] = 0.f; }
+        if (w0 < p.Tk) {
+#pragma unroll 1
+            for (int X = 0; X < nqb; ++X) {
+                f32x16 sa, dp;
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    const f32x4 nd = *reinterpret_cast<const f32x4*>(ndL + 32 * X + 8 * c4 + 4 * h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { dp[4 * c4 + e] = nd[e]; sa[4 * c4 + e] = 0.f; }
+                }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) sa = MFMA32(rfrag32(Qt, X, s, fo), kf[s], sa, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) dp = MFMA32(rfrag32(Dt, X, s, fo), vf[s], dp, 0, 0, 0);
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    const f32x4 l4 = *reinterpret_cast<const f32x4*>(lseL + 32 * X + 8 * c4 + 4 * h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int i = 4 * c4 + e;
+                        sa[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], sl2, -l4[e]));  // P
+                        dp[i] *= sa[i];                                                      // dS
+                    }
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const s16x8 pb = pack16(sa, s2);
+#pragma unroll
+                    for (int jd = 0; jd < 2; ++jd) dv[jd] = MFMA32(tfrag32(Dt, 2 * X + s2, jd, fo), pb, dv[jd], 0, 0, 0);
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const s16x8 db = pack16(dp, s2);
+#pragma unroll
+                    for (int jd = 0; jd < 2; ++jd) dk[jd] = MFMA32(tfrag32(Qt, 2 * X + s2, jd, fo), db, dk[jd], 0, 0, 0);
+                    if (p.bsum) cs = MFMA32(ones, db, cs, 0, 0, 0);
+                }
+            }
+        }
+        // P2's B operands (Q / dO rows w0 + r) while the tiles are resident
+        s16x8 qf[4], df[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qf[s] = rfrag32(Qt, wave, s, fo);
+            df[s] = rfrag32(Dt, wave, s, fo);
+        }
+        vm_wait_all();  // this head's K / V tiles (issued before A)
+        if (h == 0) csL[w0 + r] = cs[0];
+        if (w0 + r < p.Tk) {
+            float dummy = 0.f;
+            store_rows32(dk, p.scale, p.dk + b * p.dk_sb + (long)(w0 + r) * p.dk_st + hh * p.dk_sh, nullptr, true, 0.f,
+                         dummy, h);
+            store_rows32(dv, 1.f, p.dv + b * p.dv_sb + (long)(w0 + r) * p.dv_st + hh * p.dv_sh, nullptr, true, 0.f,
+                         dummy, h);
+        }
+        __syncthreads();  // B1: Q / dO tiles free; K / V tiles and Σ_q dS complete
+        if (nxt < BH) {
+            issue_qdo(nxt);
+            issue_regs(nxt);
+        }
+        if (p.bsum) {  // Σ_key (Σ_q dS[q][key]) K[key][d] over this wave's 32 keys (rows past Tk are zero)
+            float a = 0.f;
+#pragma unroll 8
+            for (int i = 0; i < 32; ++i) a += csL[w0 + i] * tile_at(Kt, w0 + i, lane);
+            bpL[wave * 64 + lane] = a;
+        }
+        // ---- P2: dQ of queries w0 .. w0+31 ----
+        f32x16 dq[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { dq[0][i] = dq[1][i] = 0.f; }
+        if (w0 < p.Tq) {
+#pragma unroll 1
+            for (int kb = 0; kb < nkb; ++kb) {
+                f32x16 sa, dp;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { sa[i] = 0.f; dp[i] = ndl; }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) sa = MFMA32(rfrag32(Kt, kb, s, fo), qf[s], sa, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) dp = MFMA32(rfrag32(Vt, kb, s, fo), df[s], dp, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sa[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], sl2, -lse2));
+                if (32 * kb + 32 > p.Tk) {  // the ragged key block (wave-uniform)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (32 * kb + arow(i, h) >= p.Tk) sa[i] = 0.f;
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dp[i] *= sa[i];
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const s16x8 db = pack16(dp, s2);
+#pragma unroll
+                    for (int jd = 0; jd < 2; ++jd) dq[jd] = MFMA32(tfrag32(Kt, 2 * kb + s2, jd, fo), db, dq[jd], 0, 0, 0);
+                }
+            }
+        }
+        if (w0 + r < p.Tq) {
+            float dummy = 0.f;
+            store_rows32(dq, p.scale, p.dq + b * p.dq_sb + (long)(w0 + r) * p.dq_st + hh * p.dq_sh, nullptr, true, 0.f,
+                         dummy, h);
+        }
+        __syncthreads();  // B2: K / V tiles free, bias partials complete
+        if (p.bsum && threadIdx.x < 128) {
+            const int part = threadIdx.x >> 6, d = lane;  // 0: dQ (and dK), 1: dV
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) a += bpL[part * 512 + w * 64 + d];
+            const int nb64 = (p.Tq + 63) / 64;
+            float* row = p.bsum + (long)b * nb64 * 3 * E + hh * 64 + d;
+            if (part == 0) {
+                row[0] = a * p.scale;
+                row[E] = 0.f;
+            } else {
+                row[2 * E] = a;
+            }
+            for (int blk = 1; blk < nb64; ++blk) {
+                float* z = row + (long)blk * 3 * E;
+                if (part == 0) {
+                    z[0] = 0.f;
+                    z[E] = 0.f;
+                } else {
+                    z[2 * E] = 0.f;
+                }
+            }
+        }
+        if (nxt < BH) issue_kv(nxt);
     }
 }
 
@@ -1726,7 +2006,11 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
         // plain causal: the 32×32×16 kernel (GPT-2-small b64: 0.187 -> 0.179 ms per layer); plain non-causal: the
         // 16×16×32 split-loop kernel (ViT-B/16 T = 197: 0.205 ms vs 0.212 for the 32×32 one) — profiles/attention_r6.txt
-        if (!bias && p_drop == 0.f && causal) {
+        if (!bias && p_drop == 0.f && Tq <= RES_T && Tk <= RES_T) {
+            // whole head resident (ViT-B/16, T = 197): one 8-wave workgroup per (b, h)
+            if (causal) attn_fwd32_k<true, true><<<dim3(B * H), 512, 65536, st>>>(a);
+            else attn_fwd32_k<false, true><<<dim3(B * H), 512, 65536, st>>>(a);
+        } else if (!bias && p_drop == 0.f && causal) {
             attn_fwd32_k<true><<<grid, 256, 32768, st>>>(a);
         } else if (!bias && p_drop == 0.f) {
             attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
@@ -1792,6 +2076,23 @@ int rn_attn_bwd(const void* dout, const void* q, const void* k, const void* v, c
         // plain causal / non-causal: two 64-query groups per wave in dQ (bwd -11 % at GPT-2-small
         // shapes) and two 64-key groups per wave in dK/dV (-2.4 %, occupancy 2 at 240 VGPRs);
         // bias / dropout: one group per wave
+        if (!bias && p_drop == 0.f && !causal && !q8 && Tq <= RES_T && Tk <= RES_T) {
+            // whole head resident, persistent over the CUs (ViT-B/16, T = 197)
+            static unsigned long long res_devs = 0;
+            static int res_cus[64];
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            const unsigned long long bit = 1ull << (dev & 63);
+            if (!(res_devs & bit)) {
+                (void)hipFuncSetAttribute((const void*)attn_bwd_res_k, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS);
+                int cus = 256;
+                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                res_cus[dev & 63] = cus > 0 ? cus : 256;
+                res_devs |= bit;
+            }
+            attn_bwd_res_k<<<std::min(B * H, res_cus[dev & 63]), 512, RES_LDS, st>>>(a);
+            return 0;
+        }
         if (!bias && p_drop == 0.f) {
             dim3 g2b(B * H * ((Tq + 127) / 128));
             if (causal) attn_bwd_dq64_k<true, false, false, 2, 2><<<g2b, 256, 32768, st>>>(a);

@@ -504,6 +504,36 @@ def test_attention_mfma_d(cuda, D, causal):
         _attn_check(2, T, 2, D, False, bias=torch.tril(torch.ones(T, T, device="cuda")).unsqueeze(0))
 
 
+@pytest.mark.parametrize("T,Tk", [(197, None), (33, None), (256, None), (150, 230), (230, 96)])
+def test_attention_resident_head(cuda, T, Tk):
+    """Whole-head-resident D = 64 kernels (Tq, Tk <= 256): the forward (8 waves, K / V staged once) and the
+    persistent backward (one workgroup per CU walking B·H heads, next head's tiles streamed during the
+    current head's phases) — B·H = 384 heads > the CU count, so workgroups carry several heads and the
+    cross-head pipelining (prefetched registers, tiles refilled between barriers) is exercised."""
+    torch.manual_seed(14)
+    _attn_check(32, T, 12, 64, False, Tk=Tk)
+
+
+def test_attention_resident_head_bias_grad(cuda):
+    """The resident backward's Σ_rows dQKV: Σ dV = Σ dO, Σ dK = 0, Σ dQ from the MFMA column sums of dS —
+    against Σ_rows of the returned dQKV over 384 heads (several per workgroup)."""
+    from replicann_amd.utils.flat import FlatParams
+    torch.manual_seed(15)
+    B, H, D, T = 32, 12, 64, 197
+    mod = torch.nn.Module()
+    mod.pb = torch.nn.Parameter(torch.zeros(3 * H * D, device="cuda").bfloat16())
+    flat = FlatParams(mod)
+    flat.zero_grad()
+    qkv = bf(B, T, 3, H, D).requires_grad_()
+    o = ops.attention_packed(qkv, causal=False, producer_bias=mod.pb)
+    o.backward(bf(B, T, H, D))
+    assert mod.pb._rn_bias_done
+    ref = qkv.grad.float().reshape(B * T, 3, H * D).sum(0)
+    got = mod.pb.grad.float().reshape(3, H * D)
+    assert rel_err(got[0], ref[0]) < 1e-2 and rel_err(got[2], ref[2]) < 1e-2
+    assert got[1].abs().max() < 1e-2 * ref[0].abs().max()  # Σ dK: zero in exact arithmetic
+
+
 @pytest.mark.parametrize("D", [32, 128])
 def test_attention_packed_qkv_bias_grad_d(cuda, D):
     """The in-kernel Σ_rows dQKV partials at head sizes 32 / 128."""
