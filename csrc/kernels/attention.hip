@@ -40,6 +40,8 @@ constexpr float LN2 = 0.6931471805599453f;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) const s16x8 lds_s16x8;
+typedef __attribute__((address_space(3))) const f32x4 lds_f32x4;
 
 struct AttnArgs {
     const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* bias;
@@ -1533,17 +1535,16 @@ __global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(Att
 // QKV bias partials (bsum): Σ_rows dV = Σ_q dO (softmax rows sum to 1), Σ_rows dK = 0 (a key bias shifts
 // all of a query's scores alike), Σ_rows dQ = scale · Σ_key (Σ_q dS[q][key]) K[key] with the column sums
 // of dS from a 1·dS MFMA in P1 — all written into the head's first 64-row block (the consumer sums them all).
-constexpr int RES_LDS = 4 * 32768 + 3 * 1024 + 2 * 8 * 64 * 4;  // tiles, lse | −δ | Σ_q dS, bias partials
+constexpr int RES_LDS = 4 * 32768 + 2 * 1024 + 2 * 8 * 64 * 4;  // tiles, lse | −δ, bias partials
 __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* const Qt = smem;
     char* const Dt = smem + 32768;
     char* const Kt = smem + 65536;
     char* const Vt = smem + 98304;
-    float* const lseL = reinterpret_cast<float*>(smem + 131072);  // [256] lse, log2 units (+inf past Tq)
+    float* const lseL = reinterpret_cast<float*>(smem + 131072);  // [256] −lse / (scale·log2 e) (−inf past Tq)
     float* const ndL = lseL + 256;                                 // [256] −δ
-    float* const csL = ndL + 256;                                  // [256] Σ_q dS[q][key]
-    float* const bpL = csL + 256;                                  // [2][8][64] bias partials: dQ, dV
+    float* const bpL = ndL + 256;                                  // [2][8][64] bias partials: dQ, dV
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const Frag32 fo = make_frag32(lane);
@@ -1559,7 +1560,8 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
     // registers of head bh: K / V rows w0 + r (P1's B operands), O rows w0 + r (δ), lse
     auto issue_regs = [&](int bh) {
         const int b = bh / p.H, hh = bh % p.H;
-        const int row = w0 + r;
+        int row = w0 + r;
+        asm volatile("" : "+v"(row));  // (as in issue_tiles)
         const bool kok = row < p.Tk, qok = row < p.Tq;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -1577,7 +1579,8 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int ins = wave + 8 * i;
-            const int row = ins * 8 + (lane >> 3);
+            int row = ins * 8 + (lane >> 3);
+            asm volatile("" : "+v"(row));  // recomputed per head: hoisted out of the head loop they were spilled
             const int cg = (lane & 7) ^ swz32(row);
             const bool ok = row < lim;
             dma16_async(rs0, ok ? (uint32_t)(((long)row * st0 + cg * 8) * 2) : 0xFFFFFFF0u, lds_addr(t0 + ins * 1024));
@@ -1597,6 +1600,22 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             *reinterpret_cast<const unsigned short*>(t + row * 128 + ((((d >> 3) ^ swz32(row)) << 4) | ((d & 7) << 1)));
         return __uint_as_float((uint32_t)u << 16);
     };
+
+    // LDS byte addresses held whole in one register (opaque to the compiler, which otherwise re-adds the
+    // >64 KiB tile bases — beyond ds_read's 16-bit offset — to every address in the loops); the block /
+    // tile / dO-V offsets then ride the instructions' immediates
+    auto la = [](const void* ptr, uint32_t off) -> uint32_t {
+        uint32_t x = (uint32_t)(uintptr_t)(lds_void*)ptr + off;
+        asm volatile("" : "+v"(x));
+        return x;
+    };
+    auto ld16 = [](uint32_t a) -> s16x8 { return *reinterpret_cast<const lds_s16x8*>((size_t)a); };
+    auto trd = [](uint32_t a0, uint32_t a1) -> s16x8 {  // a transposed fragment's two ds_read_b64_tr_b16
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)a0);
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)a1);
+        return (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    };
+    auto ldf4 = [](uint32_t a) -> f32x4 { return *reinterpret_cast<const lds_f32x4*>((size_t)a); };
 
     int bh = blockIdx.x;
     if (bh < BH) {
@@ -1622,7 +1641,7 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
         const float ndl = -swap_sum(dsum);  // −δ of query w0 + r (0 past Tq: zero rows)
         const float lse2 = lsel;
         if (h == 0) {
-            lseL[w0 + r] = lsel;
+            lseL[w0 + r] = -lsel / sl2;  // P1 starts its S accumulators here: P = exp2(acc · sl2)
             ndL[w0 + r] = ndl;
         }
         __syncthreads();  // B0: lse, −δ
@@ -1633,45 +1652,59 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             bpL[512 + wave * 64 + lane] = a;
         }
         // ---- P1: dK, dV of keys w0 .. w0+31 ----
-        f32x16 dk[2], dv[2], cs;
+        f32x16 dk[2], dv[2];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = cs[i] = 0.f; }
+        for (int i = 0; i < 16; ++i) { dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f; }
         if (w0 < p.Tk) {
+            // per-lane LDS pointers into the Q tile (dO: +32768, block X: +4096·X — immediates / one add each)
+            uint32_t qr[4], qc[2][2];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) qr[s] = la(Qt, fo.rf[s]);
+#pragma unroll
+            for (int jd = 0; jd < 2; ++jd) {
+                qc[jd][0] = la(Qt, fo.cf[jd][0]);
+                qc[jd][1] = la(Qt, fo.cf[jd][1]);
+            }
+            const uint32_t nda = la(ndL, 16 * h), lsa = la(lseL, 16 * h);
+            s16x8 qa[4], da[4];
 #pragma unroll 1
             for (int X = 0; X < nqb; ++X) {
+                const int xo = X * 4096;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    qa[s] = ld16(qr[s] + xo);
+                    da[s] = ld16(qr[s] + xo + 32768);
+                }
                 f32x16 sa, dp;
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4) {
-                    const f32x4 nd = *reinterpret_cast<const f32x4*>(ndL + 32 * X + 8 * c4 + 4 * h);
+                    const f32x4 nd = ldf4(nda + 128 * X + 32 * c4);
+                    const f32x4 nl = ldf4(lsa + 128 * X + 32 * c4);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) { dp[4 * c4 + e] = nd[e]; sa[4 * c4 + e] = 0.f; }
+                    for (int e = 0; e < 4; ++e) { dp[4 * c4 + e] = nd[e]; sa[4 * c4 + e] = nl[e]; }
                 }
 #pragma unroll
-                for (int s = 0; s < 4; ++s) sa = MFMA32(rfrag32(Qt, X, s, fo), kf[s], sa, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) sa = MFMA32(qa[s], kf[s], sa, 0, 0, 0);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) dp = MFMA32(rfrag32(Dt, X, s, fo), vf[s], dp, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) dp = MFMA32(da[s], vf[s], dp, 0, 0, 0);
 #pragma unroll
-                for (int c4 = 0; c4 < 4; ++c4) {
-                    const f32x4 l4 = *reinterpret_cast<const f32x4*>(lseL + 32 * X + 8 * c4 + 4 * h);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int i = 4 * c4 + e;
-                        sa[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], sl2, -l4[e]));  // P
-                        dp[i] *= sa[i];                                                      // dS
-                    }
+                for (int i = 0; i < 16; ++i) {
+                    sa[i] = __builtin_amdgcn_exp2f(sa[i] * sl2);  // P
+                    dp[i] *= sa[i];                               // dS
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const s16x8 pb = pack16(sa, s2);
+                    const int o = xo + s2 * 2048 + 32768;
 #pragma unroll
-                    for (int jd = 0; jd < 2; ++jd) dv[jd] = MFMA32(tfrag32(Dt, 2 * X + s2, jd, fo), pb, dv[jd], 0, 0, 0);
+                    for (int jd = 0; jd < 2; ++jd) dv[jd] = MFMA32(trd(qc[jd][0] + o, qc[jd][1] + o), pb, dv[jd], 0, 0, 0);
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const s16x8 db = pack16(dp, s2);
+                    const int o = xo + s2 * 2048;
 #pragma unroll
-                    for (int jd = 0; jd < 2; ++jd) dk[jd] = MFMA32(tfrag32(Qt, 2 * X + s2, jd, fo), db, dk[jd], 0, 0, 0);
-                    if (p.bsum) cs = MFMA32(ones, db, cs, 0, 0, 0);
+                    for (int jd = 0; jd < 2; ++jd) dk[jd] = MFMA32(trd(qc[jd][0] + o, qc[jd][1] + o), db, dk[jd], 0, 0, 0);
                 }
             }
         }
@@ -1683,7 +1716,6 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             df[s] = rfrag32(Dt, wave, s, fo);
         }
         vm_wait_all();  // this head's K / V tiles (issued before A)
-        if (h == 0) csL[w0 + r] = cs[0];
         if (w0 + r < p.Tk) {
             float dummy = 0.f;
             store_rows32(dk, p.scale, p.dk + b * p.dk_sb + (long)(w0 + r) * p.dk_st + hh * p.dk_sh, nullptr, true, 0.f,
@@ -1696,26 +1728,35 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             issue_qdo(nxt);
             issue_regs(nxt);
         }
-        if (p.bsum) {  // Σ_key (Σ_q dS[q][key]) K[key][d] over this wave's 32 keys (rows past Tk are zero)
-            float a = 0.f;
-#pragma unroll 8
-            for (int i = 0; i < 32; ++i) a += csL[w0 + i] * tile_at(Kt, w0 + i, lane);
-            bpL[wave * 64 + lane] = a;
-        }
         // ---- P2: dQ of queries w0 .. w0+31 ----
         f32x16 dq[2];
 #pragma unroll
         for (int i = 0; i < 16; ++i) { dq[0][i] = dq[1][i] = 0.f; }
         if (w0 < p.Tq) {
+            uint32_t kr[4], kc[2][2];  // per-lane addresses in the K tile (V: +32768)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) kr[s] = la(Kt, fo.rf[s]);
+#pragma unroll
+            for (int jd = 0; jd < 2; ++jd) {
+                kc[jd][0] = la(Kt, fo.cf[jd][0]);
+                kc[jd][1] = la(Kt, fo.cf[jd][1]);
+            }
+            s16x8 ka[4], va[4];
 #pragma unroll 1
             for (int kb = 0; kb < nkb; ++kb) {
+                const int ko = kb * 4096;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    ka[s] = ld16(kr[s] + ko);
+                    va[s] = ld16(kr[s] + ko + 32768);
+                }
                 f32x16 sa, dp;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) { sa[i] = 0.f; dp[i] = ndl; }
 #pragma unroll
-                for (int s = 0; s < 4; ++s) sa = MFMA32(rfrag32(Kt, kb, s, fo), qf[s], sa, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) sa = MFMA32(ka[s], qf[s], sa, 0, 0, 0);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) dp = MFMA32(rfrag32(Vt, kb, s, fo), df[s], dp, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) dp = MFMA32(va[s], df[s], dp, 0, 0, 0);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) sa[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], sl2, -lse2));
                 if (32 * kb + 32 > p.Tk) {  // the ragged key block (wave-uniform)
@@ -1728,8 +1769,9 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const s16x8 db = pack16(dp, s2);
+                    const int o = ko + s2 * 2048;
 #pragma unroll
-                    for (int jd = 0; jd < 2; ++jd) dq[jd] = MFMA32(tfrag32(Kt, 2 * kb + s2, jd, fo), db, dq[jd], 0, 0, 0);
+                    for (int jd = 0; jd < 2; ++jd) dq[jd] = MFMA32(trd(kc[jd][0] + o, kc[jd][1] + o), db, dq[jd], 0, 0, 0);
                 }
             }
         }
@@ -1738,29 +1780,50 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             store_rows32(dq, p.scale, p.dq + b * p.dq_sb + (long)(w0 + r) * p.dq_st + hh * p.dq_sh, nullptr, true, 0.f,
                          dummy, h);
         }
-        __syncthreads();  // B2: K / V tiles free, bias partials complete
-        if (p.bsum && threadIdx.x < 128) {
-            const int part = threadIdx.x >> 6, d = lane;  // 0: dQ (and dK), 1: dV
-            float a = 0.f;
+        __syncthreads();  // B2: K / V tiles free, dV bias partials complete
+        if (p.bsum) {
+            // Σ_q dQ[q][d]: every wave's dQ^T (unscaled) through the free K / V region, [32 q][64 d] per wave with
+            // the column rotated by the row (conflict-free writes and column reads)
+            float* const red = reinterpret_cast<float*>(Kt);
 #pragma unroll
-            for (int w = 0; w < 8; ++w) a += bpL[part * 512 + w * 64 + d];
-            const int nb64 = (p.Tq + 63) / 64;
-            float* row = p.bsum + (long)b * nb64 * 3 * E + hh * 64 + d;
-            if (part == 0) {
-                row[0] = a * p.scale;
-                row[E] = 0.f;
-            } else {
-                row[2 * E] = a;
+            for (int jd = 0; jd < 2; ++jd)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int d = 32 * jd + arow(i, h);
+                    red[wave * 2048 + r * 64 + ((d + r) & 63)] = (w0 + r < p.Tq) ? dq[jd][i] : 0.f;
+                }
+            __syncthreads();
+            {
+                float a = 0.f;
+#pragma unroll 8
+                for (int i = 0; i < 32; ++i) a += red[wave * 2048 + i * 64 + ((lane + i) & 63)];
+                bpL[wave * 64 + lane] = a;
             }
-            for (int blk = 1; blk < nb64; ++blk) {
-                float* z = row + (long)blk * 3 * E;
+            __syncthreads();
+            if (threadIdx.x < 128) {
+                const int part = threadIdx.x >> 6, d = lane;  // 0: dQ (and dK), 1: dV
+                float a = 0.f;
+#pragma unroll
+                for (int w = 0; w < 8; ++w) a += bpL[part * 512 + w * 64 + d];
+                const int nb64 = (p.Tq + 63) / 64;
+                float* row = p.bsum + (long)b * nb64 * 3 * E + hh * 64 + d;
                 if (part == 0) {
-                    z[0] = 0.f;
-                    z[E] = 0.f;
+                    row[0] = a * p.scale;
+                    row[E] = 0.f;
                 } else {
-                    z[2 * E] = 0.f;
+                    row[2 * E] = a;
+                }
+                for (int blk = 1; blk < nb64; ++blk) {
+                    float* z = row + (long)blk * 3 * E;
+                    if (part == 0) {
+                        z[0] = 0.f;
+                        z[E] = 0.f;
+                    } else {
+                        z[2 * E] = 0.f;
+                    }
                 }
             }
+            __syncthreads();  // the K / V region is refilled next
         }
         if (nxt < BH) issue_kv(nxt);
     }
