@@ -1687,6 +1687,17 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
                 for (int s = 0; s < 4; ++s) sa = MFMA32(qa[s], kf[s], sa, 0, 0, 0);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) dp = MFMA32(da[s], vf[s], dp, 0, 0, 0);
+                // dO^T / Q^T fragments of the dV / dK products read now: their latency hides under the softmax VALU
+                s16x8 to[2][2], tq[2][2];
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                    for (int jd = 0; jd < 2; ++jd) {
+                        const int o = xo + s2 * 2048;
+                        to[s2][jd] = trd(qc[jd][0] + o + 32768, qc[jd][1] + o + 32768);
+                        tq[s2][jd] = trd(qc[jd][0] + o, qc[jd][1] + o);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     sa[i] = __builtin_amdgcn_exp2f(sa[i] * sl2);  // P
@@ -1695,16 +1706,14 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const s16x8 pb = pack16(sa, s2);
-                    const int o = xo + s2 * 2048 + 32768;
 #pragma unroll
-                    for (int jd = 0; jd < 2; ++jd) dv[jd] = MFMA32(trd(qc[jd][0] + o, qc[jd][1] + o), pb, dv[jd], 0, 0, 0);
+                    for (int jd = 0; jd < 2; ++jd) dv[jd] = MFMA32(to[s2][jd], pb, dv[jd], 0, 0, 0);
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const s16x8 db = pack16(dp, s2);
-                    const int o = xo + s2 * 2048;
 #pragma unroll
-                    for (int jd = 0; jd < 2; ++jd) dk[jd] = MFMA32(trd(qc[jd][0] + o, qc[jd][1] + o), db, dk[jd], 0, 0, 0);
+                    for (int jd = 0; jd < 2; ++jd) dk[jd] = MFMA32(tq[s2][jd], db, dk[jd], 0, 0, 0);
                 }
             }
         }
@@ -1757,6 +1766,9 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
                 for (int s = 0; s < 4; ++s) sa = MFMA32(ka[s], qf[s], sa, 0, 0, 0);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) dp = MFMA32(va[s], df[s], dp, 0, 0, 0);
+                // both chains issued before the softmax VALU (which then overlaps the dP chain); left alone the
+                // scheduler put the dP MFMAs after the exps, exposing both chains' latency
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) sa[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], sl2, -lse2));
                 if (32 * kb + 32 > p.Tk) {  // the ragged key block (wave-uniform)
