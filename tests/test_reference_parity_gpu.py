@@ -71,8 +71,12 @@ def test_cross_decoder_gpu_vs_reference(cuda, fx):
     _, k, v = enc(src.cuda().to(torch.bfloat16), return_kv=True)
     y, (gt, gk, gv) = _fwd_bwd(dec, tgt, k, v, gseed=504)
     assert rel(y, ref["y"]) < 2e-2
+    # input gradients through a bf16 cross decoder (self + cross attention, MLP, three LayerNorms): 0.0300 /
+    # 0.0299 / 0.0280 with the round-5 attention kernels, 0.0304 / 0.0303 / 0.0282 with the whole-head-resident
+    # ones, whose own errors against a float64 reference are those of the kernels they replace within 5 %
+    # (scripts/dev/attn_err.py, profiles/attention_resident_r6.txt): the bound had no margin, not the kernels
     for a, b in ((gt, ref["g_tgt"]), (gk, ref["g_k"]), (gv, ref["g_v"])):
-        assert rel(a, b) < 3e-2
+        assert rel(a, b) < 3.5e-2
 
 
 def test_fixture_matches_live_reference(ref, fx):
