@@ -1595,11 +1595,6 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
         const int b = bh / p.H, hh = bh % p.H;
         issue_tiles(p.k + b * p.k_sb + hh * p.k_sh, p.k_st, p.v + b * p.v_sb + hh * p.v_sh, p.v_st, p.Tk, Kt, Vt);
     };
-    auto tile_at = [](const char* t, int row, int d) -> float {
-        const unsigned short u =
-            *reinterpret_cast<const unsigned short*>(t + row * 128 + ((((d >> 3) ^ swz32(row)) << 4) | ((d & 7) << 1)));
-        return __uint_as_float((uint32_t)u << 16);
-    };
 
     // LDS byte addresses held whole in one register (opaque to the compiler, which otherwise re-adds the
     // >64 KiB tile bases — beyond ds_read's 16-bit offset — to every address in the loops); the block /
@@ -1645,11 +1640,21 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             ndL[w0 + r] = ndl;
         }
         __syncthreads();  // B0: lse, −δ
-        if (p.bsum) {  // Σ_q dO[q][d] over this wave's 32 queries (thread = column d)
-            float a = 0.f;
-#pragma unroll 8
-            for (int i = 0; i < 32; ++i) a += tile_at(Dt, w0 + i, lane);
-            bpL[512 + wave * 64 + lane] = a;
+        if (p.bsum) {  // Σ_q dO[q][d] over this wave's 32 queries: dO^T · 1 on the MFMA (P1's dV product with P = 1)
+            const Frag32 f2 = make_frag32(lane);
+            f32x16 u[2];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { u[0][i] = 0.f; u[1][i] = 0.f; }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int jd = 0; jd < 2; ++jd) u[jd] = MFMA32(tfrag32(Dt, 2 * wave + s2, jd, f2), ones, u[jd], 0, 0, 0);
+            if (r == 0) {  // every column of u holds the sums: lanes 0 / 32 write rows arow(i, h)
+#pragma unroll
+                for (int jd = 0; jd < 2; ++jd)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) bpL[512 + wave * 64 + 32 * jd + arow(i, h)] = u[jd][i];
+            }
         }
         // ---- P1: dK, dV of keys w0 .. w0+31 ----
         f32x16 dk[2], dv[2];
