@@ -1522,9 +1522,9 @@ __global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(Att
 // block, the dK/dV kernel Q / dO per 128-key block, and δ makes a round trip.  Here one persistent 8-wave
 // workgroup per CU walks the heads; a head's Q, dO, K, V tiles sit in LDS (128 KiB) and every operand is read
 // from HBM once:
-//   A   δ of the wave's 32 queries from O / dO rows in registers; lse, −δ -> LDS      (barrier B0)
-//   P1  wave w owns keys [32w, 32w+32): K / V rows in registers (prefetched), loops over every query
-//       block from the Q / dO tiles: S, dP, P, dS; dV^T += dO^T P, dK^T += Q^T dS   (barrier B1)
+//   A   δ of the wave's 32 queries (O rows in registers · dO rows of the tile); lse, −δ -> LDS   (barrier B0)
+//   P1  wave w owns keys [32w, 32w+32): K / V rows in registers (loaded at the end of the previous head),
+//       loops over every query block of the Q / dO tiles: S, dP, P, dS; dV^T += dO^T P, dK^T += Q^T dS (B1)
 //       -> the Q / dO tiles of the NEXT head stream in during P2
 //   P2  wave w owns queries [32w, 32w+32): loops over every key block from the K / V tiles:
 //       S^T, dP^T, dS^T; dQ^T += K^T dS^T                                             (barrier B2)
@@ -1532,9 +1532,9 @@ __global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(Att
 // The 32×32×16 orientation and fragment helpers are the forward's (accumulator column = the row that
 // owns the result, reduced index in registers).  Rows past Tq / Tk are zero-filled by the DMA and lse = +inf
 // there, so only the ragged key block of P2 needs a mask.
-// QKV bias partials (bsum): Σ_rows dV = Σ_q dO (softmax rows sum to 1), Σ_rows dK = 0 (a key bias shifts
-// all of a query's scores alike), Σ_rows dQ = scale · Σ_key (Σ_q dS[q][key]) K[key] with the column sums
-// of dS from a 1·dS MFMA in P1 — all written into the head's first 64-row block (the consumer sums them all).
+// QKV bias partials (bsum): Σ_rows dV = Σ_q dO (softmax rows sum to 1; dO^T·1 on the MFMA), Σ_rows dK = 0 (a key
+// bias shifts all of a query's scores alike), Σ_rows dQ by a column reduction of the waves' dQ^T through the
+// freed K / V region — all written into the head's first 64-row block (the consumer sums every block).
 constexpr int RES_LDS = 4 * 32768 + 2 * 1024 + 2 * 8 * 64 * 4;  // tiles, lse | −δ, bias partials
 __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
