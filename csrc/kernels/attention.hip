@@ -1354,20 +1354,22 @@ RN_DEV void store_rows32(const f32x16 (&x)[2], float mul, bf16* dst, uint8_t* q8
 // (staged once, 64 KiB, no barrier inside the key loop): K / V are read from HBM once per head instead
 // of once per 128-query block.  At ViT-B/16's T = 197 the streaming kernel reads K and V twice and
 // the forward is HBM-bound (Q + 2K + 2V + O per layer).
+// W8 (streaming, round 6): 8 waves × 32 queries per workgroup instead of 4: every staged K / V tile serves 256
+// queries, so a causal head fetches its K / V tiles 40 times instead of 72 (T = 1024).
 constexpr int RES_T = 256;
-template <bool CAUSAL, bool RES = false>
-__global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(AttnArgs p) {
+template <bool CAUSAL, bool RES = false, bool W8 = false>
+__global__ void __launch_bounds__(RES || W8 ? 512 : 256, RES || W8 ? 4 : 2) attn_fwd32_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const Frag32 fo = make_frag32(lane);
-    constexpr int QB = RES ? RES_T : 128;  // queries per workgroup
+    constexpr int QB = RES || W8 ? 256 : 128;  // queries per workgroup
     int bh, qb;
     if constexpr (RES) {
         bh = blockIdx.x;
         qb = 0;
     } else {
-        blk_map(p, (p.Tq + 127) / 128, CAUSAL, bh, qb);
+        blk_map(p, (p.Tq + QB - 1) / QB, CAUSAL, bh, qb);
     }
     const int b = bh / p.H, hh = bh % p.H;
     const int q0 = qb * QB + wave * 32;  // this wave's first query
@@ -1386,6 +1388,21 @@ __global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(Att
     // streaming: double-buffered [K 64 rows | V 64 rows] pairs; RES: K rows [0, 256) then V rows [0, 256)
 #define Kt(i) (RES ? smem + (i) * 8192 : smem + ((i) & 1) * 16384)
 #define Vt(i) (RES ? smem + 32768 + (i) * 8192 : smem + 8192 + ((i) & 1) * 16384)
+    // one 64-row K tile and V tile (streaming): 4 waves issue 2 pieces of each, 8 waves 1
+    auto stage_kv = [&](int t) {
+        if constexpr (W8) {
+            const int row = wave * 8 + (lane >> 3);
+            const int cg = (lane & 7) ^ swz32(row);
+            const bool ok = t * 64 + row < p.Tk;
+            dma16_async(krs, ok ? (uint32_t)((((long)(t * 64 + row)) * p.k_st + cg * 8) * 2) : 0xFFFFFFF0u,
+                        lds_addr(Kt(t) + wave * 1024));
+            dma16_async(vrs, ok ? (uint32_t)((((long)(t * 64 + row)) * p.v_st + cg * 8) * 2) : 0xFFFFFFF0u,
+                        lds_addr(Vt(t) + wave * 1024));
+        } else {
+            stage32_async(krs, p.k_st, t * 64, p.Tk, Kt(t), wave, lane);
+            stage32_async(vrs, p.v_st, t * 64, p.Tk, Vt(t), wave, lane);
+        }
+    };
     if constexpr (RES) {
         // every 8-row piece of the nkv tiles (rows past Tk read as zeros: V's padding rows must be finite)
         for (int ins = wave; ins < nkv * 8; ins += 8) {
@@ -1397,8 +1414,7 @@ __global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(Att
                         lds_addr(smem + 32768 + ins * 1024));
         }
     } else if (nkv > 0) {
-        stage32_async(krs, p.k_st, 0, p.Tk, Kt(0), wave, lane);
-        stage32_async(vrs, p.v_st, 0, p.Tk, Vt(0), wave, lane);
+        stage_kv(0);
     }
     s16x8 qf[4];
 #pragma unroll
@@ -1489,10 +1505,7 @@ __global__ void __launch_bounds__(RES ? 512 : 256, RES ? 4 : 2) attn_fwd32_k(Att
         }
         vm_wait_all();
         __syncthreads();
-        if (t + 1 < nkv) {
-            stage32_async(krs, p.k_st, (t + 1) * 64, p.Tk, Kt(t + 1), wave, lane);
-            stage32_async(vrs, p.v_st, (t + 1) * 64, p.Tk, Vt(t + 1), wave, lane);
-        }
+        if (t + 1 < nkv) stage_kv(t + 1);
     };
     const int nf = q0 < p.Tq ? nfull : 0;
     int t = 0;
@@ -2091,7 +2104,7 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
             if (causal) attn_fwd32_k<true, true><<<dim3(B * H), 512, 65536, st>>>(a);
             else attn_fwd32_k<false, true><<<dim3(B * H), 512, 65536, st>>>(a);
         } else if (!bias && p_drop == 0.f && causal) {
-            attn_fwd32_k<true><<<grid, 256, 32768, st>>>(a);
+            attn_fwd32_k<true, false, true><<<dim3(B * H * ((Tq + 255) / 256)), 512, 32768, st>>>(a);
         } else if (!bias && p_drop == 0.f) {
             attn_fwd64v2_k<false, 3, true><<<grid, 256, 32768, st>>>(a);
         } else {
