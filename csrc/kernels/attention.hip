@@ -2095,10 +2095,11 @@ int rn_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
         else attn_fwd_mfma<128>(a, st);
     } else if (fast) {
         dim3 grid(B * H * ((Tq + 127) / 128));
-        // plain causal / non-causal: the split-loop v2 kernel with the LEAN softmax bookkeeping
-        // (3 blocks per CU); additive bias or dropout (the reference blocks): the single-loop kernel
-        // plain causal: the 32×32×16 kernel (GPT-2-small b64: 0.187 -> 0.179 ms per layer); plain non-causal: the
-        // 16×16×32 split-loop kernel (ViT-B/16 T = 197: 0.205 ms vs 0.212 for the 32×32 one) — profiles/attention_r6.txt
+        // plain, Tq / Tk <= 256: the whole-head-resident 32×32×16 kernel (ViT-B/16 T = 197: 0.205 -> 0.165 ms per
+        // layer, profiles/attention_resident_r6.txt); plain causal: the 32×32×16 kernel with 8 waves (256 queries) per
+        // workgroup (GPT-2-small b64: 0.187 -> 0.179 -> 0.170 ms per layer, profiles/attention_r6.txt,
+        // attention_memtraffic_r6.txt); plain non-causal: the 16×16×32 split-loop v2 kernel; additive bias or
+        // dropout (the reference blocks): the single-loop kernel
         if (!bias && p_drop == 0.f && Tq <= RES_T && Tk <= RES_T) {
             // whole head resident (ViT-B/16, T = 197): one 8-wave workgroup per (b, h)
             if (causal) attn_fwd32_k<true, true><<<dim3(B * H), 512, 65536, st>>>(a);
