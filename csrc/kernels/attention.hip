@@ -25,8 +25,10 @@
 //     per 64 keys, loops over queries): no atomics, bitwise deterministic.
 // D = 64 has extra tuned variants (split-loop forward with MFMA row sums, two query / key
 // groups per wave in the backward); D = 32 / 128 use the single-loop forward and one group.
-// Generic path (odd head sizes ≤ 256 only): per-query-row kernels with fp32 scores in LDS
-// and fp32 atomics for dK/dV (not bitwise deterministic).
+// Generic path (odd head sizes ≤ 256 only): per-query-row kernels with fp32 scores in LDS; the
+// backward is dQ per query row, then dK/dV per key row (no atomics).
+// Round 6 (D = 64): the 32×32×16 forward (causal: 8 waves / 256 queries per workgroup), and for
+// Tq, Tk ≤ 256 whole-head-resident forward / backward kernels (docs/DESIGN.md §4 has the selection table).
 #include "common.h"
 
 #include <algorithm>
