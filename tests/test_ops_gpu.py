@@ -504,7 +504,7 @@ def test_attention_mfma_d(cuda, D, causal):
         _attn_check(2, T, 2, D, False, bias=torch.tril(torch.ones(T, T, device="cuda")).unsqueeze(0))
 
 
-@pytest.mark.parametrize("T,Tk", [(197, None), (33, None), (256, None), (150, 230), (230, 96)])
+@pytest.mark.parametrize("T,Tk", [(197, None), (33, None), (256, None), (150, 230), (230, 96), (5, 3)])
 def test_attention_resident_head(cuda, T, Tk):
     """Whole-head-resident D = 64 kernels (Tq, Tk <= 256): the forward (8 waves, K / V staged once) and the
     persistent backward (one workgroup per CU walking B·H heads, next head's tiles streamed during the
@@ -512,6 +512,27 @@ def test_attention_resident_head(cuda, T, Tk):
     cross-head pipelining (prefetched registers, tiles refilled between barriers) is exercised."""
     torch.manual_seed(14)
     _attn_check(32, T, 12, 64, False, Tk=Tk)
+
+
+def test_attention_resident_single_token(cuda):
+    """T = 1 through the resident kernels: softmax over one key is exactly 1, so O = V, dV = dO and dQ = dK = 0
+    in exact arithmetic (a relative error against that zero reference is meaningless: absolute bounds)."""
+    torch.manual_seed(17)
+    B, H = 8, 12
+    q, k, v, go = (bf(B, 1, H, 64) for _ in range(4))
+    qg, kg, vg = [t.clone().requires_grad_() for t in (q, k, v)]
+    o = ops.attention(qg, kg, vg, scale=0.125, causal=False)
+    o.backward(go)
+    assert rel_err(o, v) < 1e-2 and rel_err(vg.grad, go) < 1e-2
+    assert qg.grad.float().abs().max() < 1e-4 and kg.grad.float().abs().max() < 1e-4
+
+
+@pytest.mark.parametrize("T,Tk", [(100, 200), (64, 64), (250, 256)])
+def test_attention_resident_forward_causal(cuda, T, Tk):
+    """The resident forward's causal form (Tq, Tk <= 256, incl. Tq < Tk: the causal offset) against the fp32
+    reference; its backward is the streaming pair."""
+    torch.manual_seed(16)
+    _attn_check(4, T, 6, 64, True, Tk=Tk)
 
 
 def test_attention_resident_head_bias_grad(cuda):
