@@ -1548,8 +1548,8 @@ __global__ void __launch_bounds__(RES || W8 ? 512 : 256, RES || W8 ? 4 : 2) attn
 // owns the result, reduced index in registers).  Rows past Tq / Tk are zero-filled by the DMA and lse = +inf
 // there, so only the ragged key block of P2 needs a mask.
 // QKV bias partials (bsum): Σ_rows dV = Σ_q dO (softmax rows sum to 1; dO^T·1 on the MFMA), Σ_rows dK = 0 (a key
-// bias shifts all of a query's scores alike), Σ_rows dQ by a column reduction of the waves' dQ^T through the
-// freed K / V region — all written into the head's first 64-row block (the consumer sums every block).
+// bias shifts all of a query's scores alike), Σ_rows dQ by an in-register reduce-scatter of each wave's dQ^T —
+// all written into the head's first 64-row block (the consumer sums every block).
 constexpr int RES_LDS = 4 * 32768 + 2 * 1024 + 2 * 8 * 64 * 4;  // tiles, lse | −δ, bias partials
 __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1812,50 +1812,49 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_res_k(AttnArgs p) {
             store_rows32(dq, p.scale, p.dq + b * p.dq_sb + (long)(w0 + r) * p.dq_st + hh * p.dq_sh, nullptr, true, 0.f,
                          dummy, h);
         }
-        __syncthreads();  // B2: K / V tiles free, dV bias partials complete
         if (p.bsum) {
-            // Σ_q dQ[q][d]: every wave's dQ^T (unscaled) through the free K / V region, [32 q][64 d] per wave with
-            // the column rotated by the row (conflict-free writes and column reads)
-            float* const red = reinterpret_cast<float*>(Kt);
+            // Σ_q dQ[q][d] over this wave's 32 queries: a reduce-scatter of the dQ^T accumulator across the 32
+            // lanes of each half (5 levels of XOR partners; at each, a lane keeps the half of its values its
+            // lane bit selects and adds the partner's copy of them), so lane r ends with value v = r: d = 32·(r>>4)
+            // + arow(r & 15, h).  Rows past Tq hold zeros (P = 0 there).  No LDS round trip, no extra barrier.
+            float cur[32];
 #pragma unroll
-            for (int jd = 0; jd < 2; ++jd)
+            for (int v = 0; v < 32; ++v) cur[v] = dq[v >> 4][v & 15];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int d = 32 * jd + arow(i, h);
-                    red[wave * 2048 + r * 64 + ((d + r) & 63)] = (w0 + r < p.Tq) ? dq[jd][i] : 0.f;
+            for (int m = 16; m >= 1; m >>= 1) {
+                const bool hi = (r & m) != 0;
+#pragma unroll
+                for (int k = 0; k < m; ++k) {
+                    const float keep = hi ? cur[k + m] : cur[k];
+                    const float send = hi ? cur[k] : cur[k + m];
+                    cur[k] = keep + __shfl_xor(send, m, 64);
                 }
-            __syncthreads();
-            {
-                float a = 0.f;
-#pragma unroll 8
-                for (int i = 0; i < 32; ++i) a += red[wave * 2048 + i * 64 + ((lane + i) & 63)];
-                bpL[wave * 64 + lane] = a;
             }
-            __syncthreads();
-            if (threadIdx.x < 128) {
-                const int part = threadIdx.x >> 6, d = lane;  // 0: dQ (and dK), 1: dV
-                float a = 0.f;
+            bpL[wave * 64 + 32 * (r >> 4) + arow(r & 15, h)] = cur[0];
+        }
+        __syncthreads();  // B2: K / V tiles free, bias partials complete
+        if (p.bsum && threadIdx.x < 128) {
+            const int part = threadIdx.x >> 6, d = lane;  // 0: dQ (and dK), 1: dV
+            float a = 0.f;
 #pragma unroll
-                for (int w = 0; w < 8; ++w) a += bpL[part * 512 + w * 64 + d];
-                const int nb64 = (p.Tq + 63) / 64;
-                float* row = p.bsum + (long)b * nb64 * 3 * E + hh * 64 + d;
+            for (int w = 0; w < 8; ++w) a += bpL[part * 512 + w * 64 + d];
+            const int nb64 = (p.Tq + 63) / 64;
+            float* row = p.bsum + (long)b * nb64 * 3 * E + hh * 64 + d;
+            if (part == 0) {
+                row[0] = a * p.scale;
+                row[E] = 0.f;
+            } else {
+                row[2 * E] = a;
+            }
+            for (int blk = 1; blk < nb64; ++blk) {
+                float* z = row + (long)blk * 3 * E;
                 if (part == 0) {
-                    row[0] = a * p.scale;
-                    row[E] = 0.f;
+                    z[0] = 0.f;
+                    z[E] = 0.f;
                 } else {
-                    row[2 * E] = a;
-                }
-                for (int blk = 1; blk < nb64; ++blk) {
-                    float* z = row + (long)blk * 3 * E;
-                    if (part == 0) {
-                        z[0] = 0.f;
-                        z[E] = 0.f;
-                    } else {
-                        z[2 * E] = 0.f;
-                    }
+                    z[2 * E] = 0.f;
                 }
             }
-            __syncthreads();  // the K / V region is refilled next
         }
         if (nxt < BH) issue_kv(nxt);
     }

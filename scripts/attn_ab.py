@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--D", type=int, default=64, help="head size (H = 768 // D keeps E = 768)")
     ap.add_argument("--noncausal", action="store_true")
     ap.add_argument("--T", type=int, default=1024, help="sequence length (ViT-B/16: 197, non-causal)")
+    ap.add_argument("--bias-grad", action="store_true",
+                    help="the packed QKV projection's bias gradient from the backward kernels (producer_bias)")
     a = ap.parse_args()
     B, T, D = a.B, a.T, a.D
     H = 768 // D
@@ -44,7 +46,15 @@ def main():
     qkv = torch.randn(B, T, 3, H, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
     go = torch.randn(B, T, H, D, device="cuda", dtype=torch.bfloat16)
     fl_f = 4 * B * H * T * T * D / (1 if a.noncausal else 2)
-    fwd = lambda: ops.attention_packed(qkv, causal=not a.noncausal)
+    pb = None
+    if a.bias_grad:  # the bias must live in a flat gradient buffer for the in-kernel partials
+        from replicann_amd.utils.flat import FlatParams
+        mod = torch.nn.Module()
+        mod.pb = torch.nn.Parameter(torch.zeros(3 * H * D, device="cuda").bfloat16())
+        flat = FlatParams(mod)
+        flat.zero_grad()
+        pb = mod.pb
+    fwd = lambda: ops.attention_packed(qkv, causal=not a.noncausal, producer_bias=pb)
     out = fwd()
     bwd = lambda: torch.autograd.grad(out, qkv, go, retain_graph=True)[0]
     res = {"fwd": [], "bwd": []}
@@ -56,7 +66,8 @@ def main():
     for ps, lst in res.items():
         ms = min(lst)
         fl = fl_f if ps == "fwd" else 2.5 * fl_f
-        print(json.dumps(dict(op=f"attn_{ps}", B=B, H=H, T=T, D=D, causal=not a.noncausal, ms=round(ms, 4),
+        print(json.dumps(dict(op=f"attn_{ps}", B=B, H=H, T=T, D=D, causal=not a.noncausal, bias_grad=a.bias_grad,
+                              ms=round(ms, 4),
                               tflops=round(fl / ms / 1e9, 1), all_ms=[round(x, 4) for x in lst],
                               abs_sum=sums[ps])), flush=True)
 
